@@ -1,0 +1,205 @@
+"""Benchmark: multi-source SSSP path-table rows on MI355X (BASELINE.json metric
+"SSSP sources/sec + full path-table time, % HBM roofline, at 1/2/4/8 GPU").
+
+Workload (default, config C3 of BASELINE.json / SURVEY.md §8d): synthetic
+Barabasi-Albert n=50,000, m=3, seed 3, latency U(1,100) ms, loss U(0,0.01),
+every vertex attached (A = 50,000 sources x 50,000 targets).  A step = one batch
+of `--blocks-per-step` 64-source blocks: full rows (latency, reliability, next
+hop, hops) written into the HBM-resident table.  Ranks take disjoint source
+blocks (weak scaling: fixed rows per GPU per step, no collective on the data
+path).  Rank 0 prints one JSON line.
+
+Run: python bench.py [--gpus N --steps K --warmup W]
+     torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "SSSP sources/sec + full path-table time, % HBM roofline, at 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def workload(name: str):
+    from shadow_amd import graphs
+    if name == "c3":
+        top = graphs.gen_ba(50000, 3, 3)
+        att = np.arange(top.n, dtype=np.int32)
+        desc = "C3: Barabasi-Albert n=50000 m=3 seed=3, latency U(1,100), A=50000 (all vertices)"
+    elif name == "c4":
+        top = graphs.gen_tiered()
+        att = graphs.tiered_attached(top)
+        desc = "C4: tiered BA core 20k + 180k stubs, A=100000 stubs"
+    elif name == "c2":
+        top = graphs.gen_rgg(10000, 2)
+        att = np.arange(top.n, dtype=np.int32)
+        desc = "C2: random geometric graph n=10000 seed=2, A=all"
+    else:
+        raise SystemExit(f"unknown config {name}")
+    return top, att, desc
+
+
+def cpu_baseline(top, att, seconds: float, seed: int = 6):
+    """Oracle (C restatement of igraph Dijkstra + Shadow row rules, -O2, 1 core)
+    timed on a bounded sample of this workload's sources."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    o = Oracle(top)
+    rng = np.random.default_rng(seed)
+    order = rng.permutation(att.shape[0])
+    done, t0, dj = 0, time.perf_counter(), 0.0
+    chunk = 8
+    while time.perf_counter() - t0 < seconds and done < att.shape[0]:
+        src = att[order[done:done + chunk]]
+        r = o.rows(src, att, nthreads=1, want_dijkstra_time=True)
+        dj += r["dijkstra_seconds"]
+        done += src.shape[0]
+    el = time.perf_counter() - t0
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": done / el, "unit": "sources/s", "cores": 1, "kind": "port",
+            "sample": f"{done} seeded-random sources (seed {seed}) x {att.shape[0]} targets, full row build, "
+                      f"{el:.1f} s; Dijkstra-only {done / max(dj, 1e-9):.1f} sources/s",
+            "cpu_model": model, "host_nproc": os.cpu_count()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=0, help="0 = one full table at N=1")
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--blocks-per-step", type=int, default=16)
+    ap.add_argument("--groups", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from shadow_amd import spe
+    top, att, desc = workload(args.config)
+    g = spe.Graph(top, device=local)
+    info = g.info()
+    t = spe.PathTable(g, att, groups=args.groups)
+    A = t.A
+    nblk = t.nblocks
+    bps = max(1, args.blocks_per_step)
+    nwin = math.ceil(nblk / bps)
+    steps = args.steps if args.steps > 0 else nwin
+
+    def window(k: int):
+        w = (k * world + rank) % nwin
+        return w * bps, min(nblk, (w + 1) * bps)
+
+    def sources_in(b0, b1):
+        return min(A, b1 * 64) - b0 * 64
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for k in range(args.warmup):
+        t.build_blocks(*window(k))
+    if not args.no_profile:
+        t.profile(True)
+    it_total, fr_total, done = 0, 0, 0
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        b0, b1 = window(args.warmup + k)
+        st = t.build_blocks(b0, b1)
+        it_total += st["iterations"]
+        fr_total += st["frontier_total"]
+        done += sources_in(b0, b1)
+    barrier()
+    el = time.perf_counter() - t0
+    kp = t.kernel_profile() if not args.no_profile else None
+
+    total_sources = done
+    if dist is not None:
+        import torch
+        x = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        el = float(x.item())
+        y = torch.tensor([done], dtype=torch.float64, device="cuda")
+        dist.all_reduce(y)
+        total_sources = int(y.item())
+
+    value = total_sources / el
+    n, m_dir = info["n_vertices"], info["n_relax_entries"]
+    # SURVEY §8d per-source algorithmic bytes, split by stage
+    b_relax = 12.0 * m_dir + 28.0 * n + 8.0
+    b_rows = 22.0 * A
+    roof = None
+    extra = {}
+    if kp is not None:
+        rl = kp["relax"]
+        relax_s = rl["ms"] / 1e3
+        ach = b_relax * done / relax_s / 1e9 if relax_s > 0 else 0.0
+        roof = {"bound": "hbm", "kernel": "k_relax (SSSP stage)", "achieved": round(ach, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "launches": rl["launches"], "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
+                "algorithmic_bytes_per_source": b_relax}
+        rw = kp["rows"]
+        rows_s = rw["ms"] / 1e3
+        extra["roofline_rows"] = {"kernel": "k_rows_sssp", "achieved": round(b_rows * done / rows_s / 1e9, 1)
+                                  if rows_s > 0 else 0.0, "unit": "GB/s", "launches": rw["launches"],
+                                  "launch_avg_us": round(1e3 * rw["ms"] / max(1, rw["launches"]), 2),
+                                  "algorithmic_bytes_per_source": b_rows}
+        extra["kernel_ms"] = {k: round(v["ms"], 3) for k, v in kp.items()}
+        extra["kernel_launches"] = {k: v["launches"] for k, v in kp.items()}
+        extra["pipeline_frac_of_hbm"] = round((b_relax + b_rows) * value / 1e9 / HBM_PEAK_GBS, 4)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(top, att, args.cpu_seconds)
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "sources/s", "n_gpus": world, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * el / steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": desc, "n": n, "m_dir": m_dir, "attached": A,
+                       "sources_per_step_per_gpu": bps * 64, "groups_per_launch": args.groups or "auto",
+                       "parallelism": f"source blocks sharded over {world} GPU(s), no data-path collective"},
+            "full_table_time_s": round(A / value, 3),
+            "relax_rounds_per_step": round(it_total / max(1, steps), 1),
+            "frontier_entries_per_source": round(fr_total / max(1, done), 1),
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        line.update(extra)
+        if cpu:
+            line["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

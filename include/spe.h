@@ -1,0 +1,175 @@
+/*
+ * spe.h -- C ABI of the MI355X shortest-path engine (libspe.so).
+ *
+ * This is the library the C topology host code (include/shd_topology_spe.h)
+ * calls in place of igraph + the per-pair path cache of the reference
+ * (src/main/routing/shd-topology.c).  Plain C types only: no glib, no igraph,
+ * no torch.  Device pointers appear only where the caller hands over its own
+ * HBM buffers (external table storage, batched lookups); streams are passed as
+ * `void*` holding a hipStream_t (NULL = the library's own stream).
+ *
+ * Which reference interface each entry point replaces:
+ *   spe_graph_create     igraph_read_graph_graphml result + _topology_checkGraphProperties
+ *                        + _topology_extractEdgeWeights   shd-topology.c:356-384, 709-794, 1197-1231
+ *   spe_graph_info       top->isComplete / isDirected / prefersDirectPaths  shd-topology.c:39-52, 736-775
+ *   spe_table_create     verticesWithAttachedHosts (the target set A)     shd-topology.c:1510-1528, 2366-2367
+ *   spe_table_build      _topology_computeSourcePaths / _lookupDirectPath / _computeShortestPathToSelf
+ *                        for every source row                              shd-topology.c:1530-1912
+ *   spe_table_get        _topology_getPathEntry + path_getLatency/Reliability shd-topology.c:1952-2070
+ *   spe_lookup_batch     3 x _topology_getPathEntry per packet (shd-worker.c:235,243,247), batched
+ *   spe_table_min_latency top->minimumPathLatency -> worker_updateMinTimeJump shd-topology.c:1359-1370
+ *   spe_last_error       the critical()/warning() log lines of the reference
+ *
+ * Semantics of one table entry (s_slot, t_slot), s,t = attached vertices:
+ *   DIRECT if the graph is complete, or prefers direct paths and has an s->t edge;
+ *   else t == s: the Dijkstra row's [s] path (self-loop) under SPE_SELF_ROW,
+ *                or 2 x min incident edge under SPE_SELF_RULE (and whenever s has no self-loop);
+ *   else the shortest path of the source row of s (per-source rows: tree_s(s->t)).
+ *   latency/reliability are bit-identical to the reference's f64 operation order;
+ *   route (next hop, hops) follows the canonical tie-break
+ *   parent(v) = argmin (dist[u], u) over {u : fl(dist[u] + w) == dist[v]},
+ *   which equals igraph's choice whenever no two candidates share dist[u].
+ *   Unroutable: latency = reliability = -1, hops = 0 (topology_getLatency's -1.0).
+ */
+#ifndef SPE_H_
+#define SPE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* return codes */
+#define SPE_OK 0
+#define SPE_EINVAL (-1)      /* bad argument / graph fails the reference's validation */
+#define SPE_EHIP (-2)        /* a HIP runtime call failed */
+#define SPE_ENOMEM (-3)
+#define SPE_EUNSUPPORTED (-4)
+#define SPE_ESTATE (-5)      /* call order violated (e.g. get before build) */
+#define SPE_ENODEV (-6)      /* no gfx950 device visible */
+
+#define SPE_SELF_ROW 0       /* (s,s) from the Dijkstra row's [s] path (igraph 0.7-0.9) */
+#define SPE_SELF_RULE 1      /* (s,s) = 2 x min incident edge (shd-topology.c:1530-1638) */
+
+typedef struct spe_graph spe_graph;
+typedef struct spe_table spe_table;
+
+/* Edge list exactly as the GraphML file gives it: vertex i = i-th <node>,
+ * edge e = e-th <edge>.  vertex_packetloss[v] = NaN when absent (or the
+ * pointer is NULL: all absent).  Validation mirrors _topology_checkGraph:
+ * latency > 0, 0 <= packetloss <= 1, endpoints in range. */
+typedef struct spe_graph_desc {
+    int32_t n_vertices;
+    int64_t n_edges;
+    const int32_t* edge_source;
+    const int32_t* edge_target;
+    const double* edge_latency;     /* ms */
+    const double* edge_packetloss;
+    const double* vertex_packetloss;
+    int32_t directed;
+    int32_t prefer_direct;          /* graph attribute preferdirectpaths */
+} spe_graph_desc;
+
+typedef struct spe_graph_info {
+    int32_t n_vertices;
+    int64_t n_edges;
+    int64_t n_relax_entries;        /* directed adjacency entries after merging parallel edges */
+    int32_t directed;
+    int32_t prefer_direct;
+    int32_t complete;               /* _topology_isComplete */
+    int32_t parallel_latency_differs; /* multigraph whose get_eid edge is not the lightest */
+    int32_t weight_floor_ok;        /* every fl(d + w) > d is guaranteed (no absorbed edges) */
+    int32_t device;
+} spe_graph_info;
+
+typedef struct spe_table_opts {
+    int32_t self_mode;              /* SPE_SELF_ROW | SPE_SELF_RULE */
+    int32_t force_sssp;             /* 1: ignore complete/preferdirectpaths (diagnostic) */
+    int32_t groups_per_launch;      /* 64-source groups relaxed together; 0 = auto */
+    int32_t block_begin;            /* first 64-row source block owned by this table */
+    int32_t block_end;              /* one past the last; 0,0 = all blocks */
+    /* optional caller-owned device storage for the owned blocks (all four or none),
+     * each sized (block_end-block_begin) * n_attached * 64 elements */
+    void* ext_latency;              /* double   */
+    void* ext_reliability;          /* double   */
+    void* ext_next_hop;             /* int32_t  */
+    void* ext_hops;                 /* uint16_t */
+} spe_table_opts;
+
+/* Where a table keeps its rows.  Element (s_slot, t_slot) of a field lives at
+ *   ((s_slot / 64 - block_begin) * n_attached + t_slot) * 64 + s_slot % 64
+ * ("SB64": 64 source rows interleaved per target, so one source block is one
+ * contiguous span and a 64-source batch writes whole 512-byte segments). */
+typedef struct spe_table_layout {
+    int32_t n_attached;
+    int32_t block_begin;
+    int32_t block_end;
+    int64_t elems;                  /* per field */
+    void* latency;                  /* device pointers */
+    void* reliability;
+    void* next_hop;
+    void* hops;
+} spe_table_layout;
+
+typedef struct spe_entry {
+    double latency;                 /* ms, -1 if unroutable */
+    double reliability;             /* -1 if unroutable */
+    int32_t next_hop;               /* vertex index of the first hop, -1 if unroutable */
+    int32_t hops;                   /* edges on the path, 0 if unroutable */
+} spe_entry;
+
+typedef struct spe_build_stats {
+    int64_t iterations;             /* relaxation rounds summed over launches */
+    int64_t frontier_total;         /* (group, vertex) relaxations summed */
+    int64_t launches;
+    double seconds;                 /* wall time of the last spe_table_build */
+} spe_build_stats;
+
+const char* spe_last_error(void);
+int spe_device_count(int32_t* out);
+
+int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out);
+int spe_graph_info_get(const spe_graph* g, spe_graph_info* out);
+void spe_graph_free(spe_graph* g);
+
+/* attached[i] = vertex of source/target slot i (unique vertices). */
+int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached,
+                     const spe_table_opts* opts, spe_table** out);
+/* Compute every owned source row (enqueued on `stream`, returns after completion). */
+int spe_table_build(spe_table* t, void* stream);
+/* Compute only source blocks [block_begin, block_end) (absolute block ids, a
+ * sub-range of the owned ones): incremental / stepped builds. */
+int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end, void* stream);
+
+/* Per-kernel device time, from HIP events recorded around every launch on the
+ * build stream while profiling is enabled (costs one event pair per launch). */
+enum { SPE_K_INIT = 0, SPE_K_SEED, SPE_K_COMPACT, SPE_K_RELAX, SPE_K_ROWS, SPE_K_DIRECT, SPE_K_COUNT };
+typedef struct spe_kernel_profile {
+    double ms[SPE_K_COUNT];
+    int64_t launches[SPE_K_COUNT];
+} spe_kernel_profile;
+int spe_table_profile_enable(spe_table* t, int32_t enable);   /* also resets the counters */
+int spe_table_profile_get(const spe_table* t, spe_kernel_profile* out);
+int spe_table_build_stats(const spe_table* t, spe_build_stats* out);
+int spe_table_layout_get(const spe_table* t, spe_table_layout* out);
+/* One entry, read back from HBM (synchronous). */
+int spe_table_get(const spe_table* t, int32_t s_slot, int32_t t_slot, spe_entry* out);
+/* Copy owned rows [row_begin,row_end) x [0,n_attached) to host, row-major;
+ * any output pointer may be NULL. */
+int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, double* latency,
+                       double* reliability, int32_t* next_hop, int32_t* hops);
+/* Batched per-packet lookups against the HBM-resident table.  d_pairs holds q
+ * (s_slot, t_slot) int32 pairs; outputs are device arrays of q elements.
+ * ok = 1 when routable (topology_isRoutable).  Pairs whose source row is not
+ * owned by this table return ok = 0, latency = reliability = -1. */
+int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, double* d_latency,
+                     double* d_reliability, uint8_t* d_ok, void* stream);
+/* Minimum latency over every owned routable entry (minimumPathLatency). */
+int spe_table_min_latency(const spe_table* t, double* out);
+void spe_table_free(spe_table* t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPE_H_ */

@@ -1,0 +1,60 @@
+"""Build libspe.so (gfx950 HIP kernels + C ABI) and libshdtopo.so (C host shim)
+in-tree with hipcc / gcc.  Used by __graft_entry__.build()."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+HOST = os.path.join(HERE, "host")
+LIB_SPE = os.path.join(HERE, "libspe.so")
+LIB_TOPO = os.path.join(HERE, "libshdtopo.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+HIP_FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
+             "-std=c++17", "-Wall", "-Wno-unused-function"]
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _stale(out, srcs):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > t for s in srcs)
+
+
+def build_spe(force: bool = False) -> str:
+    srcs = [os.path.join(CSRC, f) for f in ("spe.hip", "spe_graph_prep.cpp", "spe_internal.h")]
+    srcs.append(os.path.join(ROOT, "include", "spe.h"))
+    if force or _stale(LIB_SPE, srcs):
+        _run([HIPCC, *HIP_FLAGS, "-shared", "-o", LIB_SPE,
+              os.path.join(CSRC, "spe.hip"), os.path.join(CSRC, "spe_graph_prep.cpp")])
+    return LIB_SPE
+
+
+def build_topo(force: bool = False) -> str:
+    src = os.path.join(HOST, "shd_topology_spe.c")
+    hdrs = [os.path.join(ROOT, "include", "shd_topology_spe.h"), os.path.join(ROOT, "include", "spe.h")]
+    if not os.path.exists(src):
+        return ""
+    if force or _stale(LIB_TOPO, [src, LIB_SPE] + hdrs):
+        _run(["gcc", "-O2", "-ffp-contract=off", "-fPIC", "-std=c11", "-D_GNU_SOURCE", "-Wall", "-shared",
+              "-o", LIB_TOPO, src, "-I", os.path.join(ROOT, "include"),
+              "-L", HERE, "-lspe", "-Wl,-rpath,$ORIGIN", "-lpthread", "-lm"])
+    return LIB_TOPO
+
+
+def build_all(force: bool = False) -> None:
+    build_spe(force)
+    build_topo(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

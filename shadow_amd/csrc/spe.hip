@@ -1,0 +1,1023 @@
+// spe.hip -- MI355X (gfx950) shortest-path engine for Shadow's topology routing.
+//
+// Replaces, for every attached (source, target) pair at once, what the
+// reference computes lazily per cache miss in src/main/routing/shd-topology.c:
+//   DIRECT  _topology_lookupDirectPath           :1862-1912
+//   SSSP    _topology_computeSourcePaths          :1640-1860 (igraph Dijkstra :1741)
+//           + _topology_computePathProperties     :1392-1508
+//   SELF    _topology_computeShortestPathToSelf   :1530-1638
+// and serves the per-packet queries (topology_getLatency/getReliability/
+// isRoutable, :2048-2075) from an HBM-resident table.
+//
+// Kernels (all hand-written for CDNA4, wave64):
+//   k_init_state   per-batch state reset (dist = +inf, parent = none)
+//   k_seed         sources -> first frontier marks
+//   k_compact      wave-ballot compaction of marked (group, vertex) pairs into
+//                  the next frontier list; one atomicAdd per wave
+//   k_relax        multi-source label-correcting relaxation: ONE WAVE = one
+//                  vertex x 64 sources (lane = source).  Only in-neighbours that
+//                  changed last round are read (coalesced 512-B rows of the
+//                  [vertex][64] state); the canonical parent (alt, dist[u], u)
+//                  and the path-order reliability / hop count / first hop are
+//                  carried with the distance, so converged state IS the row.
+//   k_rows_sssp    state -> table rows (+ SELF / [s] rules, slow path-walk for
+//                  targets with vertex loss or multigraph get_eid latencies)
+//   k_rows_direct  complete graphs: every pair is the direct edge
+//   k_direct_overlay  preferdirectpaths: adjacent pairs get the direct edge
+//   k_lookup       batched per-packet (s, t) -> (latency, reliability, ok)
+//   k_min_latency  minimumPathLatency reduction
+//
+// Bit-exactness: every distance is the least fixpoint of
+// d[v] = min_u fl(d[u] + w), which igraph's Dijkstra also computes (IEEE
+// round-to-nearest addition is monotone); compiled with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "spe_internal.h"
+
+#define WAVE 64
+#define BLOCK 256
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t _e = (expr);                                                            \
+        if (_e != hipSuccess)                                                              \
+            return fail(SPE_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
+    } while (0)
+
+constexpr double INF = __builtin_inf();
+
+struct DevGraph {
+    int32_t n;
+    int32_t nrel;
+    const int32_t* iptr;
+    const int32_t* icol;
+    const double* iw;
+    const double* ia;
+    const double* iwrep;
+    const int32_t* optr;
+    const int32_t* ocol;
+    const double* owrep;
+    const double* oarep;
+    const double* vfac;
+    const double* loop_w;
+    const double* loop_a;
+    const double* self_w2;
+    const double* self_a2;
+    const int32_t* self_other;
+};
+
+struct RowMode {
+    int32_t complete;
+    int32_t prefer;
+    int32_t self_mode;
+    int32_t multi_rep;
+};
+
+struct State {        // [group][vertex][64 lanes]
+    double* D;        // distance
+    int32_t* P;       // in-CSR index of the chosen parent edge, -1 none
+    double* R;        // path-order reliability fold starting at the source factor
+    int2* HF;         // (hops, first hop)
+};
+
+struct Table {
+    double* lat;
+    double* rel;
+    int32_t* next;
+    uint16_t* hops;
+    int32_t A;
+};
+
+__device__ __forceinline__ bool has_attr(double x) { return !__builtin_isnan(x); }
+
+__device__ __forceinline__ size_t tidx(int32_t sb_local, int32_t A, int32_t j, int32_t lane) {
+    return ((size_t)sb_local * (size_t)A + (size_t)j) * WAVE + (size_t)lane;
+}
+
+// ----------------------------------------------------------------- kernels
+
+__global__ __launch_bounds__(BLOCK) void k_init_state(int32_t n, int32_t groups,
+                                                      const int32_t* __restrict__ srcv,
+                                                      const double* __restrict__ vfac, State st) {
+    const size_t total = (size_t)groups * n * WAVE;
+    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * BLOCK) {
+        const int32_t lane = (int32_t)(i & (WAVE - 1));
+        const size_t gv = i >> 6;
+        const int32_t g = (int32_t)(gv / n);
+        const int32_t v = (int32_t)(gv - (size_t)g * n);
+        const int32_t s = srcv[g * WAVE + lane];
+        if (v == s) {
+            st.D[i] = 0.0;
+            const double fs = vfac[s];
+            st.R[i] = has_attr(fs) ? 1.0 * fs : 1.0;  // (1 * (1 - p_src)), shd-topology.c:1428-1430
+            st.HF[i] = make_int2(0, -1);
+        } else {
+            st.D[i] = INF;
+        }
+        st.P[i] = -1;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_seed(int32_t n, int32_t groups, const int32_t* __restrict__ srcv,
+                                                DevGraph G, uint8_t* chg, uint8_t* mark) {
+    const int32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= groups * WAVE) return;
+    const int32_t s = srcv[i];
+    if (s < 0) return;
+    const size_t base = (size_t)(i / WAVE) * n;
+    chg[base + s] = 1;
+    for (int32_t k = G.optr[s]; k < G.optr[s + 1]; ++k) mark[base + G.ocol[k]] = 1;
+}
+
+// marked (group*n + v) -> frontier list; clears the marks and the stale change flags.
+__global__ __launch_bounds__(BLOCK) void k_compact(int64_t total, uint8_t* mark, uint8_t* chg_clear,
+                                                   int32_t* __restrict__ frontier, int32_t* count) {
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int64_t wave = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
+    for (int64_t base = wave * WAVE; base < total; base += nwaves * WAVE) {
+        const int64_t i = base + lane;
+        bool m = false;
+        if (i < total) {
+            m = mark[i] != 0;
+            if (m) mark[i] = 0;
+            if (chg_clear[i]) chg_clear[i] = 0;
+        }
+        const uint64_t bal = __ballot(m);
+        if (bal == 0) continue;
+        const int32_t cnt = __popcll(bal);
+        int32_t off = 0;
+        if (lane == 0) off = atomicAdd(count, cnt);
+        off = __shfl(off, 0);
+        const int32_t pre = __popcll(bal & ((1ull << lane) - 1ull));
+        if (m) frontier[off + pre] = (int32_t)i;
+    }
+}
+
+// One wave per frontier entry (group, v); lane = source of that group.
+__global__ __launch_bounds__(BLOCK) void k_relax(const int32_t* __restrict__ frontier,
+                                                 const int32_t* __restrict__ count_ptr, int32_t n,
+                                                 const int32_t* __restrict__ srcv, DevGraph G, State st,
+                                                 const uint8_t* __restrict__ chg_prev, uint8_t* chg_cur,
+                                                 uint8_t* mark) {
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int32_t nwaves = (gridDim.x * BLOCK) >> 6;
+    const int32_t cnt = *count_ptr;
+    for (int32_t e = (blockIdx.x * BLOCK + threadIdx.x) >> 6; e < cnt; e += nwaves) {
+        const int32_t idx = __builtin_amdgcn_readfirstlane(frontier[e]);
+        const int32_t g = idx / n;
+        const int32_t v = idx - g * n;
+        const size_t gbase = (size_t)g * n;
+        const int32_t s = srcv[g * WAVE + lane];
+        const size_t rv = (gbase + v) * WAVE + lane;
+        const bool active = (s >= 0) && (s != v);
+        const double d_old = st.D[rv];
+        const int32_t p_old = st.P[rv];
+        double bd = d_old;
+        int32_t bk = p_old;
+        int32_t bu = -1;        // parent vertex, lazily resolved
+        double bdu = -1.0;      // dist of the parent, lazily resolved
+        bool need = false;
+        const int32_t k0 = G.iptr[v], k1 = G.iptr[v + 1];
+        for (int32_t k = k0; k < k1; ++k) {
+            const int32_t u = G.icol[k];
+            if (!chg_prev[gbase + u]) continue;  // wave-uniform
+            const double w = G.iw[k];
+            const double du = st.D[(gbase + u) * WAVE + lane];
+            const double alt = du + w;
+            if (!active || !(alt > du)) continue;
+            bool better = false;
+            if (alt < bd) {
+                better = true;
+            } else if (alt == bd) {
+                if (k == bk) {
+                    need = true;   // current parent changed state: refresh
+                    bdu = du;
+                    bu = u;
+                } else {
+                    if (bu < 0) bu = G.icol[bk];
+                    if (bdu < 0.0) bdu = st.D[(gbase + bu) * WAVE + lane];
+                    better = (du < bdu) || (du == bdu && u < bu);
+                }
+            }
+            if (better) {
+                bd = alt;
+                bk = k;
+                bu = u;
+                bdu = du;
+                need = true;
+            }
+        }
+        bool changed = false;
+        if (need) {
+            if (bu < 0) bu = G.icol[bk];
+            const size_t ru = (gbase + bu) * WAVE + lane;
+            const double r_new = st.R[ru] * G.ia[bk];
+            const int2 hu = st.HF[ru];
+            const int2 hf_new = make_int2(hu.x + 1, (bu == s) ? v : hu.y);
+            if (d_old == INF) {
+                changed = true;
+            } else {
+                const int2 hf_old = st.HF[rv];
+                changed = (bd != d_old) || (bk != p_old) || (r_new != st.R[rv]) ||
+                          (hf_new.x != hf_old.x) || (hf_new.y != hf_old.y);
+            }
+            if (changed) {
+                st.D[rv] = bd;
+                st.P[rv] = bk;
+                st.R[rv] = r_new;
+                st.HF[rv] = hf_new;
+            }
+        }
+        if (__ballot(changed)) {
+            if (lane == 0) chg_cur[gbase + v] = 1;
+            const int32_t o0 = G.optr[v], o1 = G.optr[v + 1];
+            for (int32_t k = o0 + lane; k < o1; k += WAVE) mark[gbase + G.ocol[k]] = 1;
+        }
+    }
+}
+
+// (s, s) entry: DIRECT self-loop, the row's [s] path, or the SELF rule.
+__device__ __forceinline__ void self_entry(const DevGraph& G, const RowMode& md, int32_t s, double& L,
+                                           double& R, int32_t& N, int32_t& H) {
+    const double fs = G.vfac[s];
+    const double lw = G.loop_w[s];
+    const bool loop = has_attr(lw);
+    if (md.complete && !loop) return;                    // get_eid(s, s) fails: unroutable
+    if ((md.complete || md.prefer) && loop) {            // _topology_lookupDirectPath(s, s)
+        double r = 1.0;
+        if (has_attr(fs)) r *= fs;
+        if (has_attr(fs)) r *= fs;
+        r *= G.loop_a[s];
+        L = 0.0 + lw;
+        R = r;
+        N = s;
+        H = 1;
+    } else if (md.self_mode == SPE_SELF_ROW && loop) {   // path [s], shd-topology.c:1456-1484
+        double r = 1.0;
+        if (has_attr(fs)) r *= fs;
+        r *= G.loop_a[s];
+        double l = 0.0 + lw;
+        if (l == 0) l = 1;
+        L = l;
+        R = r;
+        N = s;
+        H = 1;
+    } else if (G.self_other[s] >= 0) {                   // SELF rule
+        L = G.self_w2[s];
+        R = G.self_a2[s];
+        N = G.self_other[s];
+        H = 2;
+    }
+}
+
+// DIRECT (s, t != s): first edge s->t in the out-CSR (merged, get_eid's edge).
+__device__ __forceinline__ bool direct_entry(const DevGraph& G, int32_t s, int32_t t, double& L, double& R,
+                                             int32_t& N, int32_t& H) {
+    int32_t lo = G.optr[s], hi = G.optr[s + 1];
+    while (lo < hi) {
+        const int32_t mid = lo + ((hi - lo) >> 1);
+        if (G.ocol[mid] < t) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo >= G.optr[s + 1] || G.ocol[lo] != t) return false;
+    const double fs = G.vfac[s], ft = G.vfac[t];
+    double r = 1.0;
+    if (has_attr(fs)) r *= fs;
+    if (has_attr(ft)) r *= ft;
+    r *= G.oarep[lo];
+    L = 0.0 + G.owrep[lo];
+    R = r;
+    N = t;
+    H = 1;
+    return true;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t groups, int32_t sb0,
+                                                     const int32_t* __restrict__ srcv,
+                                                     const int32_t* __restrict__ slot_vertex, DevGraph G,
+                                                     RowMode md, State st, Table tb) {
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
+    const int64_t items = (int64_t)groups * tb.A;
+    for (int64_t it = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it < items; it += nwaves) {
+        const int32_t g = (int32_t)(it / tb.A);
+        const int32_t j = (int32_t)(it - (int64_t)g * tb.A);
+        const int32_t t = slot_vertex[j];
+        const int32_t s = srcv[g * WAVE + lane];
+        double L = -1.0, R = -1.0;
+        int32_t N = -1, H = 0;
+        if (s >= 0) {
+            if (t == s) {
+                self_entry(G, md, s, L, R, N, H);
+            } else {
+                const size_t gbase = (size_t)g * n;
+                const size_t rt = (gbase + t) * WAVE + lane;
+                const double d = st.D[rt];
+                if (d < INF) {
+                    const int2 hf = st.HF[rt];
+                    const double ft = G.vfac[t];
+                    const bool fast = (!has_attr(ft) || ft == 1.0) && !md.multi_rep;
+                    if (fast) {
+                        L = d;
+                        R = st.R[rt];
+                    } else {
+                        // path-order re-fold, shd-topology.c:1413-1493 (rare: vertex loss on
+                        // the target, or multigraph get_eid latencies)
+                        const double fs = G.vfac[s];
+                        double l = 0.0, r = 1.0;
+                        if (has_attr(fs)) r *= fs;
+                        if (has_attr(ft)) r *= ft;
+                        const int32_t h = hf.x;
+                        for (int32_t i = 1; i <= h; ++i) {
+                            int32_t x = t;
+                            for (int32_t q = 0; q < h - i; ++q) x = G.icol[st.P[(gbase + x) * WAVE + lane]];
+                            const int32_t k = st.P[(gbase + x) * WAVE + lane];
+                            l += G.iwrep[k];
+                            r *= G.ia[k];
+                        }
+                        L = l;
+                        R = r;
+                    }
+                    if (L == 0) L = 1;   // shd-topology.c:1833-1837
+                    N = hf.y;
+                    H = hf.x;
+                }
+            }
+        }
+        const size_t o = tidx(sb0 + g, tb.A, j, lane);
+        tb.lat[o] = L;
+        tb.rel[o] = R;
+        tb.next[o] = N;
+        tb.hops[o] = (uint16_t)(H > 65535 ? 65535 : H);
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_rows_direct(int32_t groups, int32_t sb0,
+                                                       const int32_t* __restrict__ srcv,
+                                                       const int32_t* __restrict__ slot_vertex, DevGraph G,
+                                                       RowMode md, Table tb) {
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
+    const int64_t items = (int64_t)groups * tb.A;
+    for (int64_t it = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it < items; it += nwaves) {
+        const int32_t g = (int32_t)(it / tb.A);
+        const int32_t j = (int32_t)(it - (int64_t)g * tb.A);
+        const int32_t t = slot_vertex[j];
+        const int32_t s = srcv[g * WAVE + lane];
+        double L = -1.0, R = -1.0;
+        int32_t N = -1, H = 0;
+        if (s >= 0) {
+            if (t == s) self_entry(G, md, s, L, R, N, H);
+            else direct_entry(G, s, t, L, R, N, H);
+        }
+        const size_t o = tidx(sb0 + g, tb.A, j, lane);
+        tb.lat[o] = L;
+        tb.rel[o] = R;
+        tb.next[o] = N;
+        tb.hops[o] = (uint16_t)H;
+    }
+}
+
+// preferdirectpaths: every attached neighbour t of s takes the direct edge.
+__global__ __launch_bounds__(BLOCK) void k_direct_overlay(int32_t groups, int32_t sb0,
+                                                          const int32_t* __restrict__ srcv,
+                                                          const int32_t* __restrict__ vertex_slot, DevGraph G,
+                                                          Table tb) {
+    const int32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= groups * WAVE) return;
+    const int32_t g = i / WAVE, lane = i % WAVE;
+    const int32_t s = srcv[i];
+    if (s < 0) return;
+    const double fs = G.vfac[s];
+    for (int32_t k = G.optr[s]; k < G.optr[s + 1]; ++k) {
+        const int32_t t = G.ocol[k];
+        const int32_t j = vertex_slot[t];
+        if (j < 0) continue;
+        const double ft = G.vfac[t];
+        double r = 1.0;
+        if (has_attr(fs)) r *= fs;
+        if (has_attr(ft)) r *= ft;
+        r *= G.oarep[k];
+        const size_t o = tidx(sb0 + g, tb.A, j, lane);
+        tb.lat[o] = 0.0 + G.owrep[k];
+        tb.rel[o] = r;
+        tb.next[o] = t;
+        tb.hops[o] = 1;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_lookup(const int2* __restrict__ pairs, int64_t q, int32_t blk0,
+                                                  int32_t blk1, Table tb, double* __restrict__ lat,
+                                                  double* __restrict__ rel, uint8_t* __restrict__ ok) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < q; i += (int64_t)gridDim.x * BLOCK) {
+        const int2 p = pairs[i];
+        const int32_t sb = p.x >> 6;
+        double L = -1.0, R = -1.0;
+        if (p.x >= 0 && p.y >= 0 && p.y < tb.A && sb >= blk0 && sb < blk1) {
+            const size_t o = tidx(sb - blk0, tb.A, p.y, p.x & (WAVE - 1));
+            L = tb.lat[o];
+            R = tb.rel[o];
+        }
+        lat[i] = L;
+        rel[i] = R;
+        ok[i] = L > -1.0 ? 1 : 0;   // topology_isRoutable: getLatency > -1
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_min_latency(const double* __restrict__ lat, int64_t elems,
+                                                       unsigned long long* out) {
+    double m = INF;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < elems; i += (int64_t)gridDim.x * BLOCK) {
+        const double l = lat[i];
+        if (l > -1.0 && l < m) m = l;
+    }
+    for (int off = 32; off > 0; off >>= 1) m = fmin(m, __shfl_xor(m, off));
+    if ((threadIdx.x & (WAVE - 1)) == 0 && m < INF)
+        atomicMin(out, (unsigned long long)__double_as_longlong(m));  // positive doubles order as integers
+}
+
+}  // namespace
+
+// ================================================================== host side
+
+struct spe_graph {
+    spe::HostGraph hg;
+    int32_t device = 0;
+    DevGraph dev{};
+    std::vector<void*> allocs;
+};
+
+struct spe_table {
+    spe_graph* g = nullptr;
+    int32_t A = 0;
+    int32_t blk0 = 0, blk1 = 0;
+    int32_t groups = 8;
+    RowMode md{};
+    bool ext = false;
+    bool built = false;
+    Table tb{};
+    int32_t* d_slot_vertex = nullptr;
+    int32_t* d_vertex_slot = nullptr;
+    std::vector<int32_t> attached;
+    // workspace
+    State st{};
+    uint8_t* chg[2] = {nullptr, nullptr};
+    uint8_t* mark = nullptr;
+    int32_t* frontier = nullptr;
+    int32_t* counts = nullptr;
+    int32_t max_iters = 0;
+    int32_t* d_srcv = nullptr;
+    int32_t* h_srcv = nullptr;
+    int32_t* h_counts = nullptr;
+    unsigned long long* d_min = nullptr;
+    hipStream_t stream = nullptr;
+    spe_build_stats stats{};
+    std::vector<void*> allocs;
+    // profiling: one event pair per launch, resolved after each batch's sync
+    bool prof = false;
+    std::vector<hipEvent_t> ev_pool;
+    struct Rec {
+        int kind;
+        hipEvent_t a, b;
+    };
+    std::vector<Rec> pending;
+    size_t ev_next = 0;
+    spe_kernel_profile kp{};
+    std::vector<int32_t> h_hist;
+};
+
+namespace {
+
+template <typename T>
+int dev_alloc(std::vector<void*>& allocs, T** p, size_t count) {
+    void* q = nullptr;
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc(&q, count * sizeof(T));
+    if (e != hipSuccess)
+        return fail(SPE_ENOMEM, "hipMalloc(" + std::to_string(count * sizeof(T)) + " B): " + hipGetErrorString(e));
+    allocs.push_back(q);
+    *p = static_cast<T*>(q);
+    return SPE_OK;
+}
+
+template <typename T>
+int dev_upload(std::vector<void*>& allocs, const std::vector<T>& h, const T** out) {
+    T* p = nullptr;
+    int r = dev_alloc(allocs, &p, h.size());
+    if (r) return r;
+    if (!h.empty()) HIP_TRY(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    *out = p;
+    return SPE_OK;
+}
+
+int check_device(int32_t device) {
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0) return fail(SPE_ENODEV, "no HIP device visible");
+    if (device < 0 || device >= cnt) return fail(SPE_EINVAL, "device index out of range");
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(SPE_ENODEV, std::string("libspe is built for gfx950, device is ") + prop.gcnArchName);
+    HIP_TRY(hipSetDevice(device));
+    return SPE_OK;
+}
+
+int grid_for(int64_t work_items, int64_t per_block, int cap = 8192) {
+    int64_t b = (work_items + per_block - 1) / per_block;
+    if (b < 1) b = 1;
+    if (b > cap) b = cap;
+    return (int)b;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* spe_last_error(void) { return g_err.c_str(); }
+
+int spe_device_count(int32_t* out) {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    if (out) *out = c;
+    return SPE_OK;
+}
+
+int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out) {
+    if (!out) return fail(SPE_EINVAL, "out is NULL");
+    *out = nullptr;
+    auto* g = new spe_graph();
+    std::string err;
+    int r = spe::prepare_graph(desc, &g->hg, &err);
+    if (r) {
+        delete g;
+        return fail(r, err);
+    }
+    r = check_device(device);
+    if (r) {
+        delete g;
+        return r;
+    }
+    g->device = device;
+    const spe::HostGraph& h = g->hg;
+    DevGraph& d = g->dev;
+    d.n = h.n;
+    d.nrel = (int32_t)h.icol.size();
+#define UP(field, src)                                   \
+    do {                                                 \
+        r = dev_upload(g->allocs, src, &d.field);        \
+        if (r) {                                         \
+            spe_graph_free(g);                           \
+            return r;                                    \
+        }                                                \
+    } while (0)
+    UP(iptr, h.iptr);
+    UP(icol, h.icol);
+    UP(iw, h.iw);
+    UP(ia, h.ia);
+    UP(iwrep, h.iwrep);
+    if (h.directed) {
+        UP(optr, h.optr);
+        UP(ocol, h.ocol);
+        UP(owrep, h.owrep);
+        UP(oarep, h.oarep);
+    } else {
+        d.optr = d.iptr;
+        d.ocol = d.icol;
+        d.owrep = d.iwrep;
+        d.oarep = d.ia;
+    }
+    UP(vfac, h.vfac);
+    UP(loop_w, h.loop_w);
+    UP(loop_a, h.loop_a);
+    UP(self_w2, h.self_w2);
+    UP(self_a2, h.self_a2);
+    UP(self_other, h.self_other);
+#undef UP
+    *out = g;
+    return SPE_OK;
+}
+
+int spe_graph_info_get(const spe_graph* g, spe_graph_info* out) {
+    if (!g || !out) return fail(SPE_EINVAL, "NULL argument");
+    out->n_vertices = g->hg.n;
+    out->n_edges = g->hg.m;
+    out->n_relax_entries = (int64_t)g->hg.icol.size();
+    out->directed = g->hg.directed;
+    out->prefer_direct = g->hg.prefer_direct;
+    out->complete = g->hg.complete;
+    out->parallel_latency_differs = g->hg.multi_rep;
+    out->weight_floor_ok = g->hg.weight_floor_ok;
+    out->device = g->device;
+    return SPE_OK;
+}
+
+void spe_graph_free(spe_graph* g) {
+    if (!g) return;
+    (void)hipSetDevice(g->device);
+    for (void* p : g->allocs) (void)hipFree(p);
+    delete g;
+}
+
+int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, const spe_table_opts* opts,
+                     spe_table** out) {
+    if (!g || !attached || n_attached <= 0 || !out) return fail(SPE_EINVAL, "spe_table_create: bad arguments");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(g->device));
+    const int32_t n = g->hg.n;
+    std::vector<int32_t> vslot(n, -1);
+    for (int32_t i = 0; i < n_attached; ++i) {
+        const int32_t v = attached[i];
+        if (v < 0 || v >= n) return fail(SPE_EINVAL, "attached vertex out of range");
+        if (vslot[v] >= 0) return fail(SPE_EINVAL, "attached vertices must be unique");
+        vslot[v] = i;
+    }
+    auto* t = new spe_table();
+    t->g = g;
+    t->A = n_attached;
+    t->attached.assign(attached, attached + n_attached);
+    const int32_t nblk_all = (n_attached + WAVE - 1) / WAVE;
+    t->blk0 = 0;
+    t->blk1 = nblk_all;
+    spe_table_opts o{};
+    if (opts) o = *opts;
+    if (o.block_begin != 0 || o.block_end != 0) {
+        if (o.block_begin < 0 || o.block_end > nblk_all || o.block_begin > o.block_end) {
+            delete t;
+            return fail(SPE_EINVAL, "block range out of bounds");
+        }
+        t->blk0 = o.block_begin;
+        t->blk1 = o.block_end;
+    }
+    const bool force = o.force_sssp != 0;
+    t->md.complete = g->hg.complete && !force;
+    t->md.prefer = g->hg.prefer_direct && !force;
+    t->md.self_mode = o.self_mode;
+    t->md.multi_rep = g->hg.multi_rep;
+    // state per group = n * 64 * 28 B; keep the batch's working set within a few GB
+    int32_t groups = o.groups_per_launch;
+    if (groups <= 0) {
+        const double per_group = (double)n * WAVE * 28.0;
+        groups = (int32_t)std::max(1.0, std::min(16.0, 4.0e9 / per_group));
+    }
+    t->groups = std::max(1, std::min(groups, std::max(1, t->blk1 - t->blk0)));
+    t->tb.A = n_attached;
+    const size_t elems = (size_t)(t->blk1 - t->blk0) * n_attached * WAVE;
+    int r = SPE_OK;
+#define TRY(x)                  \
+    do {                        \
+        r = (x);                \
+        if (r) {                \
+            spe_table_free(t);  \
+            return r;           \
+        }                       \
+    } while (0)
+    if (o.ext_latency || o.ext_reliability || o.ext_next_hop || o.ext_hops) {
+        if (!(o.ext_latency && o.ext_reliability && o.ext_next_hop && o.ext_hops)) {
+            delete t;
+            return fail(SPE_EINVAL, "external storage needs all four fields");
+        }
+        t->ext = true;
+        t->tb.lat = (double*)o.ext_latency;
+        t->tb.rel = (double*)o.ext_reliability;
+        t->tb.next = (int32_t*)o.ext_next_hop;
+        t->tb.hops = (uint16_t*)o.ext_hops;
+    } else {
+        TRY(dev_alloc(t->allocs, &t->tb.lat, elems));
+        TRY(dev_alloc(t->allocs, &t->tb.rel, elems));
+        TRY(dev_alloc(t->allocs, &t->tb.next, elems));
+        TRY(dev_alloc(t->allocs, &t->tb.hops, elems));
+    }
+    const std::vector<int32_t> sv(attached, attached + n_attached);
+    const int32_t* tmp = nullptr;
+    TRY(dev_upload(t->allocs, sv, &tmp));
+    t->d_slot_vertex = const_cast<int32_t*>(tmp);
+    TRY(dev_upload(t->allocs, vslot, &tmp));
+    t->d_vertex_slot = const_cast<int32_t*>(tmp);
+    const size_t G = (size_t)t->groups;
+    if (!t->md.complete) {
+        const size_t se = G * n * WAVE;
+        TRY(dev_alloc(t->allocs, &t->st.D, se));
+        TRY(dev_alloc(t->allocs, &t->st.P, se));
+        TRY(dev_alloc(t->allocs, &t->st.R, se));
+        TRY(dev_alloc(t->allocs, &t->st.HF, se));
+        TRY(dev_alloc(t->allocs, &t->chg[0], G * n));
+        TRY(dev_alloc(t->allocs, &t->chg[1], G * n));
+        TRY(dev_alloc(t->allocs, &t->mark, G * n));
+        TRY(dev_alloc(t->allocs, &t->frontier, G * n));
+        t->max_iters = 4 * n + 64;
+        TRY(dev_alloc(t->allocs, &t->counts, (size_t)t->max_iters + 2));
+        HIP_TRY(hipMemset(t->chg[0], 0, G * n));
+        HIP_TRY(hipMemset(t->chg[1], 0, G * n));
+        HIP_TRY(hipMemset(t->mark, 0, G * n));
+    }
+    TRY(dev_alloc(t->allocs, &t->d_srcv, G * WAVE));
+    TRY(dev_alloc(t->allocs, &t->d_min, 1));
+#undef TRY
+    HIP_TRY(hipHostMalloc((void**)&t->h_srcv, G * WAVE * sizeof(int32_t), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&t->h_counts, 64 * sizeof(int32_t), hipHostMallocDefault));
+    HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+    *out = t;
+    return SPE_OK;
+}
+
+// Event bracketing around a launch (no-op unless profiling is enabled).
+struct LaunchTimer {
+    spe_table* t;
+    hipStream_t s;
+    int kind;
+    hipEvent_t a = nullptr, b = nullptr;
+    LaunchTimer(spe_table* t_, hipStream_t s_, int kind_) : t(t_), s(s_), kind(kind_) {
+        if (!t->prof) return;
+        if (t->ev_next + 2 > t->ev_pool.size()) {
+            for (int i = 0; i < 256; ++i) {
+                hipEvent_t e;
+                if (hipEventCreate(&e) != hipSuccess) return;
+                t->ev_pool.push_back(e);
+            }
+        }
+        a = t->ev_pool[t->ev_next++];
+        b = t->ev_pool[t->ev_next++];
+        (void)hipEventRecord(a, s);
+    }
+    ~LaunchTimer() {
+        if (!a) return;
+        (void)hipEventRecord(b, s);
+        t->pending.push_back({kind, a, b});
+    }
+};
+
+static int resolve_profile(spe_table* t) {
+    for (auto& r : t->pending) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+        t->kp.ms[r.kind] += ms;
+        t->kp.launches[r.kind] += 1;
+    }
+    t->pending.clear();
+    t->ev_next = 0;
+    return SPE_OK;
+}
+
+static int relax_to_convergence(spe_table* t, int32_t groups, hipStream_t s) {
+    const spe_graph* g = t->g;
+    const int32_t n = g->hg.n;
+    const int64_t total = (int64_t)groups * n;
+    const int relax_grid = 4096;   // persistent-style grid-stride over the frontier
+    const int compact_grid = grid_for(total, BLOCK, 4096);
+    HIP_TRY(hipMemsetAsync(t->counts, 0, sizeof(int32_t) * ((size_t)t->max_iters + 2), s));
+    {
+        LaunchTimer lt(t, s, SPE_K_INIT);
+        k_init_state<<<grid_for(total * WAVE, BLOCK, 8192), BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev.vfac, t->st);
+    }
+    {
+        LaunchTimer lt(t, s, SPE_K_SEED);
+        k_seed<<<(groups * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev, t->chg[0],
+                                                                     t->mark);
+    }
+    {
+        LaunchTimer lt(t, s, SPE_K_COMPACT);
+        k_compact<<<compact_grid, BLOCK, 0, s>>>(total, t->mark, t->chg[1], t->frontier, t->counts + 1);
+    }
+    // frontier lists alternate between the two halves of one buffer only through
+    // the counts array: relax(it) consumes frontier written by compact(it).
+    int32_t it = 1;
+    int32_t check_every = 8;
+    int32_t* fr_a = t->frontier;
+    for (;;) {
+        for (int32_t q = 0; q < check_every; ++q, ++it) {
+            if (it > t->max_iters) return fail(SPE_ESTATE, "relaxation did not converge");
+            uint8_t* prev = t->chg[(it - 1) & 1];
+            uint8_t* cur = t->chg[it & 1];
+            {
+                LaunchTimer lt(t, s, SPE_K_RELAX);
+                k_relax<<<relax_grid, BLOCK, 0, s>>>(fr_a, t->counts + it, n, t->d_srcv, g->dev, t->st, prev, cur,
+                                                     t->mark);
+            }
+            // the frontier buffer is rewritten by compact only after relax finished (stream order)
+            {
+                LaunchTimer lt(t, s, SPE_K_COMPACT);
+                k_compact<<<compact_grid, BLOCK, 0, s>>>(total, t->mark, prev, fr_a, t->counts + it + 1);
+            }
+        }
+        HIP_TRY(hipMemcpyAsync(t->h_counts, t->counts + it, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        t->stats.launches += 2 * check_every;
+        if (t->h_counts[0] == 0) break;
+        check_every = 4;
+    }
+    // frontier sizes of this batch (for work accounting)
+    const int32_t nit = it;
+    if ((int32_t)t->h_hist.size() < nit + 1) t->h_hist.resize(nit + 1);
+    HIP_TRY(hipMemcpy(t->h_hist.data(), t->counts, sizeof(int32_t) * (nit + 1), hipMemcpyDeviceToHost));
+    for (int32_t i = 1; i <= nit; ++i) t->stats.frontier_total += t->h_hist[i];
+    t->stats.iterations += it - 1;
+    return SPE_OK;
+}
+
+int spe_table_build(spe_table* t, void* stream) {
+    if (!t) return fail(SPE_EINVAL, "NULL table");
+    return spe_table_build_blocks(t, t->blk0, t->blk1, stream);
+}
+
+int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end, void* stream) {
+    if (!t) return fail(SPE_EINVAL, "NULL table");
+    if (block_begin < t->blk0 || block_end > t->blk1 || block_begin > block_end)
+        return fail(SPE_EINVAL, "block range not owned by this table");
+    HIP_TRY(hipSetDevice(t->g->device));
+    hipStream_t s = stream ? (hipStream_t)stream : t->stream;
+    const auto t0 = std::chrono::steady_clock::now();
+    const spe_graph* g = t->g;
+    t->stats = spe_build_stats{};
+    for (int32_t b = block_begin; b < block_end; b += t->groups) {
+        const int32_t groups = std::min(t->groups, block_end - b);
+        HIP_TRY(hipStreamSynchronize(s));   // h_srcv is reused per batch
+        for (int32_t gi = 0; gi < groups; ++gi)
+            for (int32_t l = 0; l < WAVE; ++l) {
+                const int32_t slot = (b + gi) * WAVE + l;
+                t->h_srcv[gi * WAVE + l] = slot < t->A ? t->attached[slot] : -1;
+            }
+        HIP_TRY(hipMemcpyAsync(t->d_srcv, t->h_srcv, sizeof(int32_t) * groups * WAVE, hipMemcpyHostToDevice, s));
+        const int32_t sb0 = b - t->blk0;
+        const int64_t items = (int64_t)groups * t->A;
+        const int row_grid = grid_for(items * WAVE, BLOCK, 8192);
+        if (t->md.complete) {
+            LaunchTimer lt(t, s, SPE_K_DIRECT);
+            k_rows_direct<<<row_grid, BLOCK, 0, s>>>(groups, sb0, t->d_srcv, t->d_slot_vertex, g->dev, t->md, t->tb);
+        } else {
+            int r = relax_to_convergence(t, groups, s);
+            if (r) return r;
+            {
+                LaunchTimer lt(t, s, SPE_K_ROWS);
+                k_rows_sssp<<<row_grid, BLOCK, 0, s>>>(g->hg.n, groups, sb0, t->d_srcv, t->d_slot_vertex, g->dev,
+                                                       t->md, t->st, t->tb);
+            }
+            if (t->md.prefer) {
+                LaunchTimer lt(t, s, SPE_K_DIRECT);
+                k_direct_overlay<<<(groups * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(
+                    groups, sb0, t->d_srcv, t->d_vertex_slot, g->dev, t->tb);
+            }
+        }
+        HIP_TRY(hipGetLastError());
+        if (t->prof) {
+            HIP_TRY(hipStreamSynchronize(s));
+            int r = resolve_profile(t);
+            if (r) return r;
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    t->stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    t->built = true;
+    return SPE_OK;
+}
+
+int spe_table_profile_enable(spe_table* t, int32_t enable) {
+    if (!t) return fail(SPE_EINVAL, "NULL table");
+    t->prof = enable != 0;
+    t->kp = spe_kernel_profile{};
+    t->pending.clear();
+    t->ev_next = 0;
+    return SPE_OK;
+}
+
+int spe_table_profile_get(const spe_table* t, spe_kernel_profile* out) {
+    if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
+    *out = t->kp;
+    return SPE_OK;
+}
+
+int spe_table_build_stats(const spe_table* t, spe_build_stats* out) {
+    if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
+    *out = t->stats;
+    return SPE_OK;
+}
+
+int spe_table_layout_get(const spe_table* t, spe_table_layout* out) {
+    if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
+    out->n_attached = t->A;
+    out->block_begin = t->blk0;
+    out->block_end = t->blk1;
+    out->elems = (int64_t)(t->blk1 - t->blk0) * t->A * WAVE;
+    out->latency = t->tb.lat;
+    out->reliability = t->tb.rel;
+    out->next_hop = t->tb.next;
+    out->hops = t->tb.hops;
+    return SPE_OK;
+}
+
+int spe_table_get(const spe_table* t, int32_t s_slot, int32_t t_slot, spe_entry* out) {
+    if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
+    if (!t->built) return fail(SPE_ESTATE, "table not built");
+    if (s_slot < 0 || s_slot >= t->A || t_slot < 0 || t_slot >= t->A) return fail(SPE_EINVAL, "slot out of range");
+    const int32_t sb = s_slot / WAVE;
+    if (sb < t->blk0 || sb >= t->blk1) return fail(SPE_EINVAL, "source row not owned by this table");
+    HIP_TRY(hipSetDevice(t->g->device));
+    const size_t o = ((size_t)(sb - t->blk0) * t->A + t_slot) * WAVE + (s_slot % WAVE);
+    uint16_t h = 0;
+    HIP_TRY(hipMemcpy(&out->latency, t->tb.lat + o, sizeof(double), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&out->reliability, t->tb.rel + o, sizeof(double), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&out->next_hop, t->tb.next + o, sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&h, t->tb.hops + o, sizeof(uint16_t), hipMemcpyDeviceToHost));
+    out->hops = h;
+    return SPE_OK;
+}
+
+int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, double* latency,
+                       double* reliability, int32_t* next_hop, int32_t* hops) {
+    if (!t) return fail(SPE_EINVAL, "NULL table");
+    if (!t->built) return fail(SPE_ESTATE, "table not built");
+    if (row_begin < t->blk0 * WAVE || row_end > std::min(t->A, t->blk1 * WAVE) || row_begin > row_end)
+        return fail(SPE_EINVAL, "row range not owned by this table");
+    HIP_TRY(hipSetDevice(t->g->device));
+    const int32_t A = t->A;
+    const int32_t b0 = row_begin / WAVE, b1 = (row_end + WAVE - 1) / WAVE;
+    const size_t blk_elems = (size_t)A * WAVE;
+    std::vector<double> bl(blk_elems), br(blk_elems);
+    std::vector<int32_t> bn(blk_elems);
+    std::vector<uint16_t> bh(blk_elems);
+    for (int32_t b = b0; b < b1; ++b) {
+        const size_t off = (size_t)(b - t->blk0) * blk_elems;
+        if (latency) HIP_TRY(hipMemcpy(bl.data(), t->tb.lat + off, blk_elems * 8, hipMemcpyDeviceToHost));
+        if (reliability) HIP_TRY(hipMemcpy(br.data(), t->tb.rel + off, blk_elems * 8, hipMemcpyDeviceToHost));
+        if (next_hop) HIP_TRY(hipMemcpy(bn.data(), t->tb.next + off, blk_elems * 4, hipMemcpyDeviceToHost));
+        if (hops) HIP_TRY(hipMemcpy(bh.data(), t->tb.hops + off, blk_elems * 2, hipMemcpyDeviceToHost));
+        for (int32_t l = 0; l < WAVE; ++l) {
+            const int32_t row = b * WAVE + l;
+            if (row < row_begin || row >= row_end) continue;
+            const size_t ro = (size_t)(row - row_begin) * A;
+            for (int32_t j = 0; j < A; ++j) {
+                const size_t src = (size_t)j * WAVE + l;
+                if (latency) latency[ro + j] = bl[src];
+                if (reliability) reliability[ro + j] = br[src];
+                if (next_hop) next_hop[ro + j] = bn[src];
+                if (hops) hops[ro + j] = bh[src];
+            }
+        }
+    }
+    return SPE_OK;
+}
+
+int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, double* d_latency,
+                     double* d_reliability, uint8_t* d_ok, void* stream) {
+    if (!t || (q > 0 && (!d_pairs || !d_latency || !d_reliability || !d_ok))) return fail(SPE_EINVAL, "bad arguments");
+    if (!t->built) return fail(SPE_ESTATE, "table not built");
+    if (q == 0) return SPE_OK;
+    HIP_TRY(hipSetDevice(t->g->device));
+    hipStream_t s = stream ? (hipStream_t)stream : t->stream;
+    k_lookup<<<grid_for(q, BLOCK, 16384), BLOCK, 0, s>>>((const int2*)d_pairs, q, t->blk0, t->blk1, t->tb, d_latency,
+                                                        d_reliability, d_ok);
+    HIP_TRY(hipGetLastError());
+    if (!stream) HIP_TRY(hipStreamSynchronize(s));
+    return SPE_OK;
+}
+
+int spe_table_min_latency(const spe_table* t, double* out) {
+    if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
+    if (!t->built) return fail(SPE_ESTATE, "table not built");
+    HIP_TRY(hipSetDevice(t->g->device));
+    const unsigned long long init = 0x7FF0000000000000ull;  // +inf
+    HIP_TRY(hipMemcpyAsync(t->d_min, &init, sizeof(init), hipMemcpyHostToDevice, t->stream));
+    const int64_t elems = (int64_t)(t->blk1 - t->blk0) * t->A * WAVE;
+    k_min_latency<<<grid_for(elems, BLOCK, 4096), BLOCK, 0, t->stream>>>(t->tb.lat, elems, t->d_min);
+    HIP_TRY(hipGetLastError());
+    unsigned long long bits = 0;
+    HIP_TRY(hipMemcpyAsync(&bits, t->d_min, sizeof(bits), hipMemcpyDeviceToHost, t->stream));
+    HIP_TRY(hipStreamSynchronize(t->stream));
+    double v;
+    std::memcpy(&v, &bits, sizeof(v));
+    *out = (v == INF) ? 0.0 : v;   // reference's "0 = unset" sentinel, shd-topology.c:1360
+    return SPE_OK;
+}
+
+void spe_table_free(spe_table* t) {
+    if (!t) return;
+    (void)hipSetDevice(t->g->device);
+    if (t->stream) (void)hipStreamSynchronize(t->stream);
+    for (void* p : t->allocs) (void)hipFree(p);
+    if (t->h_srcv) (void)hipHostFree(t->h_srcv);
+    if (t->h_counts) (void)hipHostFree(t->h_counts);
+    for (hipEvent_t e : t->ev_pool) (void)hipEventDestroy(e);
+    if (t->stream) (void)hipStreamDestroy(t->stream);
+    delete t;
+}
+
+}  // extern "C"

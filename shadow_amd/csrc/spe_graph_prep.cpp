@@ -1,0 +1,206 @@
+// spe_graph_prep.cpp -- host-side ingest of a topology edge list into the
+// device layout used by the gfx950 kernels.  This is boundary code: it
+// validates the graph like the reference's topology_new and builds index
+// structures (CSR, per-vertex rule constants); it performs no path computation.
+//
+// Reference behaviour restated here:
+//   * validation: latency > 0, 0 <= loss <= 1        shd-topology.c:1026-1109
+//   * completeness (_topology_isComplete)             shd-topology.c:435-537
+//   * get_eid edge of a vertex pair: igraph keeps each vertex's incidence index
+//     sorted by (neighbour asc, edge id desc) and get_eid takes the first match,
+//     i.e. the HIGHEST edge id among parallel edges (see oracle/oracle.c header)
+//   * SELF rule constants: first incident edge in igraph order with strictly
+//     smaller latency; lat = 2.0*min, rel = r*r     shd-topology.c:1567-1626
+//   * edge reliability factor 1.0f - p (f64)          shd-topology.c:422, 1582
+#include "spe_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+
+namespace spe {
+
+static bool has_attr(double x) { return !std::isnan(x); }
+
+int prepare_graph(const spe_graph_desc* d, HostGraph* hg, std::string* err) {
+    if (!d || d->n_vertices <= 0 || d->n_edges < 0 || !d->edge_source || !d->edge_target ||
+        !d->edge_latency || !d->edge_packetloss) {
+        *err = "spe_graph_create: invalid descriptor";
+        return SPE_EINVAL;
+    }
+    const int32_t n = d->n_vertices;
+    const int64_t m = d->n_edges;
+    hg->n = n;
+    hg->m = m;
+    hg->directed = d->directed != 0;
+    hg->prefer_direct = d->prefer_direct != 0;
+
+    double wmin = INFINITY, wsum = 0.0;
+    for (int64_t e = 0; e < m; ++e) {
+        const int32_t a = d->edge_source[e], b = d->edge_target[e];
+        const double w = d->edge_latency[e], p = d->edge_packetloss[e];
+        if (a < 0 || b < 0 || a >= n || b >= n) {
+            *err = "edge " + std::to_string(e) + " has an endpoint out of range";
+            return SPE_EINVAL;
+        }
+        if (!(w > 0.0) || !std::isfinite(w)) {
+            *err = "edge " + std::to_string(e) + " latency must be > 0";
+            return SPE_EINVAL;
+        }
+        if (!(p >= 0.0 && p <= 1.0)) {
+            *err = "edge " + std::to_string(e) + " packetloss must be in [0,1]";
+            return SPE_EINVAL;
+        }
+        wmin = std::min(wmin, w);
+        wsum += w;
+    }
+    // fl(d + w) > d for every d <= wsum when w > wsum * 2^-53 (round to nearest even)
+    hg->weight_floor_ok = (m == 0) || (wmin > std::ldexp(wsum, -52));
+
+    hg->vfac.assign(n, NAN);
+    for (int32_t v = 0; v < n; ++v) {
+        const double p = d->vertex_packetloss ? d->vertex_packetloss[v] : NAN;
+        if (has_attr(p)) hg->vfac[v] = 1.0 - p;
+    }
+
+    // ---- directed adjacency entries (from, to, eid), self-loops kept apart
+    struct Ent {
+        int32_t to, from;
+        int64_t eid;
+    };
+    std::vector<Ent> ents;
+    ents.reserve(static_cast<size_t>(hg->directed ? m : 2 * m));
+    hg->loop_eid.assign(n, -1);
+    for (int64_t e = 0; e < m; ++e) {
+        const int32_t a = d->edge_source[e], b = d->edge_target[e];
+        if (a == b) {
+            if (e > hg->loop_eid[a]) hg->loop_eid[a] = e;  // get_eid(v,v): highest id
+            continue;
+        }
+        ents.push_back({b, a, e});
+        if (!hg->directed) ents.push_back({a, b, e});
+    }
+    hg->loop_w.assign(n, NAN);
+    hg->loop_a.assign(n, NAN);
+    for (int32_t v = 0; v < n; ++v) {
+        const int64_t e = hg->loop_eid[v];
+        if (e >= 0) {
+            hg->loop_w[v] = d->edge_latency[e];
+            hg->loop_a[v] = 1.0 - d->edge_packetloss[e];
+        }
+    }
+
+    // ---- relaxation in-CSR: by (to, from); parallel edges merged
+    std::sort(ents.begin(), ents.end(), [](const Ent& x, const Ent& y) {
+        if (x.to != y.to) return x.to < y.to;
+        if (x.from != y.from) return x.from < y.from;
+        return x.eid > y.eid;  // first = highest id = get_eid's choice
+    });
+    hg->iptr.assign(static_cast<size_t>(n) + 1, 0);
+    hg->icol.clear();
+    hg->iw.clear();
+    hg->ia.clear();
+    hg->iwrep.clear();
+    hg->multi_rep = false;
+    for (size_t i = 0; i < ents.size();) {
+        size_t j = i;
+        double wrel = INFINITY;
+        while (j < ents.size() && ents[j].to == ents[i].to && ents[j].from == ents[i].from) {
+            wrel = std::min(wrel, d->edge_latency[ents[j].eid]);
+            ++j;
+        }
+        const int64_t rep = ents[i].eid;
+        const double wrep = d->edge_latency[rep];
+        if (wrep != wrel) hg->multi_rep = true;
+        hg->icol.push_back(ents[i].from);
+        hg->iw.push_back(wrel);
+        hg->ia.push_back(1.0 - d->edge_packetloss[rep]);
+        hg->iwrep.push_back(wrep);
+        hg->iptr[ents[i].to + 1]++;
+        i = j;
+    }
+    if (hg->icol.size() >= (size_t)INT32_MAX) {
+        *err = "graph too large for 32-bit adjacency offsets";
+        return SPE_EUNSUPPORTED;
+    }
+    for (int32_t v = 0; v < n; ++v) hg->iptr[v + 1] += hg->iptr[v];
+
+    // ---- out-CSR (frontier marking + DIRECT lookups): by (from, to)
+    if (hg->directed) {
+        std::vector<int64_t> idx(hg->icol.size());
+        std::vector<int32_t> to_of(hg->icol.size());
+        for (int32_t v = 0; v < n; ++v)
+            for (int32_t k = hg->iptr[v]; k < hg->iptr[v + 1]; ++k) to_of[k] = v;
+        std::iota(idx.begin(), idx.end(), 0);
+        std::sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) {
+            if (hg->icol[x] != hg->icol[y]) return hg->icol[x] < hg->icol[y];
+            return to_of[x] < to_of[y];
+        });
+        hg->optr.assign(static_cast<size_t>(n) + 1, 0);
+        hg->ocol.resize(idx.size());
+        hg->owrep.resize(idx.size());
+        hg->oarep.resize(idx.size());
+        for (size_t i = 0; i < idx.size(); ++i) {
+            hg->ocol[i] = to_of[idx[i]];
+            hg->owrep[i] = hg->iwrep[idx[i]];
+            hg->oarep[i] = hg->ia[idx[i]];
+            hg->optr[hg->icol[idx[i]] + 1]++;
+        }
+        for (int32_t v = 0; v < n; ++v) hg->optr[v + 1] += hg->optr[v];
+    }
+
+    // ---- SELF rule constants and completeness, both over incident(v, OUT)
+    struct Inc {
+        int32_t v, nb;
+        int64_t eid;
+    };
+    std::vector<Inc> inc;
+    inc.reserve(static_cast<size_t>(hg->directed ? m : 2 * m));
+    std::vector<int64_t> inc_count(n, 0);
+    for (int64_t e = 0; e < m; ++e) {
+        const int32_t a = d->edge_source[e], b = d->edge_target[e];
+        inc.push_back({a, b, e});
+        inc_count[a]++;
+        if (!hg->directed) {  // undirected: both endpoints (a self-loop twice)
+            inc.push_back({b, a, e});
+            inc_count[b]++;
+        }
+    }
+    std::sort(inc.begin(), inc.end(), [](const Inc& x, const Inc& y) {
+        if (x.v != y.v) return x.v < y.v;
+        if (x.nb != y.nb) return x.nb < y.nb;
+        return x.eid > y.eid;
+    });
+    hg->self_w2.assign(n, NAN);
+    hg->self_a2.assign(n, NAN);
+    hg->self_other.assign(n, -1);
+    for (size_t i = 0; i < inc.size();) {
+        const int32_t v = inc[i].v;
+        double minLatency = 0.0, relMin = 0.0;
+        int64_t best = -1;
+        for (; i < inc.size() && inc[i].v == v; ++i) {
+            const double w = d->edge_latency[inc[i].eid];
+            if (minLatency == 0 || w < minLatency) {
+                minLatency = w;
+                relMin = 1.0 - d->edge_packetloss[inc[i].eid];
+                best = inc[i].eid;
+            }
+        }
+        if (best >= 0) {
+            hg->self_w2[v] = 2.0 * minLatency;
+            hg->self_a2[v] = relMin * relMin;
+            const int32_t a = d->edge_source[best], b = d->edge_target[best];
+            hg->self_other[v] = (a == v) ? b : a;
+        }
+    }
+    bool complete = true;
+    for (int32_t v = 0; v < n && complete; ++v) {
+        int64_t cnt = inc_count[v];
+        if (!hg->directed && hg->loop_eid[v] >= 0) cnt -= 1;
+        if (cnt < n) complete = false;
+    }
+    hg->complete = complete;
+    return SPE_OK;
+}
+
+}  // namespace spe

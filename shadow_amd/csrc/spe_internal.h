@@ -1,0 +1,40 @@
+// spe_internal.h -- shared declarations of libspe (not part of the public ABI).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/spe.h"
+
+namespace spe {
+
+// Host copy of the device graph layout.
+struct HostGraph {
+    int32_t n = 0;
+    int64_t m = 0;
+    bool directed = false;
+    bool prefer_direct = false;
+    bool complete = false;
+    bool multi_rep = false;        // some merged pair's get_eid latency != relaxation latency
+    bool weight_floor_ok = true;
+
+    // relaxation in-CSR: entries u -> v grouped by v, sorted by u
+    std::vector<int32_t> iptr, icol;
+    std::vector<double> iw;        // min latency over parallel u->v edges (what Dijkstra relaxes)
+    std::vector<double> ia;        // 1 - loss of the get_eid edge
+    std::vector<double> iwrep;     // latency of the get_eid edge
+    // out-CSR (directed only; undirected graphs reuse the in-CSR)
+    std::vector<int32_t> optr, ocol;
+    std::vector<double> owrep, oarep;
+    // per vertex
+    std::vector<double> vfac;      // 1 - vertex loss, NaN when absent
+    std::vector<int64_t> loop_eid;
+    std::vector<double> loop_w, loop_a;       // get_eid(v,v) self-loop, NaN when none
+    std::vector<double> self_w2, self_a2;     // SELF rule: 2*min latency, r*r
+    std::vector<int32_t> self_other;          // other endpoint of the SELF edge, -1 none
+};
+
+int prepare_graph(const spe_graph_desc* d, HostGraph* hg, std::string* err);
+
+}  // namespace spe

@@ -1,0 +1,241 @@
+"""Python mirror of the path-engine C ABI (include/spe.h) over ctypes.
+
+This is plumbing for tests and the benchmark: every computation runs in
+libspe.so's gfx950 kernels.  There is no CPU fallback -- if the library or a
+gfx950 device is missing, construction raises SpeError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+from .graphs import Topology
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libspe.so")
+
+SPE_OK = 0
+SPE_SELF_ROW = 0
+SPE_SELF_RULE = 1
+WAVE = 64
+
+
+class SpeError(RuntimeError):
+    pass
+
+
+class GraphDesc(C.Structure):
+    _fields_ = [("n_vertices", C.c_int32), ("n_edges", C.c_int64),
+                ("edge_source", C.c_void_p), ("edge_target", C.c_void_p),
+                ("edge_latency", C.c_void_p), ("edge_packetloss", C.c_void_p),
+                ("vertex_packetloss", C.c_void_p), ("directed", C.c_int32), ("prefer_direct", C.c_int32)]
+
+
+class GraphInfo(C.Structure):
+    _fields_ = [("n_vertices", C.c_int32), ("n_edges", C.c_int64), ("n_relax_entries", C.c_int64),
+                ("directed", C.c_int32), ("prefer_direct", C.c_int32), ("complete", C.c_int32),
+                ("parallel_latency_differs", C.c_int32), ("weight_floor_ok", C.c_int32), ("device", C.c_int32)]
+
+
+class TableOpts(C.Structure):
+    _fields_ = [("self_mode", C.c_int32), ("force_sssp", C.c_int32), ("groups_per_launch", C.c_int32),
+                ("block_begin", C.c_int32), ("block_end", C.c_int32),
+                ("ext_latency", C.c_void_p), ("ext_reliability", C.c_void_p),
+                ("ext_next_hop", C.c_void_p), ("ext_hops", C.c_void_p)]
+
+
+class TableLayout(C.Structure):
+    _fields_ = [("n_attached", C.c_int32), ("block_begin", C.c_int32), ("block_end", C.c_int32),
+                ("elems", C.c_int64), ("latency", C.c_void_p), ("reliability", C.c_void_p),
+                ("next_hop", C.c_void_p), ("hops", C.c_void_p)]
+
+
+class Entry(C.Structure):
+    _fields_ = [("latency", C.c_double), ("reliability", C.c_double), ("next_hop", C.c_int32),
+                ("hops", C.c_int32)]
+
+
+KERNELS = ["init", "seed", "compact", "relax", "rows", "direct"]
+
+
+class KernelProfile(C.Structure):
+    _fields_ = [("ms", C.c_double * 6), ("launches", C.c_int64 * 6)]
+
+
+class BuildStats(C.Structure):
+    _fields_ = [("iterations", C.c_int64), ("frontier_total", C.c_int64), ("launches", C.c_int64),
+                ("seconds", C.c_double)]
+
+
+# every symbol include/spe.h declares (tests/test_abi.py checks the export table)
+EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_info_get", "spe_graph_free",
+           "spe_table_create", "spe_table_build", "spe_table_build_blocks", "spe_table_profile_enable",
+           "spe_table_profile_get", "spe_table_build_stats", "spe_table_layout_get",
+           "spe_table_get", "spe_table_download", "spe_lookup_batch", "spe_table_min_latency",
+           "spe_table_free"]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SpeError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        L.spe_last_error.restype = C.c_char_p
+        L.spe_device_count.argtypes = [P]
+        L.spe_graph_create.argtypes = [P, C.c_int32, P]
+        L.spe_graph_info_get.argtypes = [P, P]
+        L.spe_graph_free.argtypes = [P]
+        L.spe_graph_free.restype = None
+        L.spe_table_create.argtypes = [P, P, C.c_int32, P, P]
+        L.spe_table_build.argtypes = [P, P]
+        L.spe_table_build_blocks.argtypes = [P, C.c_int32, C.c_int32, P]
+        L.spe_table_profile_enable.argtypes = [P, C.c_int32]
+        L.spe_table_profile_get.argtypes = [P, P]
+        L.spe_table_build_stats.argtypes = [P, P]
+        L.spe_table_layout_get.argtypes = [P, P]
+        L.spe_table_get.argtypes = [P, C.c_int32, C.c_int32, P]
+        L.spe_table_download.argtypes = [P, C.c_int32, C.c_int32, P, P, P, P]
+        L.spe_lookup_batch.argtypes = [P, P, C.c_int64, P, P, P, P]
+        L.spe_table_min_latency.argtypes = [P, P]
+        L.spe_table_free.argtypes = [P]
+        L.spe_table_free.restype = None
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != SPE_OK:
+        msg = lib().spe_last_error().decode(errors="replace")
+        raise SpeError(f"{what} failed ({rc}): {msg}")
+
+
+def _p(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def device_count() -> int:
+    c = C.c_int32(0)
+    lib().spe_device_count(C.byref(c))
+    return int(c.value)
+
+
+class Graph:
+    """spe_graph: the topology uploaded to one device (topology_new's role)."""
+
+    def __init__(self, top: Topology, device: int = 0):
+        self.top = top
+        keep = [np.ascontiguousarray(top.esrc, np.int32), np.ascontiguousarray(top.edst, np.int32),
+                np.ascontiguousarray(top.elat, np.float64), np.ascontiguousarray(top.eloss, np.float64),
+                np.ascontiguousarray(top.vloss, np.float64)]
+        d = GraphDesc(int(top.n), int(keep[0].shape[0]), _p(keep[0]), _p(keep[1]), _p(keep[2]), _p(keep[3]),
+                      _p(keep[4]), int(bool(top.directed)), int(bool(top.prefer_direct)))
+        h = C.c_void_p()
+        _check(lib().spe_graph_create(C.byref(d), int(device), C.byref(h)), "spe_graph_create")
+        self.h = h
+        self.device = device
+
+    def info(self) -> dict:
+        i = GraphInfo()
+        _check(lib().spe_graph_info_get(self.h, C.byref(i)), "spe_graph_info_get")
+        return {f: getattr(i, f) for f, _ in GraphInfo._fields_}
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().spe_graph_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+class PathTable:
+    """spe_table: the per-(source, target) path table for attached vertices."""
+
+    def __init__(self, graph: Graph, attached, self_mode: int = SPE_SELF_ROW, force_sssp: bool = False,
+                 groups: int = 0, blocks=None, ext=None):
+        self.graph = graph
+        self.attached = np.ascontiguousarray(attached, np.int32)
+        self.A = int(self.attached.shape[0])
+        o = TableOpts()
+        o.self_mode = int(self_mode)
+        o.force_sssp = int(bool(force_sssp))
+        o.groups_per_launch = int(groups)
+        if blocks is not None:
+            o.block_begin, o.block_end = int(blocks[0]), int(blocks[1])
+        if ext is not None:  # four device pointers (ints)
+            o.ext_latency, o.ext_reliability, o.ext_next_hop, o.ext_hops = [int(x) for x in ext]
+        h = C.c_void_p()
+        _check(lib().spe_table_create(graph.h, _p(self.attached), self.A, C.byref(o), C.byref(h)),
+               "spe_table_create")
+        self.h = h
+
+    @property
+    def nblocks(self) -> int:
+        return (self.A + WAVE - 1) // WAVE
+
+    def build(self, stream: Optional[int] = None) -> dict:
+        _check(lib().spe_table_build(self.h, C.c_void_p(stream) if stream else None), "spe_table_build")
+        return self.stats()
+
+    def build_blocks(self, b0: int, b1: int, stream: Optional[int] = None) -> dict:
+        _check(lib().spe_table_build_blocks(self.h, int(b0), int(b1), C.c_void_p(stream) if stream else None),
+               "spe_table_build_blocks")
+        return self.stats()
+
+    def profile(self, enable: bool = True):
+        _check(lib().spe_table_profile_enable(self.h, int(bool(enable))), "spe_table_profile_enable")
+
+    def kernel_profile(self) -> dict:
+        k = KernelProfile()
+        _check(lib().spe_table_profile_get(self.h, C.byref(k)), "spe_table_profile_get")
+        return {name: {"ms": k.ms[i], "launches": k.launches[i]} for i, name in enumerate(KERNELS)}
+
+    def stats(self) -> dict:
+        s = BuildStats()
+        _check(lib().spe_table_build_stats(self.h, C.byref(s)), "spe_table_build_stats")
+        return {f: getattr(s, f) for f, _ in BuildStats._fields_}
+
+    def layout(self) -> dict:
+        l = TableLayout()
+        _check(lib().spe_table_layout_get(self.h, C.byref(l)), "spe_table_layout_get")
+        return {f: getattr(l, f) for f, _ in TableLayout._fields_}
+
+    def get(self, s_slot: int, t_slot: int) -> dict:
+        e = Entry()
+        _check(lib().spe_table_get(self.h, int(s_slot), int(t_slot), C.byref(e)), "spe_table_get")
+        return {"latency": e.latency, "reliability": e.reliability, "next_hop": e.next_hop, "hops": e.hops}
+
+    def download(self, row_begin: int = 0, row_end: Optional[int] = None) -> dict:
+        row_end = self.A if row_end is None else row_end
+        nr = row_end - row_begin
+        out = {"lat": np.empty((nr, self.A), np.float64), "rel": np.empty((nr, self.A), np.float64),
+               "next": np.empty((nr, self.A), np.int32), "hops": np.empty((nr, self.A), np.int32)}
+        _check(lib().spe_table_download(self.h, int(row_begin), int(row_end), _p(out["lat"]), _p(out["rel"]),
+                                        _p(out["next"]), _p(out["hops"])), "spe_table_download")
+        out["ok"] = out["lat"] > -1.0
+        return out
+
+    def lookup_batch(self, d_pairs: int, q: int, d_lat: int, d_rel: int, d_ok: int, stream: Optional[int] = None):
+        _check(lib().spe_lookup_batch(self.h, C.c_void_p(d_pairs), int(q), C.c_void_p(d_lat), C.c_void_p(d_rel),
+                                      C.c_void_p(d_ok), C.c_void_p(stream) if stream else None),
+               "spe_lookup_batch")
+
+    def min_latency(self) -> float:
+        v = C.c_double(0)
+        _check(lib().spe_table_min_latency(self.h, C.byref(v)), "spe_table_min_latency")
+        return float(v.value)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().spe_table_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()

@@ -1,0 +1,153 @@
+"""CPU tests: the oracle against the reference's own fixtures (pinning), and
+against an independent Dijkstra (scipy) for the SSSP regime."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from shadow_amd import graphs
+from oracle import Oracle, KIND_DIRECT, KIND_SELF, KIND_SSSP, KIND_FAIL
+
+
+def shipped(golden_dir):
+    z = np.load(os.path.join(golden_dir, "shipped_topology.npz"))
+    top = graphs.Topology(n=int(z["n"]), esrc=z["esrc"], edst=z["edst"], elat=z["elat"], eloss=z["eloss"],
+                          vloss=z["vloss"], directed=bool(z["directed"]), prefer_direct=bool(z["prefer_direct"]))
+    return top, z
+
+
+def test_kat_1vertex_configs(golden_dir):
+    """K1/K2: resource/examples/shadow.config.xml:2-28 and src/test/tcp/*lossy/lossless* embed a
+    1-vertex graph with one self-loop: (0,0) is DIRECT, latency 50.0, reliability 1*(1-0)*(1-p_e)."""
+    kats = json.load(open(os.path.join(golden_dir, "kat_1vertex.json")))
+    expect = {"examples": (50.0, 0.95), "tcp_lossy": (50.0, 0.75), "tcp_lossless": (50.0, 1.0)}
+    for name, (lat, rel) in expect.items():
+        t = graphs.load_graphml(kats[name]["graphml"], is_text=True)
+        o = Oracle(t)
+        assert o.complete
+        r = o.rows([0], [0])
+        assert r["kind"][0, 0] == KIND_DIRECT
+        assert r["lat"][0, 0] == lat and r["rel"][0, 0] == rel
+        assert kats[name]["lat"] == lat and kats[name]["rel"] == rel
+
+
+def test_shipped_topology_facts(golden_dir):
+    """183 vertices, 16,836 edges, complete => DIRECT everywhere,
+    and 737 unordered pairs have a shorter multi-hop path than the direct edge."""
+    top, z = shipped(golden_dir)
+    assert top.n == 183 and top.m == 16836 and not top.directed
+    o = Oracle(top)
+    assert o.complete
+    A = np.arange(top.n)
+    r = o.rows(A, A)
+    assert (r["kind"] == KIND_DIRECT).all()
+    # DIRECT latency = the edge attribute itself; reliability = (1-0)*(1-0)*(1-0.005)
+    eid = {}
+    for e in range(top.m):
+        a, b = int(top.esrc[e]), int(top.edst[e])
+        eid[(max(a, b), min(a, b))] = e   # highest id wins (get_eid restatement)
+    for s in range(0, top.n, 7):
+        for t in range(top.n):
+            e = eid[(max(s, t), min(s, t))]
+            assert r["lat"][s, t] == top.elat[e]
+            fs = 1.0 - top.vloss[s]
+            ft = 1.0 - top.vloss[t]
+            assert r["rel"][s, t] == ((1.0 * fs) * ft) * (1.0 - top.eloss[e])
+    np.testing.assert_array_equal(r["lat"], z["direct_lat"])
+    np.testing.assert_array_equal(r["rel"], z["direct_rel"])
+    diag = o.rows(A, A, force_sssp=True)
+    off = ~np.eye(top.n, dtype=bool)
+    shorter = (diag["lat"] < r["lat"]) & off
+    assert shorter.sum() // 2 == 737
+    np.testing.assert_array_equal(diag["lat"], z["sssp_lat"])
+    np.testing.assert_array_equal(diag["next"], z["sssp_next"])
+
+
+def _scipy_dist(top, src):
+    import scipy.sparse as sp
+    import scipy.sparse.csgraph as cg
+    d = {}
+    for a, b, w in zip(top.esrc, top.edst, top.elat):
+        if a == b:
+            continue
+        k = (a, b) if top.directed else (min(a, b), max(a, b))
+        d[k] = min(d.get(k, np.inf), w)
+    rr = [k[0] for k in d]
+    cc = [k[1] for k in d]
+    W = sp.csr_matrix((list(d.values()), (rr, cc)), shape=(top.n, top.n))
+    return cg.dijkstra(W, directed=top.directed, indices=src)
+
+
+@pytest.mark.parametrize("case", [
+    dict(n=400, extra_edges=1200, seed=11),
+    dict(n=300, extra_edges=900, seed=12, directed=True),
+    dict(n=300, extra_edges=900, seed=13, integer_weights=True),
+    dict(n=200, extra_edges=500, seed=14, multi=60),
+])
+def test_sssp_distances_match_independent_dijkstra(case):
+    top = graphs.gen_random_small(**case)
+    o = Oracle(top)
+    A = np.arange(top.n)
+    src = A[:25]
+    r = o.rows(src, A, force_sssp=True)
+    D = _scipy_dist(top, src)
+    off = src[:, None] != A[None, :]
+    if not case.get("multi"):
+        np.testing.assert_array_equal(r["lat"][off], D[off])   # bit-exact: same fixpoint
+    else:
+        # multigraph: latency is re-summed over get_eid's edge, not the lightest one
+        assert (r["lat"][off] >= D[off]).all()
+    assert (r["kind"][off] == KIND_SSSP).all()
+    # hop counts / next hops are consistent paths
+    assert (r["hops"][off] >= 1).all()
+
+
+def test_canonical_equals_igraph_without_ties():
+    top = graphs.gen_random_small(500, 1500, 21)
+    o = Oracle(top)
+    A = np.arange(top.n)
+    a = o.rows(A[:40], A, tie_mode=0, want_ties=True)
+    b = o.rows(A[:40], A, tie_mode=1)
+    assert a["double_ties"] == 0
+    for k in ("lat", "rel", "next", "hops", "kind"):
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+def test_ties_are_reported_and_only_change_routes():
+    top = graphs.gen_random_small(300, 900, 22, integer_weights=True)
+    o = Oracle(top)
+    A = np.arange(top.n)
+    a = o.rows(A[:30], A, tie_mode=0, want_ties=True)
+    b = o.rows(A[:30], A, tie_mode=1)
+    assert a["double_ties"] > 0
+    np.testing.assert_array_equal(a["lat"], b["lat"])   # distances never depend on ties
+
+
+def test_self_rules_and_prefer_direct_triangle():
+    """K3: generate_test_graph.py:4-13 restated: poi-1..3, 1-2 10ms, 2-3 10ms, 1-3 50ms, loss 0.05,
+    preferdirectpaths=true, no self-loops."""
+    gml = """<graphml xmlns="http://graphml.graphdrawing.org/xmlns">
+ <key attr.name="preferdirectpaths" attr.type="string" for="graph" id="g0"/>
+ <key attr.name="packetloss" attr.type="double" for="edge" id="d4"/>
+ <key attr.name="latency" attr.type="double" for="edge" id="d3"/>
+ <key attr.name="packetloss" attr.type="double" for="node" id="d0"/>
+ <graph edgedefault="undirected"><data key="g0">True</data>
+  <node id="poi-1"><data key="d0">0.0</data></node><node id="poi-2"/><node id="poi-3"><data key="d0">0.0</data></node>
+  <edge source="poi-1" target="poi-2"><data key="d3">10.0</data><data key="d4">0.05</data></edge>
+  <edge source="poi-2" target="poi-3"><data key="d3">10.0</data><data key="d4">0.05</data></edge>
+  <edge source="poi-1" target="poi-3"><data key="d3">50.0</data><data key="d4">0.05</data></edge>
+ </graph></graphml>"""
+    t = graphs.load_graphml(gml, is_text=True)
+    assert t.prefer_direct and np.isnan(t.vloss[1])
+    o = Oracle(t)
+    assert not o.complete
+    r = o.rows([0], [0, 1, 2])
+    assert r["kind"][0, 2] == KIND_DIRECT and r["lat"][0, 2] == 50.0 and r["rel"][0, 2] == 1.0 * 1.0 * (1.0 - 0.05)
+    assert r["kind"][0, 0] == KIND_SELF and r["lat"][0, 0] == 20.0 and r["rel"][0, 0] == 0.95 * 0.95
+    # without the preference the row goes through poi-2 (no vertex loss attr there, not an endpoint)
+    t.prefer_direct = False
+    r2 = Oracle(t).rows([0], [2])
+    assert r2["kind"][0, 0] == KIND_SSSP and r2["lat"][0, 0] == 20.0
+    assert r2["rel"][0, 0] == ((1.0 * 1.0) * 1.0) * 0.95 * 0.95
+    assert r2["next"][0, 0] == 1 and r2["hops"][0, 0] == 2
