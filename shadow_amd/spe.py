@@ -85,6 +85,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise SpeError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (soname
+        # libamdhip64.so.7, NEEDED as "libamdhip64.so" via $ORIGIN).  Loading torch first
+        # lets libspe's libamdhip64.so.7 dependency bind to that same copy; the other order
+        # would map two runtimes and torch would see no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         P = C.c_void_p
         L.spe_last_error.restype = C.c_char_p
