@@ -137,7 +137,7 @@ def main():
         b0, b1 = window(args.warmup + k)
         st = t.build_blocks(b0, b1)
         it_total += st["iterations"]
-        fr_total += st["frontier_total"]
+        fr_total += st["active_rounds"]
         done += sources_in(b0, b1)
     barrier()
     el = time.perf_counter() - t0
@@ -190,7 +190,7 @@ def main():
                        "parallelism": f"source blocks sharded over {world} GPU(s), no data-path collective"},
             "full_table_time_s": round(A / value, 3),
             "relax_rounds_per_step": round(it_total / max(1, steps), 1),
-            "frontier_entries_per_source": round(fr_total / max(1, done), 1),
+            "active_rounds_per_step": round(fr_total / max(1, steps), 1),
             "roofline": roof, "cpu_baseline": cpu,
         }
         line.update(extra)

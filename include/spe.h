@@ -121,7 +121,7 @@ typedef struct spe_entry {
 
 typedef struct spe_build_stats {
     int64_t iterations;             /* relaxation rounds summed over launches */
-    int64_t frontier_total;         /* (group, vertex) relaxations summed */
+    int64_t active_rounds;          /* relaxation rounds in which some distance/route changed */
     int64_t launches;
     double seconds;                 /* wall time of the last spe_table_build */
 } spe_build_stats;
@@ -144,7 +144,7 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
 
 /* Per-kernel device time, from HIP events recorded around every launch on the
  * build stream while profiling is enabled (costs one event pair per launch). */
-enum { SPE_K_INIT = 0, SPE_K_SEED, SPE_K_COMPACT, SPE_K_RELAX, SPE_K_ROWS, SPE_K_DIRECT, SPE_K_COUNT };
+enum { SPE_K_INIT = 0, SPE_K_SEED, SPE_K_HEAVY, SPE_K_RELAX, SPE_K_ROWS, SPE_K_DIRECT, SPE_K_COUNT };
 typedef struct spe_kernel_profile {
     double ms[SPE_K_COUNT];
     int64_t launches[SPE_K_COUNT];

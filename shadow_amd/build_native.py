@@ -46,8 +46,8 @@ def build_topo(force: bool = False) -> str:
         return ""
     if force or _stale(LIB_TOPO, [src, LIB_SPE] + hdrs):
         _run(["gcc", "-O2", "-ffp-contract=off", "-fPIC", "-std=c11", "-D_GNU_SOURCE", "-Wall", "-shared",
-              "-o", LIB_TOPO, src, "-I", os.path.join(ROOT, "include"),
-              "-L", HERE, "-lspe", "-Wl,-rpath,$ORIGIN", "-lpthread", "-lm"])
+              "-o", LIB_TOPO, src, "-I", os.path.join(ROOT, "include"), "-I", "/usr/include/libxml2",
+              "-L", HERE, "-lspe", "-Wl,-rpath,$ORIGIN", "-lxml2", "-lpthread", "-lm"])
     return LIB_TOPO
 
 

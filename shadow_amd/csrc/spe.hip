@@ -12,11 +12,11 @@
 // Kernels (all hand-written for CDNA4, wave64):
 //   k_init_state   per-batch state reset (dist = +inf, parent = none)
 //   k_seed         sources -> first frontier marks
-//   k_compact      wave-ballot compaction of marked (group, vertex) pairs into
-//                  the next frontier list; one atomicAdd per wave
-//   k_relax        multi-source label-correcting relaxation: ONE WAVE = one
-//                  vertex x 64 sources (lane = source).  Only in-neighbours that
-//                  changed last round are read (coalesced 512-B rows of the
+//   k_relax        multi-source label-correcting relaxation over a dense
+//                  frontier bitmap (wave-ballot compaction, no global counter):
+//                  ONE WAVE = one vertex x 64 sources (lane = source).  Only
+//                  in-neighbours that changed last round are read (their flags
+//                  are ballot-scanned 64 at a time; 4 coalesced 512-B rows of the
 //                  [vertex][64] state); the canonical parent (alt, dist[u], u)
 //                  and the path-order reliability / hop count / first hop are
 //                  carried with the distance, so converged state IS the row.
@@ -74,8 +74,10 @@ struct DevGraph {
     const double* iwrep;
     const int32_t* optr;
     const int32_t* ocol;
+    const int32_t* orev;     // out-entry -> index of the same edge in the target's in-CSR list
     const double* owrep;
     const double* oarep;
+    int32_t undirected;      // out-CSR == in-CSR
     const double* vfac;
     const double* loop_w;
     const double* loop_a;
@@ -91,11 +93,19 @@ struct RowMode {
     int32_t multi_rep;
 };
 
+// Per-lane route record carried with the distance: the path-order reliability
+// fold (starting at the source factor) and (hops, first hop).  16 B so a parent
+// lookup is ONE scattered 16-B access per lane.
+struct alignas(16) Route {
+    double r;
+    int32_t h;
+    int32_t f;
+};
+
 struct State {        // [group][vertex][64 lanes]
     double* D;        // distance
     int32_t* P;       // in-CSR index of the chosen parent edge, -1 none
-    double* R;        // path-order reliability fold starting at the source factor
-    int2* HF;         // (hops, first hop)
+    Route* RT;        // route record
 };
 
 struct Table {
@@ -128,8 +138,11 @@ __global__ __launch_bounds__(BLOCK) void k_init_state(int32_t n, int32_t groups,
         if (v == s) {
             st.D[i] = 0.0;
             const double fs = vfac[s];
-            st.R[i] = has_attr(fs) ? 1.0 * fs : 1.0;  // (1 * (1 - p_src)), shd-topology.c:1428-1430
-            st.HF[i] = make_int2(0, -1);
+            Route rt;
+            rt.r = has_attr(fs) ? 1.0 * fs : 1.0;  // (1 * (1 - p_src)), shd-topology.c:1428-1430
+            rt.h = 0;
+            rt.f = -1;
+            st.RT[i] = rt;
         } else {
             st.D[i] = INF;
         }
@@ -137,123 +150,320 @@ __global__ __launch_bounds__(BLOCK) void k_init_state(int32_t n, int32_t groups,
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_seed(int32_t n, int32_t groups, const int32_t* __restrict__ srcv,
-                                                DevGraph G, uint8_t* chg, uint8_t* mark) {
+// Change propagation.  When (group, u) changes in round r, it sets, for every
+// out-edge u -> x, the frontier mark of (group, x) and the in-edge flag of the
+// mirrored in-CSR entry (reverse index G.orev) in round r+1's buffers.  A vertex
+// then sees WHICH of its in-neighbours changed with one coalesced byte load per
+// 64 in-edges, without dereferencing the neighbour ids first.
+struct Flags {
+    uint8_t* mark_cur;     // [group][vertex]   frontier of this round (consumed)
+    uint8_t* mark_next;
+    uint8_t* in_cur;       // [group][in-CSR entry] changed in-neighbour (consumed)
+    uint8_t* in_next;
+    int32_t* any_changed;  // set when some vertex changed this round
+};
+
+__global__ __launch_bounds__(BLOCK) void k_seed(int32_t n, int32_t nrel, int32_t groups,
+                                                const int32_t* __restrict__ srcv, DevGraph G, uint8_t* mark,
+                                                uint8_t* in_flags) {
     const int32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= groups * WAVE) return;
     const int32_t s = srcv[i];
     if (s < 0) return;
-    const size_t base = (size_t)(i / WAVE) * n;
-    chg[base + s] = 1;
-    for (int32_t k = G.optr[s]; k < G.optr[s + 1]; ++k) mark[base + G.ocol[k]] = 1;
+    const int32_t g = i / WAVE;
+    for (int32_t k = G.optr[s]; k < G.optr[s + 1]; ++k) {
+        mark[(size_t)g * n + G.ocol[k]] = 1;
+        in_flags[(size_t)g * nrel + G.orev[k]] = 1;
+    }
 }
 
-// marked (group*n + v) -> frontier list; clears the marks and the stale change flags.
-__global__ __launch_bounds__(BLOCK) void k_compact(int64_t total, uint8_t* mark, uint8_t* chg_clear,
-                                                   int32_t* __restrict__ frontier, int32_t* count) {
+__device__ __forceinline__ double readlane_d(double x, int32_t l) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+constexpr int INFLIGHT = 8;   // independent 512-B row gathers in flight per wave
+
+// Lexicographic candidate update (alt, d[u], u) against the running best of one
+// lane.  Ties against the current parent resolve with the parent's CURRENT
+// distance; an offer from the current parent itself (kk == bk) refreshes it.
+struct Best {
+    double bd;     // best alt (= distance)
+    int32_t bk;    // in-CSR index of the parent edge
+    int32_t bu;    // parent vertex (-1: not resolved yet)
+    double bdu;    // parent distance (-1: not resolved yet)
+    bool need;     // the parent's (R, H, F) must be (re)gathered
+};
+
+__device__ __forceinline__ void offer(Best& b, const DevGraph& G, const State& st, size_t gbase, int32_t lane,
+                                      int32_t kk, int32_t u, double du, double alt) {
+    bool better = false;
+    if (alt < b.bd) {
+        better = true;
+    } else if (alt == b.bd) {
+        if (kk == b.bk) {
+            b.need = true;
+            b.bdu = du;
+            b.bu = u;
+        } else {
+            if (b.bu < 0) b.bu = G.icol[b.bk];
+            if (b.bdu < 0.0) b.bdu = st.D[(gbase + b.bu) * WAVE + lane];
+            better = (du < b.bdu) || (du == b.bdu && u < b.bu);
+        }
+    }
+    if (better) {
+        b.bd = alt;
+        b.bk = kk;
+        b.bu = u;
+        b.bdu = du;
+        b.need = true;
+    }
+}
+
+// In-CSR entries [kb, ke) (at most 64) of one vertex, one entry per lane.
+struct Seg {
+    int32_t kb;
+    bool valid;
+    int32_t u_l;    // neighbour id of this lane's entry
+    double w_l;     // relaxation weight of this lane's entry
+};
+
+__device__ __forceinline__ Seg load_segment(int32_t kb, int32_t ke, int32_t lane, const DevGraph& G) {
+    Seg sg;
+    sg.kb = kb;
+    const int32_t k = kb + lane;
+    sg.valid = k < ke;
+    sg.u_l = sg.valid ? G.icol[k] : 0;
+    sg.w_l = sg.valid ? G.iw[k] : 0.0;
+    return sg;
+}
+
+// Candidates of a segment whose in-edge flag is set: rows gathered INFLIGHT at a
+// time, `f(kk, u, du, alt)` called for lanes where it is a valid candidate.
+template <typename F>
+__device__ __forceinline__ void scan_changed(const Seg& sg, uint64_t cm, size_t gbase, int32_t lane, bool active,
+                                             const State& st, F&& f) {
+    while (cm) {
+        int32_t us[INFLIGHT], ks[INFLIGHT];
+        double ws[INFLIGHT], dus[INFLIGHT];
+#pragma unroll
+        for (int q = 0; q < INFLIGHT; ++q) {
+            us[q] = -1;
+            if (cm) {
+                const int32_t b = __builtin_ctzll(cm);
+                cm &= cm - 1;
+                us[q] = __builtin_amdgcn_readlane(sg.u_l, b);
+                ks[q] = sg.kb + b;
+                ws[q] = readlane_d(sg.w_l, b);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < INFLIGHT; ++q)
+            if (us[q] >= 0) dus[q] = st.D[(gbase + us[q]) * WAVE + lane];
+#pragma unroll
+        for (int q = 0; q < INFLIGHT; ++q) {
+            if (us[q] < 0) continue;
+            const double alt = dus[q] + ws[q];
+            if (active && alt > dus[q]) f(ks[q], us[q], dus[q], alt);
+        }
+    }
+}
+
+// Gather the chosen parent's (R, H, F), write the lane's state if it changed.
+__device__ __forceinline__ bool finish_vertex(Best& b, const DevGraph& G, const State& st, size_t gbase,
+                                              int32_t lane, int32_t v, int32_t s, size_t rv, double d_old,
+                                              int32_t p_old) {
+    bool changed = false;
+    if (b.need) {
+        if (b.bu < 0) b.bu = G.icol[b.bk];
+        const size_t ru = (gbase + b.bu) * WAVE + lane;
+        const Route pu = st.RT[ru];
+        Route nr;
+        nr.r = pu.r * G.ia[b.bk];
+        nr.h = pu.h + 1;
+        nr.f = (b.bu == s) ? v : pu.f;
+        if (d_old == INF || b.bd != d_old || b.bk != p_old) {
+            changed = true;
+        } else {   // same parent, same distance: did the parent's route change?
+            const Route old = st.RT[rv];
+            changed = (nr.r != old.r) || (nr.h != old.h) || (nr.f != old.f);
+        }
+        if (changed) {
+            st.D[rv] = b.bd;
+            st.P[rv] = b.bk;
+            st.RT[rv] = nr;
+        }
+    }
+    return __ballot(changed) != 0;
+}
+
+// (group, v) changed: flag its out-edges for the next round.
+__device__ __forceinline__ void mark_out(const DevGraph& G, int32_t g, int32_t n, int32_t v, int32_t lane,
+                                         const Flags& fl) {
+    const int32_t o0 = G.optr[v], o1 = G.optr[v + 1];
+    for (int32_t k = o0 + lane; k < o1; k += WAVE) {
+        fl.mark_next[(size_t)g * n + G.ocol[k]] = 1;
+        fl.in_next[(size_t)g * G.nrel + G.orev[k]] = 1;
+    }
+}
+
+// Relaxation of one light (in-degree <= 64) (group, v) for the 64 sources of
+// the group (lane = source).  Returns the wave-uniform "some lane changed".
+__device__ __forceinline__ bool relax_vertex(int32_t g, int32_t v, int32_t n, int32_t lane,
+                                             const int32_t* __restrict__ srcv, const DevGraph& G,
+                                             const State& st, const Flags& fl) {
+    const size_t gbase = (size_t)g * n;
+    const int32_t s = srcv[g * WAVE + lane];
+    const size_t rv = (gbase + v) * WAVE + lane;
+    const bool active = (s >= 0) && (s != v);
+    const int32_t k0 = G.iptr[v], k1 = G.iptr[v + 1];
+    const Seg sg = load_segment(k0, k1, lane, G);
+    const size_t fo = (size_t)g * G.nrel + k0 + lane;
+    const bool f = sg.valid && fl.in_cur[fo] != 0;
+    const double d_old = st.D[rv];
+    const int32_t p_old = st.P[rv];
+    const uint64_t cm = __ballot(f);
+    if (f) fl.in_cur[fo] = 0;   // consumed
+    Best b{d_old, p_old, -1, -1.0, false};
+    scan_changed(sg, cm, gbase, lane, active, st,
+                 [&](int32_t kk, int32_t u, double du, double alt) { offer(b, G, st, gbase, lane, kk, u, du, alt); });
+    const bool changed = finish_vertex(b, G, st, gbase, lane, v, s, rv, d_old, p_old);
+    if (changed) {
+        if (G.undirected) {   // out-list == in-list, already in registers
+            if (sg.valid) {
+                fl.mark_next[gbase + sg.u_l] = 1;
+                fl.in_next[(size_t)g * G.nrel + G.orev[k0 + lane]] = 1;
+            }
+        } else {
+            mark_out(G, g, n, v, lane, fl);
+        }
+    }
+    return changed;
+}
+
+// One relaxation round over a dense frontier bitmap.  Work unit = 8 consecutive
+// (group, vertex) flags read as one scalar 64-bit word, so marked vertices are
+// spread over the grid's waves (a 64-flag unit would serialise up to 64
+// vertices on one wave).  Heavy vertices (in-degree > 64) stay marked for
+// k_heavy_partial / k_heavy_combine.
+__global__ __launch_bounds__(BLOCK) void k_relax(int64_t total, int32_t n, const int32_t* __restrict__ srcv,
+                                                 DevGraph G, State st, const uint8_t* __restrict__ heavy, Flags fl) {
     const int32_t lane = threadIdx.x & (WAVE - 1);
     const int64_t wave = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
-    for (int64_t base = wave * WAVE; base < total; base += nwaves * WAVE) {
-        const int64_t i = base + lane;
-        bool m = false;
-        if (i < total) {
-            m = mark[i] != 0;
-            if (m) mark[i] = 0;
-            if (chg_clear[i]) chg_clear[i] = 0;
+    const int64_t units = (total + 7) >> 3;   // mark buffers are padded to a multiple of 8 bytes
+    uint64_t* words = reinterpret_cast<uint64_t*>(fl.mark_cur);
+    bool wrote = false;
+    for (int64_t u8 = wave; u8 < units; u8 += nwaves) {
+        const uint64_t wl = words[u8];   // same address in every lane: make it wave-uniform
+        uint64_t w = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(wl >> 32)) << 32) |
+                     (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)wl);
+        if (!w) continue;
+        uint64_t keep = 0;
+        while (w) {
+            const int32_t bit = __builtin_ctzll(w) >> 3;           // byte index 0..7
+            w &= ~(0xFFull << (8 * bit));
+            const int64_t e = u8 * 8 + bit;
+            if (e >= total) break;
+            const int32_t g = (int32_t)(e / n);
+            const int32_t v = (int32_t)(e - (int64_t)g * n);
+            if (heavy[v]) {
+                keep |= 0x01ull << (8 * bit);
+                continue;
+            }
+            wrote |= relax_vertex(g, v, n, lane, srcv, G, st, fl);
         }
-        const uint64_t bal = __ballot(m);
-        if (bal == 0) continue;
-        const int32_t cnt = __popcll(bal);
-        int32_t off = 0;
-        if (lane == 0) off = atomicAdd(count, cnt);
-        off = __shfl(off, 0);
-        const int32_t pre = __popcll(bal & ((1ull << lane) - 1ull));
-        if (m) frontier[off + pre] = (int32_t)i;
+        if (lane == 0) words[u8] = keep;   // consumed (heavy marks kept for the heavy kernels)
+    }
+    if (wrote && lane == 0) *fl.any_changed = 1;   // at most one plain store per wave
+}
+
+// Heavy vertices: their in-neighbour lists are cut into 64-entry segments; one
+// wave per (group, segment) computes the lexicographic best changed candidate
+// of its segment (no comparison with the stored state).
+struct HeavyPlan {
+    int32_t nseg;                 // segments over all heavy vertices
+    int32_t nheavy;
+    const int32_t* seg_vertex;    // [nseg]
+    const int32_t* seg_begin;     // [nseg] in-CSR start of the segment
+    const int32_t* heavy_vertex;  // [nheavy]
+    const int32_t* heavy_seg0;    // [nheavy + 1] segment range of each heavy vertex
+};
+
+struct Partial {                  // [group][segment][lane]
+    double* alt;
+    double* du;
+    int2* uk;                     // (u, k), u = -1: no candidate
+};
+
+__global__ __launch_bounds__(BLOCK) void k_heavy_partial(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
+                                                         DevGraph G, State st, HeavyPlan hp, Partial pp, Flags fl) {
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
+    const int64_t items = (int64_t)groups * hp.nseg;
+    for (int64_t it = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it < items; it += nwaves) {
+        const int32_t g = (int32_t)(it / hp.nseg);
+        const int32_t sgi = (int32_t)(it - (int64_t)g * hp.nseg);
+        const int32_t v = hp.seg_vertex[sgi];
+        const size_t gbase = (size_t)g * n;
+        if (!fl.mark_cur[gbase + v]) continue;
+        const int32_t s = srcv[g * WAVE + lane];
+        const bool active = (s >= 0) && (s != v);
+        const int32_t kb = hp.seg_begin[sgi];
+        const Seg sg = load_segment(kb, min(kb + WAVE, G.iptr[v + 1]), lane, G);
+        const size_t fo = (size_t)g * G.nrel + kb + lane;
+        const bool f = sg.valid && fl.in_cur[fo] != 0;
+        const uint64_t cm = __ballot(f);
+        if (f) fl.in_cur[fo] = 0;
+        double ba = INF, bdu = INF;
+        int32_t bu = -1, bk = -1;
+        scan_changed(sg, cm, gbase, lane, active, st, [&](int32_t kk, int32_t u, double du, double alt) {
+            if (alt < ba || (alt == ba && (du < bdu || (du == bdu && u < bu)))) {
+                ba = alt;
+                bdu = du;
+                bu = u;
+                bk = kk;
+            }
+        });
+        const size_t o = ((size_t)g * hp.nseg + sgi) * WAVE + lane;
+        pp.alt[o] = ba;
+        pp.du[o] = bdu;
+        pp.uk[o] = make_int2(bu, bk);
     }
 }
 
-// One wave per frontier entry (group, v); lane = source of that group.
-__global__ __launch_bounds__(BLOCK) void k_relax(const int32_t* __restrict__ frontier,
-                                                 const int32_t* __restrict__ count_ptr, int32_t n,
-                                                 const int32_t* __restrict__ srcv, DevGraph G, State st,
-                                                 const uint8_t* __restrict__ chg_prev, uint8_t* chg_cur,
-                                                 uint8_t* mark) {
+// Combine the segment partials of each marked heavy (group, v) into its state.
+__global__ __launch_bounds__(BLOCK) void k_heavy_combine(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
+                                                         DevGraph G, State st, HeavyPlan hp, Partial pp, Flags fl) {
     const int32_t lane = threadIdx.x & (WAVE - 1);
-    const int32_t nwaves = (gridDim.x * BLOCK) >> 6;
-    const int32_t cnt = *count_ptr;
-    for (int32_t e = (blockIdx.x * BLOCK + threadIdx.x) >> 6; e < cnt; e += nwaves) {
-        const int32_t idx = __builtin_amdgcn_readfirstlane(frontier[e]);
-        const int32_t g = idx / n;
-        const int32_t v = idx - g * n;
+    const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
+    const int64_t items = (int64_t)groups * hp.nheavy;
+    bool wrote = false;
+    for (int64_t it = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it < items; it += nwaves) {
+        const int32_t g = (int32_t)(it / hp.nheavy);
+        const int32_t h = (int32_t)(it - (int64_t)g * hp.nheavy);
+        const int32_t v = hp.heavy_vertex[h];
         const size_t gbase = (size_t)g * n;
+        if (!fl.mark_cur[gbase + v]) continue;
         const int32_t s = srcv[g * WAVE + lane];
         const size_t rv = (gbase + v) * WAVE + lane;
-        const bool active = (s >= 0) && (s != v);
         const double d_old = st.D[rv];
         const int32_t p_old = st.P[rv];
-        double bd = d_old;
-        int32_t bk = p_old;
-        int32_t bu = -1;        // parent vertex, lazily resolved
-        double bdu = -1.0;      // dist of the parent, lazily resolved
-        bool need = false;
-        const int32_t k0 = G.iptr[v], k1 = G.iptr[v + 1];
-        for (int32_t k = k0; k < k1; ++k) {
-            const int32_t u = G.icol[k];
-            if (!chg_prev[gbase + u]) continue;  // wave-uniform
-            const double w = G.iw[k];
-            const double du = st.D[(gbase + u) * WAVE + lane];
-            const double alt = du + w;
-            if (!active || !(alt > du)) continue;
-            bool better = false;
-            if (alt < bd) {
-                better = true;
-            } else if (alt == bd) {
-                if (k == bk) {
-                    need = true;   // current parent changed state: refresh
-                    bdu = du;
-                    bu = u;
-                } else {
-                    if (bu < 0) bu = G.icol[bk];
-                    if (bdu < 0.0) bdu = st.D[(gbase + bu) * WAVE + lane];
-                    better = (du < bdu) || (du == bdu && u < bu);
-                }
-            }
-            if (better) {
-                bd = alt;
-                bk = k;
-                bu = u;
-                bdu = du;
-                need = true;
-            }
+        Best b{d_old, p_old, -1, -1.0, false};
+        for (int32_t sgi = hp.heavy_seg0[h]; sgi < hp.heavy_seg0[h + 1]; ++sgi) {
+            const size_t o = ((size_t)g * hp.nseg + sgi) * WAVE + lane;
+            const int2 uk = pp.uk[o];
+            if (uk.x >= 0) offer(b, G, st, gbase, lane, uk.y, uk.x, pp.du[o], pp.alt[o]);
         }
-        bool changed = false;
-        if (need) {
-            if (bu < 0) bu = G.icol[bk];
-            const size_t ru = (gbase + bu) * WAVE + lane;
-            const double r_new = st.R[ru] * G.ia[bk];
-            const int2 hu = st.HF[ru];
-            const int2 hf_new = make_int2(hu.x + 1, (bu == s) ? v : hu.y);
-            if (d_old == INF) {
-                changed = true;
-            } else {
-                const int2 hf_old = st.HF[rv];
-                changed = (bd != d_old) || (bk != p_old) || (r_new != st.R[rv]) ||
-                          (hf_new.x != hf_old.x) || (hf_new.y != hf_old.y);
-            }
-            if (changed) {
-                st.D[rv] = bd;
-                st.P[rv] = bk;
-                st.R[rv] = r_new;
-                st.HF[rv] = hf_new;
-            }
-        }
-        if (__ballot(changed)) {
-            if (lane == 0) chg_cur[gbase + v] = 1;
-            const int32_t o0 = G.optr[v], o1 = G.optr[v + 1];
-            for (int32_t k = o0 + lane; k < o1; k += WAVE) mark[gbase + G.ocol[k]] = 1;
+        if (lane == 0) fl.mark_cur[gbase + v] = 0;
+        if (finish_vertex(b, G, st, gbase, lane, v, s, rv, d_old, p_old)) {
+            mark_out(G, g, n, v, lane, fl);
+            wrote = true;
         }
     }
+    if (wrote && lane == 0) *fl.any_changed = 1;
 }
 
 // (s, s) entry: DIRECT self-loop, the row's [s] path, or the SELF rule.
@@ -334,12 +544,12 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t groups, 
                 const size_t rt = (gbase + t) * WAVE + lane;
                 const double d = st.D[rt];
                 if (d < INF) {
-                    const int2 hf = st.HF[rt];
+                    const Route rr = st.RT[rt];
                     const double ft = G.vfac[t];
                     const bool fast = (!has_attr(ft) || ft == 1.0) && !md.multi_rep;
                     if (fast) {
                         L = d;
-                        R = st.R[rt];
+                        R = rr.r;
                     } else {
                         // path-order re-fold, shd-topology.c:1413-1493 (rare: vertex loss on
                         // the target, or multigraph get_eid latencies)
@@ -347,7 +557,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t groups, 
                         double l = 0.0, r = 1.0;
                         if (has_attr(fs)) r *= fs;
                         if (has_attr(ft)) r *= ft;
-                        const int32_t h = hf.x;
+                        const int32_t h = rr.h;
                         for (int32_t i = 1; i <= h; ++i) {
                             int32_t x = t;
                             for (int32_t q = 0; q < h - i; ++q) x = G.icol[st.P[(gbase + x) * WAVE + lane]];
@@ -359,8 +569,8 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t groups, 
                         R = r;
                     }
                     if (L == 0) L = 1;   // shd-topology.c:1833-1837
-                    N = hf.y;
-                    H = hf.x;
+                    N = rr.f;
+                    H = rr.h;
                 }
             }
         }
@@ -464,6 +674,8 @@ struct spe_graph {
     spe::HostGraph hg;
     int32_t device = 0;
     DevGraph dev{};
+    HeavyPlan hp{};
+    const uint8_t* d_heavy = nullptr;
     std::vector<void*> allocs;
 };
 
@@ -481,10 +693,10 @@ struct spe_table {
     std::vector<int32_t> attached;
     // workspace
     State st{};
-    uint8_t* chg[2] = {nullptr, nullptr};
-    uint8_t* mark = nullptr;
-    int32_t* frontier = nullptr;
-    int32_t* counts = nullptr;
+    uint8_t* inflag[2] = {nullptr, nullptr};
+    uint8_t* mark[2] = {nullptr, nullptr};
+    Partial pp{};
+    int32_t* counts = nullptr;   // per round: 1 if any vertex changed
     int32_t max_iters = 0;
     int32_t* d_srcv = nullptr;
     int32_t* h_srcv = nullptr;
@@ -582,9 +794,10 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
     DevGraph& d = g->dev;
     d.n = h.n;
     d.nrel = (int32_t)h.icol.size();
+#define UPBASE d
 #define UP(field, src)                                   \
     do {                                                 \
-        r = dev_upload(g->allocs, src, &d.field);        \
+        r = dev_upload(g->allocs, src, &UPBASE.field);   \
         if (r) {                                         \
             spe_graph_free(g);                           \
             return r;                                    \
@@ -595,16 +808,19 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
     UP(iw, h.iw);
     UP(ia, h.ia);
     UP(iwrep, h.iwrep);
+    UP(orev, h.orev);
     if (h.directed) {
         UP(optr, h.optr);
         UP(ocol, h.ocol);
         UP(owrep, h.owrep);
         UP(oarep, h.oarep);
+        d.undirected = 0;
     } else {
         d.optr = d.iptr;
         d.ocol = d.icol;
         d.owrep = d.iwrep;
         d.oarep = d.ia;
+        d.undirected = 1;
     }
     UP(vfac, h.vfac);
     UP(loop_w, h.loop_w);
@@ -612,6 +828,36 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
     UP(self_w2, h.self_w2);
     UP(self_a2, h.self_a2);
     UP(self_other, h.self_other);
+    {   // heavy-vertex segment plan (in-degree > 64)
+        std::vector<uint8_t> heavy(h.n, 0);
+        std::vector<int32_t> seg_vertex, seg_begin, heavy_vertex, heavy_seg0;
+        for (int32_t v = 0; v < h.n; ++v) {
+            const int32_t k0 = h.iptr[v], k1 = h.iptr[v + 1];
+            if (k1 - k0 <= WAVE) continue;
+            heavy[v] = 1;
+            heavy_vertex.push_back(v);
+            heavy_seg0.push_back((int32_t)seg_vertex.size());
+            for (int32_t k = k0; k < k1; k += WAVE) {
+                seg_vertex.push_back(v);
+                seg_begin.push_back(k);
+            }
+        }
+        heavy_seg0.push_back((int32_t)seg_vertex.size());
+        g->hp.nseg = (int32_t)seg_vertex.size();
+        g->hp.nheavy = (int32_t)heavy_vertex.size();
+#undef UPBASE
+#define UPBASE g->hp
+        UP(seg_vertex, seg_vertex);
+        UP(seg_begin, seg_begin);
+        UP(heavy_vertex, heavy_vertex);
+        UP(heavy_seg0, heavy_seg0);
+#undef UPBASE
+        r = dev_upload(g->allocs, heavy, &g->d_heavy);
+        if (r) {
+            spe_graph_free(g);
+            return r;
+        }
+    }
 #undef UP
     *out = g;
     return SPE_OK;
@@ -718,17 +964,18 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         const size_t se = G * n * WAVE;
         TRY(dev_alloc(t->allocs, &t->st.D, se));
         TRY(dev_alloc(t->allocs, &t->st.P, se));
-        TRY(dev_alloc(t->allocs, &t->st.R, se));
-        TRY(dev_alloc(t->allocs, &t->st.HF, se));
-        TRY(dev_alloc(t->allocs, &t->chg[0], G * n));
-        TRY(dev_alloc(t->allocs, &t->chg[1], G * n));
-        TRY(dev_alloc(t->allocs, &t->mark, G * n));
-        TRY(dev_alloc(t->allocs, &t->frontier, G * n));
+        TRY(dev_alloc(t->allocs, &t->st.RT, se));
+        const size_t nrel = std::max<size_t>(1, g->hg.icol.size());
+        TRY(dev_alloc(t->allocs, &t->inflag[0], G * nrel));
+        TRY(dev_alloc(t->allocs, &t->inflag[1], G * nrel));
+        TRY(dev_alloc(t->allocs, &t->mark[0], (G * n + 8) & ~(size_t)7));
+        TRY(dev_alloc(t->allocs, &t->mark[1], (G * n + 8) & ~(size_t)7));
+        const size_t pe = G * std::max<size_t>(1, (size_t)g->hp.nseg) * WAVE;
+        TRY(dev_alloc(t->allocs, &t->pp.alt, pe));
+        TRY(dev_alloc(t->allocs, &t->pp.du, pe));
+        TRY(dev_alloc(t->allocs, &t->pp.uk, pe));
         t->max_iters = 4 * n + 64;
         TRY(dev_alloc(t->allocs, &t->counts, (size_t)t->max_iters + 2));
-        HIP_TRY(hipMemset(t->chg[0], 0, G * n));
-        HIP_TRY(hipMemset(t->chg[1], 0, G * n));
-        HIP_TRY(hipMemset(t->mark, 0, G * n));
     }
     TRY(dev_alloc(t->allocs, &t->d_srcv, G * WAVE));
     TRY(dev_alloc(t->allocs, &t->d_min, 1));
@@ -781,55 +1028,56 @@ static int resolve_profile(spe_table* t) {
 static int relax_to_convergence(spe_table* t, int32_t groups, hipStream_t s) {
     const spe_graph* g = t->g;
     const int32_t n = g->hg.n;
+    const int32_t nrel = (int32_t)g->hg.icol.size();
     const int64_t total = (int64_t)groups * n;
-    const int relax_grid = 4096;   // persistent-style grid-stride over the frontier
-    const int compact_grid = grid_for(total, BLOCK, 4096);
+    const int relax_grid = grid_for((total + 7) / 8 * WAVE, BLOCK, 2048);   // waves stride over 8-flag units
     HIP_TRY(hipMemsetAsync(t->counts, 0, sizeof(int32_t) * ((size_t)t->max_iters + 2), s));
+    for (int i = 0; i < 2; ++i) {   // consumers clear what they read; this only guards a failed batch
+        HIP_TRY(hipMemsetAsync(t->inflag[i], 0, (size_t)groups * std::max(1, nrel), s));
+        HIP_TRY(hipMemsetAsync(t->mark[i], 0, ((size_t)total + 8) & ~(size_t)7, s));
+    }
     {
         LaunchTimer lt(t, s, SPE_K_INIT);
         k_init_state<<<grid_for(total * WAVE, BLOCK, 8192), BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev.vfac, t->st);
     }
     {
         LaunchTimer lt(t, s, SPE_K_SEED);
-        k_seed<<<(groups * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev, t->chg[0],
-                                                                     t->mark);
+        // the sources "changed in round 0": their out-edges form round 1's frontier
+        k_seed<<<(groups * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(n, nrel, groups, t->d_srcv, g->dev, t->mark[1],
+                                                                     t->inflag[1]);
     }
-    {
-        LaunchTimer lt(t, s, SPE_K_COMPACT);
-        k_compact<<<compact_grid, BLOCK, 0, s>>>(total, t->mark, t->chg[1], t->frontier, t->counts + 1);
-    }
-    // frontier lists alternate between the two halves of one buffer only through
-    // the counts array: relax(it) consumes frontier written by compact(it).
     int32_t it = 1;
     int32_t check_every = 8;
-    int32_t* fr_a = t->frontier;
     for (;;) {
         for (int32_t q = 0; q < check_every; ++q, ++it) {
             if (it > t->max_iters) return fail(SPE_ESTATE, "relaxation did not converge");
-            uint8_t* prev = t->chg[(it - 1) & 1];
-            uint8_t* cur = t->chg[it & 1];
+            Flags fl{t->mark[it & 1], t->mark[(it + 1) & 1], t->inflag[it & 1], t->inflag[(it + 1) & 1],
+                     t->counts + it};
             {
                 LaunchTimer lt(t, s, SPE_K_RELAX);
-                k_relax<<<relax_grid, BLOCK, 0, s>>>(fr_a, t->counts + it, n, t->d_srcv, g->dev, t->st, prev, cur,
-                                                     t->mark);
+                k_relax<<<relax_grid, BLOCK, 0, s>>>(total, n, t->d_srcv, g->dev, t->st, g->d_heavy, fl);
             }
-            // the frontier buffer is rewritten by compact only after relax finished (stream order)
-            {
-                LaunchTimer lt(t, s, SPE_K_COMPACT);
-                k_compact<<<compact_grid, BLOCK, 0, s>>>(total, t->mark, prev, fr_a, t->counts + it + 1);
+            if (g->hp.nheavy > 0) {
+                LaunchTimer lt(t, s, SPE_K_HEAVY);
+                k_heavy_partial<<<grid_for((int64_t)groups * g->hp.nseg * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
+                    groups, n, t->d_srcv, g->dev, t->st, g->hp, t->pp, fl);
+                k_heavy_combine<<<grid_for((int64_t)groups * g->hp.nheavy * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
+                    groups, n, t->d_srcv, g->dev, t->st, g->hp, t->pp, fl);
             }
         }
-        HIP_TRY(hipMemcpyAsync(t->h_counts, t->counts + it, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(t->h_counts, t->counts + it - 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        t->stats.launches += 2 * check_every;
+        t->stats.launches += check_every;
         if (t->h_counts[0] == 0) break;
         check_every = 4;
     }
-    // frontier sizes of this batch (for work accounting)
+    // rounds that changed something (work accounting)
     const int32_t nit = it;
     if ((int32_t)t->h_hist.size() < nit + 1) t->h_hist.resize(nit + 1);
     HIP_TRY(hipMemcpy(t->h_hist.data(), t->counts, sizeof(int32_t) * (nit + 1), hipMemcpyDeviceToHost));
-    for (int32_t i = 1; i <= nit; ++i) t->stats.frontier_total += t->h_hist[i];
+    int32_t active_rounds = 0;
+    for (int32_t i = 1; i <= nit; ++i) active_rounds += t->h_hist[i];
+    t->stats.active_rounds += active_rounds;
     t->stats.iterations += it - 1;
     return SPE_OK;
 }

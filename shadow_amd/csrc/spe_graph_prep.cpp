@@ -138,15 +138,28 @@ int prepare_graph(const spe_graph_desc* d, HostGraph* hg, std::string* err) {
         });
         hg->optr.assign(static_cast<size_t>(n) + 1, 0);
         hg->ocol.resize(idx.size());
+        hg->orev.resize(idx.size());
         hg->owrep.resize(idx.size());
         hg->oarep.resize(idx.size());
         for (size_t i = 0; i < idx.size(); ++i) {
             hg->ocol[i] = to_of[idx[i]];
+            hg->orev[i] = (int32_t)idx[i];
             hg->owrep[i] = hg->iwrep[idx[i]];
             hg->oarep[i] = hg->ia[idx[i]];
             hg->optr[hg->icol[idx[i]] + 1]++;
         }
         for (int32_t v = 0; v < n; ++v) hg->optr[v + 1] += hg->optr[v];
+    } else {
+        // undirected: one CSR serves both directions; the reverse of entry
+        // (x -> y) is the entry of x in y's (sorted) list
+        hg->orev.resize(hg->icol.size());
+        for (int32_t x = 0; x < n; ++x)
+            for (int32_t k = hg->iptr[x]; k < hg->iptr[x + 1]; ++k) {
+                const int32_t y = hg->icol[k];
+                const int32_t* b = hg->icol.data() + hg->iptr[y];
+                const int32_t* e = hg->icol.data() + hg->iptr[y + 1];
+                hg->orev[k] = (int32_t)(std::lower_bound(b, e, x) - hg->icol.data());
+            }
     }
 
     // ---- SELF rule constants and completeness, both over incident(v, OUT)

@@ -26,6 +26,7 @@ struct HostGraph {
     std::vector<double> iwrep;     // latency of the get_eid edge
     // out-CSR (directed only; undirected graphs reuse the in-CSR)
     std::vector<int32_t> optr, ocol;
+    std::vector<int32_t> orev;     // out entry -> in-CSR index of the same (merged) edge
     std::vector<double> owrep, oarep;
     // per vertex
     std::vector<double> vfac;      // 1 - vertex loss, NaN when absent

@@ -11,8 +11,10 @@ called at src/main/routing/shd-topology.c:371):
   * <graph edgedefault="directed|undirected">;
   * the graph attribute ``preferdirectpaths`` is read as a string and is true
     for a case-insensitive prefix "true"/"yes"/"1" (shd-topology.c:745-775);
-  * attribute names match case-insensitively by the canonical prefix
-    (shd-topology.c:178-267): e.g. ``latency`` is found under ``latencyms``.
+  * values are looked up by their exact igraph attribute name ("latency",
+    "packetloss", ...: igraph_cattribute_has_attr / EAN / VAN with the
+    canonical names, shd-topology.c:272-354); the reference's case-insensitive
+    prefix match (:178-267) only drives its type-check warnings.
 """
 from __future__ import annotations
 
@@ -60,8 +62,7 @@ class Topology:
 
 
 def _attr_match(name: str, canonical: str) -> bool:
-    # g_ascii_strncasecmp(name, canonical, len(canonical)) == 0
-    return name[: len(canonical)].lower() == canonical.lower()
+    return name == canonical
 
 
 def load_graphml(source: str, is_text: bool = False) -> Topology:

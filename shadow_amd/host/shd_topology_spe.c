@@ -1,0 +1,931 @@
+/*
+ * shd_topology_spe.c -- the reference's topology API (src/main/routing/
+ * shd-topology.{c,h}) re-hosted on the MI355X path engine (include/spe.h).
+ *
+ * What stays on the host (C, as in the reference):
+ *   GraphML ingest + validation       shd-topology.c:356-384, 550-1195
+ *   host attachment by hints / LPM    shd-topology.c:2077-2413
+ *   IP -> vertex map, packet counters shd-topology.c:1373-1390, shd-path.c:53-56
+ * What moves to the GPU (spe_table_build, once, at the first query):
+ *   every (source, target) row the reference computed lazily per cache miss
+ *   with igraph Dijkstra under the global graphLock (shd-topology.c:1640-1912).
+ * Queries are then lock-free reads of the sealed table's host mirror.
+ *
+ * Semantics differences, all documented in DESIGN.md:
+ *   - per-source rows: (s,t) is always tree_s(s->t).  The reference returns
+ *     whichever of tree_s(s->t) / tree_t(t->s) was cached first (first-writer
+ *     wins, shd-topology.c:1292-1321) -- identical values whenever both rows
+ *     agree, which is every DIRECT pair and every undirected pair whose
+ *     forward/backward sums round the same.
+ *   - (s,s) uses the row's [s] path when s has a self-loop (SPE_SELF_ROW).
+ */
+#include "shd_topology_spe.h"
+
+#include <arpa/inet.h>
+#include <math.h>
+#include <netinet/in.h>
+#include <pthread.h>
+#include <stdarg.h>
+#include <stdatomic.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <strings.h>
+#include <time.h>
+
+#include <libxml/parser.h>
+#include <libxml/tree.h>
+
+#include "spe.h"
+
+enum { LOG_ERROR = 0, LOG_CRITICAL, LOG_WARNING, LOG_MESSAGE, LOG_INFO, LOG_DEBUG };
+
+/* vertex string / numeric attributes the reference reads, by exact name */
+enum { VS_ID = 0, VS_IP, VS_CITYCODE, VS_COUNTRYCODE, VS_GEOCODE, VS_TYPE, VS_COUNT };
+enum { VN_BWDOWN = 0, VN_BWUP, VN_PACKETLOSS, VN_ASN, VN_COUNT };
+static const char* VS_NAMES[VS_COUNT] = {"id", "ip", "citycode", "countrycode", "geocode", "type"};
+static const char* VN_NAMES[VN_COUNT] = {"bandwidthdown", "bandwidthup", "packetloss", "asn"};
+
+typedef struct {
+    uint64_t key;   /* (s_slot << 32 | t_slot) + 1, 0 = empty */
+    _Atomic uint64_t count;
+} PairCount;
+
+struct _Topology {
+    int32_t device;
+    int32_t n;
+    int64_t m;
+    int32_t directed;
+    int32_t prefer_direct;
+    /* graph, edge list form (GraphML order) */
+    int32_t *esrc, *edst;
+    double *elat, *eloss;
+    char** vstr[VS_COUNT];     /* NULL array = attribute absent from the graph */
+    double* vnum[VN_COUNT];
+    spe_graph* graph;
+
+    /* attachment: ip -> vertex (open addressing), vertex -> slot */
+    pthread_rwlock_t ip_lock;
+    uint32_t* ip_keys;
+    int32_t* ip_vals;
+    uint8_t* ip_used;
+    size_t ip_cap, ip_size;
+    int32_t* slot_of_vertex;
+    int32_t* attached;          /* slot -> vertex, in first-attach order */
+    int32_t n_attached;
+
+    /* sealed table (host mirror) */
+    pthread_mutex_t seal_lock;
+    _Atomic int sealed;
+    spe_table* table;
+    int32_t A;
+    double* lat;                /* [A][A] row-major */
+    double* rel;
+    double min_latency;
+    double build_seconds;
+    int64_t build_rows;
+
+    /* per-pair packet counters (shd-path.c:53-56), lock-free insert */
+    PairCount* counts;
+    size_t counts_cap;
+
+    topology_log_fn log_fn;
+    void* log_ctx;
+    topology_min_latency_fn minlat_fn;
+    void* minlat_ctx;
+};
+
+static void tlog(Topology* top, int level, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (top && top->log_fn) top->log_fn(level, buf, top->log_ctx);
+    else if (level <= LOG_WARNING) fprintf(stderr, "[shd-topology-spe] %s\n", buf);
+}
+
+/* ------------------------------------------------------------ GraphML */
+
+typedef struct {
+    char* id;
+    char* name;
+    int numeric;   /* attr.type int/long/float/double */
+    int for_;      /* 0 graph, 1 node, 2 edge, 3 all */
+    char* def;
+} GKey;
+
+static char* xstrdup(const xmlChar* s) { return s ? strdup((const char*)s) : NULL; }
+
+static double parse_num(const char* s) {
+    if (!s) return NAN;
+    while (*s == ' ' || *s == '\t' || *s == '\n' || *s == '\r') s++;
+    if (*s == '\0') return NAN;
+    return strtod(s, NULL);
+}
+
+static int key_for(const char* f) {
+    if (!f || !strcmp(f, "all")) return 3;
+    if (!strcmp(f, "graph")) return 0;
+    if (!strcmp(f, "node")) return 1;
+    if (!strcmp(f, "edge")) return 2;
+    return 3;
+}
+
+/* vertex index = order of first reference (igraph's GraphML id trie) */
+typedef struct {
+    char** names;
+    size_t n, cap;
+    char** hkeys;
+    int32_t* hvals;
+    size_t hcap;
+} NameMap;
+
+static uint64_t hash_str(const char* s) {
+    uint64_t h = 1469598103934665603ull;
+    for (; *s; ++s) h = (h ^ (uint8_t)*s) * 1099511628211ull;
+    return h;
+}
+
+static int32_t name_index(NameMap* nm, const char* name) {
+    if (nm->n * 2 + 2 > nm->hcap) {
+        size_t nc = nm->hcap ? nm->hcap * 2 : 1024;
+        char** nk = calloc(nc, sizeof(char*));
+        int32_t* nv = calloc(nc, sizeof(int32_t));
+        for (size_t i = 0; i < nm->hcap; ++i)
+            if (nm->hkeys[i]) {
+                size_t j = hash_str(nm->hkeys[i]) & (nc - 1);
+                while (nk[j]) j = (j + 1) & (nc - 1);
+                nk[j] = nm->hkeys[i];
+                nv[j] = nm->hvals[i];
+            }
+        free(nm->hkeys);
+        free(nm->hvals);
+        nm->hkeys = nk;
+        nm->hvals = nv;
+        nm->hcap = nc;
+    }
+    size_t j = hash_str(name) & (nm->hcap - 1);
+    while (nm->hkeys[j]) {
+        if (!strcmp(nm->hkeys[j], name)) return nm->hvals[j];
+        j = (j + 1) & (nm->hcap - 1);
+    }
+    if (nm->n == nm->cap) {
+        nm->cap = nm->cap ? nm->cap * 2 : 1024;
+        nm->names = realloc(nm->names, nm->cap * sizeof(char*));
+    }
+    char* copy = strdup(name);
+    nm->names[nm->n] = copy;
+    nm->hkeys[j] = copy;
+    nm->hvals[j] = (int32_t)nm->n;
+    return (int32_t)nm->n++;
+}
+
+typedef struct {
+    int32_t v;
+    xmlNode* el;
+} NodeRef;
+
+static int load_graphml(Topology* top, const char* path) {
+    xmlDoc* doc = xmlReadFile(path, NULL, XML_PARSE_NONET | XML_PARSE_HUGE | XML_PARSE_NOBLANKS);
+    if (!doc) {
+        tlog(top, LOG_CRITICAL, "unable to parse graphml file '%s'", path);
+        return 0;
+    }
+    xmlNode* root = xmlDocGetRootElement(doc);
+    GKey* keys = NULL;
+    size_t nkeys = 0, capkeys = 0;
+    xmlNode* graph = NULL;
+    for (xmlNode* c = root ? root->children : NULL; c; c = c->next) {
+        if (c->type != XML_ELEMENT_NODE) continue;
+        if (!xmlStrcmp(c->name, (const xmlChar*)"key")) {
+            if (nkeys == capkeys) {
+                capkeys = capkeys ? capkeys * 2 : 16;
+                keys = realloc(keys, capkeys * sizeof(GKey));
+            }
+            GKey* k = &keys[nkeys++];
+            memset(k, 0, sizeof *k);
+            xmlChar* a = xmlGetProp(c, (const xmlChar*)"id");
+            k->id = xstrdup(a);
+            xmlFree(a);
+            a = xmlGetProp(c, (const xmlChar*)"attr.name");
+            k->name = xstrdup(a);
+            xmlFree(a);
+            a = xmlGetProp(c, (const xmlChar*)"attr.type");
+            k->numeric = a && (!xmlStrcmp(a, (const xmlChar*)"int") || !xmlStrcmp(a, (const xmlChar*)"long") ||
+                               !xmlStrcmp(a, (const xmlChar*)"float") || !xmlStrcmp(a, (const xmlChar*)"double"));
+            xmlFree(a);
+            a = xmlGetProp(c, (const xmlChar*)"for");
+            k->for_ = key_for((const char*)a);
+            xmlFree(a);
+            for (xmlNode* d = c->children; d; d = d->next)
+                if (d->type == XML_ELEMENT_NODE && !xmlStrcmp(d->name, (const xmlChar*)"default")) {
+                    xmlChar* t = xmlNodeGetContent(d);
+                    k->def = xstrdup(t);
+                    xmlFree(t);
+                }
+        } else if (!xmlStrcmp(c->name, (const xmlChar*)"graph") && !graph) {
+            graph = c;
+        }
+    }
+    int ok = 1;
+    if (!graph) {
+        tlog(top, LOG_CRITICAL, "graphml file '%s' has no <graph>", path);
+        ok = 0;
+        goto out;
+    }
+    {
+        xmlChar* ed = xmlGetProp(graph, (const xmlChar*)"edgedefault");
+        top->directed = !(ed && !xmlStrcmp(ed, (const xmlChar*)"undirected"));
+        xmlFree(ed);
+    }
+    /* first pass: vertex ids, edge count, graph data */
+    NameMap nm;
+    memset(&nm, 0, sizeof nm);
+    size_t ne = 0, ncap = 0;
+    NodeRef* nodes = NULL;
+    size_t nn = 0;
+    const char* pref_val = NULL;
+    char* pref_key = NULL;
+    for (size_t i = 0; i < nkeys; ++i)
+        if (keys[i].name && (keys[i].for_ == 0 || keys[i].for_ == 3) && !strcmp(keys[i].name, "preferdirectpaths"))
+            pref_key = keys[i].id;
+    xmlChar* pref_text = NULL;
+    for (xmlNode* c = graph->children; c; c = c->next) {
+        if (c->type != XML_ELEMENT_NODE) continue;
+        if (!xmlStrcmp(c->name, (const xmlChar*)"node")) {
+            xmlChar* id = xmlGetProp(c, (const xmlChar*)"id");
+            int32_t v = name_index(&nm, id ? (const char*)id : "");
+            xmlFree(id);
+            if (nn == ncap) {
+                ncap = ncap ? ncap * 2 : 1024;
+                nodes = realloc(nodes, ncap * sizeof(NodeRef));
+            }
+            nodes[nn].v = v;
+            nodes[nn].el = c;
+            nn++;
+        } else if (!xmlStrcmp(c->name, (const xmlChar*)"edge")) {
+            xmlChar* s = xmlGetProp(c, (const xmlChar*)"source");
+            xmlChar* t = xmlGetProp(c, (const xmlChar*)"target");
+            name_index(&nm, s ? (const char*)s : "");
+            name_index(&nm, t ? (const char*)t : "");
+            xmlFree(s);
+            xmlFree(t);
+            ne++;
+        } else if (!xmlStrcmp(c->name, (const xmlChar*)"data") && pref_key) {
+            xmlChar* k = xmlGetProp(c, (const xmlChar*)"key");
+            if (k && !strcmp((const char*)k, pref_key)) {
+                if (pref_text) xmlFree(pref_text);
+                pref_text = xmlNodeGetContent(c);
+            }
+            xmlFree(k);
+        }
+    }
+    if (pref_text) pref_val = (const char*)pref_text;
+    else if (pref_key)
+        for (size_t i = 0; i < nkeys; ++i)
+            if (keys[i].id == pref_key) pref_val = keys[i].def;
+    /* preferdirectpaths: string, true/yes/1 prefix (shd-topology.c:754-775) */
+    top->prefer_direct = pref_val && (!strncasecmp(pref_val, "true", 4) || !strncasecmp(pref_val, "yes", 3) ||
+                                      !strncasecmp(pref_val, "1", 1));
+    if (pref_text) xmlFree(pref_text);
+
+    const int32_t n = (int32_t)nm.n;
+    top->n = n;
+    top->m = (int64_t)ne;
+    top->esrc = malloc((ne ? ne : 1) * sizeof(int32_t));
+    top->edst = malloc((ne ? ne : 1) * sizeof(int32_t));
+    top->elat = malloc((ne ? ne : 1) * sizeof(double));
+    top->eloss = malloc((ne ? ne : 1) * sizeof(double));
+    /* vertex attributes: keys by exact attr.name (igraph attribute names) */
+    int vs_key[VS_COUNT], vn_key[VN_COUNT];
+    for (int a = 0; a < VS_COUNT; ++a) vs_key[a] = -1;
+    for (int a = 0; a < VN_COUNT; ++a) vn_key[a] = -1;
+    for (size_t i = 0; i < nkeys; ++i) {
+        if (!keys[i].name || !(keys[i].for_ == 1 || keys[i].for_ == 3)) continue;
+        for (int a = 1; a < VS_COUNT; ++a)
+            if (!strcmp(keys[i].name, VS_NAMES[a])) vs_key[a] = (int)i;
+        for (int a = 0; a < VN_COUNT; ++a)
+            if (!strcmp(keys[i].name, VN_NAMES[a])) vn_key[a] = (int)i;
+    }
+    top->vstr[VS_ID] = calloc((size_t)n + 1, sizeof(char*));
+    for (int32_t v = 0; v < n; ++v) top->vstr[VS_ID][v] = strdup(nm.names[v]);
+    for (int a = 1; a < VS_COUNT; ++a)
+        if (vs_key[a] >= 0) {
+            top->vstr[a] = calloc((size_t)n + 1, sizeof(char*));
+            for (int32_t v = 0; v < n; ++v)
+                top->vstr[a][v] = strdup(keys[vs_key[a]].def ? keys[vs_key[a]].def : "");
+        }
+    for (int a = 0; a < VN_COUNT; ++a)
+        if (vn_key[a] >= 0) {
+            top->vnum[a] = malloc(((size_t)n + 1) * sizeof(double));
+            const double d = parse_num(keys[vn_key[a]].def);
+            for (int32_t v = 0; v < n; ++v) top->vnum[a][v] = d;
+        }
+    for (size_t i = 0; i < nn; ++i) {
+        const int32_t v = nodes[i].v;
+        for (xmlNode* d = nodes[i].el->children; d; d = d->next) {
+            if (d->type != XML_ELEMENT_NODE || xmlStrcmp(d->name, (const xmlChar*)"data")) continue;
+            xmlChar* k = xmlGetProp(d, (const xmlChar*)"key");
+            xmlChar* txt = xmlNodeGetContent(d);
+            for (int a = 1; a < VS_COUNT; ++a)
+                if (vs_key[a] >= 0 && k && !strcmp((const char*)k, keys[vs_key[a]].id)) {
+                    free(top->vstr[a][v]);
+                    top->vstr[a][v] = strdup(txt ? (const char*)txt : "");
+                }
+            for (int a = 0; a < VN_COUNT; ++a)
+                if (vn_key[a] >= 0 && k && !strcmp((const char*)k, keys[vn_key[a]].id))
+                    top->vnum[a][v] = parse_num((const char*)txt);
+            xmlFree(k);
+            xmlFree(txt);
+        }
+    }
+    /* edges: latency / packetloss / jitter by exact name */
+    int ek_lat = -1, ek_loss = -1, ek_jit = -1;
+    for (size_t i = 0; i < nkeys; ++i) {
+        if (!keys[i].name || !(keys[i].for_ == 2 || keys[i].for_ == 3)) continue;
+        if (!strcmp(keys[i].name, "latency")) ek_lat = (int)i;
+        if (!strcmp(keys[i].name, "packetloss")) ek_loss = (int)i;
+        if (!strcmp(keys[i].name, "jitter")) ek_jit = (int)i;
+    }
+    /* required attributes are defined on the graph (shd-topology.c:634-690) */
+    if (vn_key[VN_BWDOWN] < 0 || vn_key[VN_BWUP] < 0) {
+        tlog(top, LOG_WARNING, "vertex attributes 'bandwidthdown' and 'bandwidthup' are required");
+        ok = 0;
+    }
+    if (ek_lat < 0 || ek_loss < 0) {
+        tlog(top, LOG_WARNING, "edge attributes 'latency' and 'packetloss' are required");
+        ok = 0;
+    }
+    size_t e = 0;
+    for (xmlNode* c = graph->children; c; c = c->next) {
+        if (c->type != XML_ELEMENT_NODE || xmlStrcmp(c->name, (const xmlChar*)"edge")) continue;
+        xmlChar* s = xmlGetProp(c, (const xmlChar*)"source");
+        xmlChar* t = xmlGetProp(c, (const xmlChar*)"target");
+        top->esrc[e] = name_index(&nm, s ? (const char*)s : "");
+        top->edst[e] = name_index(&nm, t ? (const char*)t : "");
+        xmlFree(s);
+        xmlFree(t);
+        double lat = ek_lat >= 0 ? parse_num(keys[ek_lat].def) : NAN;
+        double loss = ek_loss >= 0 ? parse_num(keys[ek_loss].def) : NAN;
+        double jit = ek_jit >= 0 ? parse_num(keys[ek_jit].def) : NAN;
+        for (xmlNode* d = c->children; d; d = d->next) {
+            if (d->type != XML_ELEMENT_NODE || xmlStrcmp(d->name, (const xmlChar*)"data")) continue;
+            xmlChar* k = xmlGetProp(d, (const xmlChar*)"key");
+            xmlChar* txt = xmlNodeGetContent(d);
+            if (k && ek_lat >= 0 && !strcmp((const char*)k, keys[ek_lat].id)) lat = parse_num((const char*)txt);
+            if (k && ek_loss >= 0 && !strcmp((const char*)k, keys[ek_loss].id)) loss = parse_num((const char*)txt);
+            if (k && ek_jit >= 0 && !strcmp((const char*)k, keys[ek_jit].id)) jit = parse_num((const char*)txt);
+            xmlFree(k);
+            xmlFree(txt);
+        }
+        /* _topology_checkGraphEdgesHelperHook, shd-topology.c:1026-1109 */
+        if (!(lat > 0.0)) {
+            tlog(top, LOG_WARNING, "required attribute 'latency' on edge %zu is non-positive, missing or NAN", e);
+            ok = 0;
+        }
+        if (!(loss >= 0.0 && loss <= 1.0)) {
+            tlog(top, LOG_WARNING, "required attribute 'packetloss' on edge %zu is out of range or missing", e);
+            ok = 0;
+        }
+        if (!isnan(jit) && !(jit >= 0.0)) {
+            tlog(top, LOG_WARNING, "optional attribute 'jitter' on edge %zu is negative", e);
+            ok = 0;
+        }
+        top->elat[e] = lat;
+        top->eloss[e] = loss;
+        e++;
+    }
+    /* _topology_checkGraphVerticesHelperHook, shd-topology.c:796-963 */
+    for (int32_t v = 0; v < n && ok; ++v) {
+        if (!(top->vnum[VN_BWDOWN][v] > 0.0) || !(top->vnum[VN_BWUP][v] > 0.0)) {
+            tlog(top, LOG_WARNING, "required bandwidth attribute on vertex %d ('%s') is NAN or negative", v,
+                 top->vstr[VS_ID][v]);
+            ok = 0;
+        }
+        if (top->vnum[VN_ASN] && !isnan(top->vnum[VN_ASN][v]) && !(top->vnum[VN_ASN][v] > 0.0)) {
+            tlog(top, LOG_WARNING, "optional attribute 'asn' on vertex %d is non-positive", v);
+            ok = 0;
+        }
+        const double pl = top->vnum[VN_PACKETLOSS] ? top->vnum[VN_PACKETLOSS][v] : NAN;
+        if (!isnan(pl) && !(pl >= 0.0 && pl <= 1.0)) {
+            tlog(top, LOG_WARNING, "optional attribute 'packetloss' on vertex %d is out of range [0.0,1.0]", v);
+            ok = 0;
+        }
+    }
+    free(nodes);
+    for (size_t i = 0; i < nm.n; ++i) free(nm.names[i]);
+    free(nm.names);
+    free(nm.hkeys);
+    free(nm.hvals);
+out:
+    for (size_t i = 0; i < nkeys; ++i) {
+        free(keys[i].id);
+        free(keys[i].name);
+        free(keys[i].def);
+    }
+    free(keys);
+    xmlFreeDoc(doc);
+    return ok;
+}
+
+/* one strong component (igraph_is_connected STRONG + clusters == 1, :723-791) */
+static int strongly_connected(const Topology* top) {
+    const int32_t n = top->n;
+    if (n <= 1) return 1;
+    int32_t* deg = calloc((size_t)n + 1, sizeof(int32_t));
+    int32_t* rdeg = calloc((size_t)n + 1, sizeof(int32_t));
+    for (int64_t e = 0; e < top->m; ++e) {
+        deg[top->esrc[e] + 1]++;
+        rdeg[top->edst[e] + 1]++;
+        if (!top->directed) {
+            deg[top->edst[e] + 1]++;
+            rdeg[top->esrc[e] + 1]++;
+        }
+    }
+    for (int32_t v = 0; v < n; ++v) {
+        deg[v + 1] += deg[v];
+        rdeg[v + 1] += rdeg[v];
+    }
+    int32_t* adj = malloc(((size_t)deg[n] + 1) * sizeof(int32_t));
+    int32_t* radj = malloc(((size_t)rdeg[n] + 1) * sizeof(int32_t));
+    int32_t* fill = calloc((size_t)n, sizeof(int32_t));
+    int32_t* rfill = calloc((size_t)n, sizeof(int32_t));
+    for (int64_t e = 0; e < top->m; ++e) {
+        const int32_t a = top->esrc[e], b = top->edst[e];
+        adj[deg[a] + fill[a]++] = b;
+        radj[rdeg[b] + rfill[b]++] = a;
+        if (!top->directed) {
+            adj[deg[b] + fill[b]++] = a;
+            radj[rdeg[a] + rfill[a]++] = b;
+        }
+    }
+    int32_t* stack = malloc((size_t)n * sizeof(int32_t));
+    uint8_t* seen = calloc((size_t)n, 1);
+    int ok = 1;
+    for (int pass = 0; pass < 2 && ok; ++pass) {
+        const int32_t* P = pass ? rdeg : deg;
+        const int32_t* E = pass ? radj : adj;
+        memset(seen, 0, (size_t)n);
+        int32_t sp = 0, cnt = 1;
+        stack[sp++] = 0;
+        seen[0] = 1;
+        while (sp) {
+            const int32_t x = stack[--sp];
+            for (int32_t k = P[x]; k < P[x + 1]; ++k)
+                if (!seen[E[k]]) {
+                    seen[E[k]] = 1;
+                    cnt++;
+                    stack[sp++] = E[k];
+                }
+        }
+        ok = cnt == n;
+    }
+    free(deg); free(rdeg); free(adj); free(radj); free(fill); free(rfill); free(stack); free(seen);
+    return ok;
+}
+
+/* --------------------------------------------------------- lifecycle */
+
+static void topo_release(Topology* top) {
+    if (!top) return;
+    if (top->table) spe_table_free(top->table);
+    if (top->graph) spe_graph_free(top->graph);
+    for (int a = 0; a < VS_COUNT; ++a)
+        if (top->vstr[a]) {
+            for (int32_t v = 0; v < top->n; ++v) free(top->vstr[a][v]);
+            free(top->vstr[a]);
+        }
+    for (int a = 0; a < VN_COUNT; ++a) free(top->vnum[a]);
+    free(top->esrc); free(top->edst); free(top->elat); free(top->eloss);
+    free(top->ip_keys); free(top->ip_vals); free(top->ip_used);
+    free(top->slot_of_vertex); free(top->attached);
+    free(top->lat); free(top->rel); free(top->counts);
+    pthread_rwlock_destroy(&top->ip_lock);
+    pthread_mutex_destroy(&top->seal_lock);
+    free(top);
+}
+
+Topology* topology_new_on_device(const char* graphPath, int32_t device) {
+    if (!graphPath) return NULL;
+    Topology* top = calloc(1, sizeof(Topology));
+    top->device = device;
+    pthread_rwlock_init(&top->ip_lock, NULL);
+    pthread_mutex_init(&top->seal_lock, NULL);
+    tlog(top, LOG_MESSAGE, "reading graphml topology graph at '%s'...", graphPath);
+    if (!load_graphml(top, graphPath) || !strongly_connected(top)) {
+        tlog(top, LOG_CRITICAL, "we failed to create the simulation topology because we were unable to "
+                                "validate the topology graphml file");
+        topo_release(top);
+        return NULL;
+    }
+    double* vloss = top->vnum[VN_PACKETLOSS];
+    double* nanv = NULL;
+    if (!vloss) {
+        nanv = malloc(((size_t)top->n + 1) * sizeof(double));
+        for (int32_t v = 0; v < top->n; ++v) nanv[v] = NAN;
+    }
+    spe_graph_desc d = {top->n, top->m, top->esrc, top->edst, top->elat, top->eloss, vloss ? vloss : nanv,
+                        top->directed, top->prefer_direct};
+    const int rc = spe_graph_create(&d, device, &top->graph);
+    free(nanv);
+    if (rc != SPE_OK) {
+        tlog(top, LOG_CRITICAL, "spe_graph_create failed: %s", spe_last_error());
+        topo_release(top);
+        return NULL;
+    }
+    spe_graph_info info;
+    spe_graph_info_get(top->graph, &info);
+    tlog(top, LOG_MESSAGE, "topology graph is %s, %s, and strongly connected with 1 cluster. It does%s prefer "
+                           "direct paths.", info.complete ? "complete" : "incomplete",
+         top->directed ? "directed" : "undirected", top->prefer_direct ? "" : " not");
+    top->ip_cap = 1024;
+    top->ip_keys = calloc(top->ip_cap, sizeof(uint32_t));
+    top->ip_vals = calloc(top->ip_cap, sizeof(int32_t));
+    top->ip_used = calloc(top->ip_cap, 1);
+    top->slot_of_vertex = malloc(((size_t)top->n + 1) * sizeof(int32_t));
+    for (int32_t v = 0; v < top->n; ++v) top->slot_of_vertex[v] = -1;
+    top->attached = malloc(((size_t)top->n + 1) * sizeof(int32_t));
+    return top;
+}
+
+Topology* topology_new(const char* graphPath) { return topology_new_on_device(graphPath, 0); }
+
+void topology_set_log_callback(Topology* top, topology_log_fn fn, void* ctx) {
+    if (!top) return;
+    top->log_fn = fn;
+    top->log_ctx = ctx;
+}
+
+void topology_set_min_latency_callback(Topology* top, topology_min_latency_fn fn, void* ctx) {
+    if (!top) return;
+    top->minlat_fn = fn;
+    top->minlat_ctx = ctx;
+}
+
+int32_t topology_vertex_count(const Topology* top) { return top ? top->n : 0; }
+
+/* ----------------------------------------------------- IP -> vertex map */
+
+static uint64_t hash_ip(uint32_t ip) { return (uint64_t)ip * 0x9E3779B97F4A7C15ull; }
+
+static void ip_put(Topology* top, uint32_t ip, int32_t v) {
+    if ((top->ip_size + 1) * 2 > top->ip_cap) {
+        size_t nc = top->ip_cap * 2;
+        uint32_t* nk = calloc(nc, sizeof(uint32_t));
+        int32_t* nv = calloc(nc, sizeof(int32_t));
+        uint8_t* nu = calloc(nc, 1);
+        for (size_t i = 0; i < top->ip_cap; ++i)
+            if (top->ip_used[i] == 1) {
+                size_t j = hash_ip(top->ip_keys[i]) & (nc - 1);
+                while (nu[j]) j = (j + 1) & (nc - 1);
+                nk[j] = top->ip_keys[i];
+                nv[j] = top->ip_vals[i];
+                nu[j] = 1;
+            }
+        free(top->ip_keys); free(top->ip_vals); free(top->ip_used);
+        top->ip_keys = nk;
+        top->ip_vals = nv;
+        top->ip_used = nu;
+        top->ip_cap = nc;
+    }
+    size_t j = hash_ip(ip) & (top->ip_cap - 1);
+    while (top->ip_used[j]) {
+        if (top->ip_used[j] == 1 && top->ip_keys[j] == ip) {
+            top->ip_vals[j] = v;
+            return;
+        }
+        j = (j + 1) & (top->ip_cap - 1);
+    }
+    top->ip_used[j] = 1;
+    top->ip_keys[j] = ip;
+    top->ip_vals[j] = v;
+    top->ip_size++;
+}
+
+static int32_t ip_get(Topology* top, uint32_t ip) {
+    size_t j = hash_ip(ip) & (top->ip_cap - 1);
+    while (top->ip_used[j]) {
+        if (top->ip_used[j] == 1 && top->ip_keys[j] == ip) return top->ip_vals[j];
+        j = (j + 1) & (top->ip_cap - 1);
+    }
+    return -1;
+}
+
+static void ip_del(Topology* top, uint32_t ip) {
+    size_t j = hash_ip(ip) & (top->ip_cap - 1);
+    while (top->ip_used[j]) {
+        if (top->ip_used[j] == 1 && top->ip_keys[j] == ip) {
+            top->ip_used[j] = 2;   /* tombstone */
+            return;
+        }
+        j = (j + 1) & (top->ip_cap - 1);
+    }
+}
+
+int32_t topology_attached_vertex(const Topology* top, spe_in_addr_t address) {
+    if (!top) return -1;
+    pthread_rwlock_rdlock((pthread_rwlock_t*)&top->ip_lock);
+    const int32_t v = ip_get((Topology*)top, address);
+    pthread_rwlock_unlock((pthread_rwlock_t*)&top->ip_lock);
+    return v;
+}
+
+/* ---------------------------------------------------------- attachment */
+
+static uint32_t string_to_ip(const char* s) {   /* address_stringToIP, shd-address.c:137-144 */
+    struct in_addr a;
+    if (s && inet_pton(AF_INET, s, &a) == 1) return a.s_addr;
+    return INADDR_NONE;
+}
+
+typedef struct {
+    int32_t* q;
+    size_t n;
+    uint32_t nips;
+} Cand;
+
+static void cand_push(Cand* c, int32_t v, int usable, size_t cap) {
+    if (!c->q) c->q = malloc(cap * sizeof(int32_t));
+    c->q[c->n++] = v;
+    if (usable) c->nips++;
+}
+
+static int str_match(const char* attr, const char* hint) {   /* found && hint && !g_ascii_strcasecmp */
+    return attr && attr[0] != '\0' && hint && !strcasecmp(attr, hint);
+}
+
+/* _topology_findAttachmentVertex + hook, shd-topology.c:2077-2352 */
+static int32_t find_attachment_vertex(Topology* top, topology_random_fn rnd, void* rctx, const char* ipHint,
+                                      const char* cityHint, const char* countryHint, const char* geoHint,
+                                      const char* typeHint) {
+    enum { C_CITYTYPE = 0, C_CITY, C_COUNTRYTYPE, C_COUNTRY, C_GEOTYPE, C_GEO, C_TYPE, C_ALL, C_N };
+    Cand c[C_N];
+    memset(c, 0, sizeof c);
+    const size_t cap = (size_t)top->n + 1;
+    int requestedUsable = 0, foundExact = 0;
+    uint32_t requestedIP = 0;
+    if (ipHint) {
+        const uint32_t ip = string_to_ip(ipHint);
+        if (ip != INADDR_NONE && ip != INADDR_ANY && ip != INADDR_LOOPBACK) {
+            requestedUsable = 1;
+            requestedIP = ip;
+        }
+    }
+    for (int32_t v = 0; v < top->n; ++v) {
+        const char* ipS = top->vstr[VS_IP] ? top->vstr[VS_IP][v] : NULL;
+        const char* city = top->vstr[VS_CITYCODE] ? top->vstr[VS_CITYCODE][v] : NULL;
+        const char* country = top->vstr[VS_COUNTRYCODE] ? top->vstr[VS_COUNTRYCODE][v] : NULL;
+        const char* geo = top->vstr[VS_GEOCODE] ? top->vstr[VS_GEOCODE][v] : NULL;
+        const char* type = top->vstr[VS_TYPE] ? top->vstr[VS_TYPE][v] : NULL;
+        const int cityM = str_match(city, cityHint), countryM = str_match(country, countryHint);
+        const int geoM = str_match(geo, geoHint), typeM = str_match(type, typeHint);
+        int usable = 0;
+        uint32_t vip = INADDR_NONE;
+        if (ipS && ipS[0] != '\0') {
+            const uint32_t ip = string_to_ip(ipS);
+            if (ip != INADDR_NONE && ip != INADDR_ANY && ip != INADDR_LOOPBACK) {
+                usable = 1;
+                vip = ip;
+            }
+        }
+        if (requestedUsable && usable && vip == requestedIP) {
+            if (!foundExact)   /* g_queue_clear on every queue; the numIPs counters are kept */
+                for (int i = 0; i < C_N; ++i) c[i].n = 0;
+            foundExact = 1;
+            cand_push(&c[C_ALL], v, usable, cap);
+        }
+        if (foundExact) continue;
+        cand_push(&c[C_ALL], v, usable, cap);
+        if (cityM && typeM) cand_push(&c[C_CITYTYPE], v, usable, cap);
+        if (cityM) cand_push(&c[C_CITY], v, usable, cap);
+        if (countryM && typeM) cand_push(&c[C_COUNTRYTYPE], v, usable, cap);
+        if (countryM) cand_push(&c[C_COUNTRY], v, usable, cap);
+        if (geoM && typeM) cand_push(&c[C_GEOTYPE], v, usable, cap);
+        if (geoM) cand_push(&c[C_GEO], v, usable, cap);
+        if (typeM) cand_push(&c[C_TYPE], v, usable, cap);
+    }
+    Cand* pick = NULL;
+    int lpm = 0;
+    for (int i = 0; i < C_ALL && !pick; ++i)
+        if (c[i].n > 0) {
+            pick = &c[i];
+            lpm = requestedUsable && c[i].nips > 0;
+        }
+    if (!pick) {
+        pick = &c[C_ALL];
+        lpm = ipHint && c[C_ALL].nips > 0;
+    }
+    int32_t chosen = -1;
+    if (pick->n > 0) {
+        if (lpm && !foundExact) {   /* _topology_getLongestPrefixMatch, :2202-2229 */
+            uint32_t best = 0;
+            for (size_t i = 0; i < pick->n; ++i) {
+                const int32_t v = pick->q[i];
+                const uint32_t vip = string_to_ip(top->vstr[VS_IP] ? top->vstr[VS_IP][v] : NULL);
+                const uint32_t match = vip & requestedIP;
+                if (match > best) {
+                    best = match;
+                    chosen = v;
+                }
+            }
+        } else {
+            const double r = rnd ? rnd(rctx) : 0.0;
+            const int indexRange = (int)pick->n - 1;
+            const int idx = (int)round((double)(indexRange * r));   /* :2310-2316 */
+            chosen = pick->q[idx < 0 ? 0 : (idx >= (int)pick->n ? (int)pick->n - 1 : idx)];
+        }
+    }
+    for (int i = 0; i < C_N; ++i) free(c[i].q);
+    return chosen;
+}
+
+void topology_attach(Topology* top, spe_in_addr_t address, topology_random_fn random, void* random_ctx,
+                     const char* ipHint, const char* citycodeHint, const char* countrycodeHint,
+                     const char* geocodeHint, const char* typeHint, uint64_t* bwDownOut, uint64_t* bwUpOut) {
+    if (!top) return;
+    const int32_t v = find_attachment_vertex(top, random, random_ctx, ipHint, citycodeHint, countrycodeHint,
+                                             geocodeHint, typeHint);
+    if (v < 0) {
+        tlog(top, LOG_CRITICAL, "unable to find an attachment vertex");
+        return;
+    }
+    pthread_rwlock_wrlock(&top->ip_lock);
+    ip_put(top, address, v);
+    if (top->slot_of_vertex[v] < 0) {
+        top->slot_of_vertex[v] = top->n_attached;
+        top->attached[top->n_attached++] = v;
+        if (atomic_load(&top->sealed)) atomic_store(&top->sealed, 0);   /* A grew: rebuild on next query */
+    }
+    pthread_rwlock_unlock(&top->ip_lock);
+    if (bwUpOut) *bwUpOut = (uint64_t)top->vnum[VN_BWUP][v];
+    if (bwDownOut) *bwDownOut = (uint64_t)top->vnum[VN_BWDOWN][v];
+    struct in_addr a = {address};
+    tlog(top, LOG_MESSAGE, "attached address '%s' to vertex %d ('%s')", inet_ntoa(a), v, top->vstr[VS_ID][v]);
+}
+
+void topology_detach(Topology* top, spe_in_addr_t address) {
+    if (!top) return;
+    pthread_rwlock_wrlock(&top->ip_lock);
+    ip_del(top, address);   /* the vertex stays in A, like the reference (:2415-2421) */
+    pthread_rwlock_unlock(&top->ip_lock);
+}
+
+/* -------------------------------------------------------------- sealing */
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+int32_t topology_seal(Topology* top) {
+    if (!top) return SPE_EINVAL;
+    if (atomic_load_explicit(&top->sealed, memory_order_acquire)) return SPE_OK;
+    pthread_mutex_lock(&top->seal_lock);
+    int rc = SPE_OK;
+    if (!atomic_load(&top->sealed)) {
+        pthread_rwlock_rdlock(&top->ip_lock);
+        const int32_t A = top->n_attached;
+        int32_t* att = malloc(((size_t)A + 1) * sizeof(int32_t));
+        memcpy(att, top->attached, (size_t)A * sizeof(int32_t));
+        pthread_rwlock_unlock(&top->ip_lock);
+        if (top->table) {
+            spe_table_free(top->table);
+            top->table = NULL;
+        }
+        if (A == 0) {
+            rc = SPE_ESTATE;
+        } else {
+            const double t0 = now_s();
+            spe_table_opts o;
+            memset(&o, 0, sizeof o);
+            o.self_mode = SPE_SELF_ROW;
+            rc = spe_table_create(top->graph, att, A, &o, &top->table);
+            if (rc == SPE_OK) rc = spe_table_build(top->table, NULL);
+            if (rc == SPE_OK) {
+                free(top->lat);
+                free(top->rel);
+                top->lat = malloc((size_t)A * A * sizeof(double));
+                top->rel = malloc((size_t)A * A * sizeof(double));
+                if (!top->lat || !top->rel) rc = SPE_ENOMEM;
+                else rc = spe_table_download(top->table, 0, A, top->lat, top->rel, NULL, NULL);
+            }
+            if (rc == SPE_OK) rc = spe_table_min_latency(top->table, &top->min_latency);
+            if (rc == SPE_OK) {
+                top->A = A;
+                top->build_seconds += now_s() - t0;
+                top->build_rows += A;
+                free(top->counts);
+                top->counts_cap = 1024;
+                while (top->counts_cap < (size_t)A * 4) top->counts_cap *= 2;
+                top->counts = calloc(top->counts_cap, sizeof(PairCount));
+            }
+        }
+        free(att);
+        if (rc == SPE_OK) {
+            atomic_store_explicit(&top->sealed, 1, memory_order_release);
+            /* worker_updateMinTimeJump(minimumPathLatency), shd-topology.c:1359-1370: runs on the
+             * querying (worker) thread, as the reference requires */
+            if (top->minlat_fn && top->min_latency > 0) top->minlat_fn(top->min_latency, top->minlat_ctx);
+        } else {
+            tlog(top, LOG_CRITICAL, "path table build failed: %s", spe_last_error());
+        }
+    }
+    pthread_mutex_unlock(&top->seal_lock);
+    return rc;
+}
+
+/* slots of a pair, -1 when an address is not attached */
+static int pair_slots(Topology* top, uint32_t src, uint32_t dst, int32_t* s, int32_t* t) {
+    pthread_rwlock_rdlock(&top->ip_lock);
+    const int32_t sv = ip_get(top, src), dv = ip_get(top, dst);
+    *s = sv >= 0 ? top->slot_of_vertex[sv] : -1;
+    *t = dv >= 0 ? top->slot_of_vertex[dv] : -1;
+    pthread_rwlock_unlock(&top->ip_lock);
+    if (*s < 0 || *t < 0) {
+        struct in_addr a = {*s < 0 ? src : dst};
+        tlog(top, LOG_CRITICAL, "invalid vertex, address %s is not connected to topology", inet_ntoa(a));
+        return 0;
+    }
+    if (topology_seal(top) != SPE_OK) return 0;
+    return 1;
+}
+
+double topology_getLatency(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {
+    int32_t s, t;
+    if (!top || !pair_slots(top, srcAddress, dstAddress, &s, &t)) return -1.0;
+    return top->lat[(size_t)s * top->A + t];
+}
+
+double topology_getReliability(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {
+    int32_t s, t;
+    if (!top || !pair_slots(top, srcAddress, dstAddress, &s, &t)) return -1.0;
+    return top->rel[(size_t)s * top->A + t];
+}
+
+int32_t topology_isRoutable(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {
+    return topology_getLatency(top, srcAddress, dstAddress) > -1 ? 1 : 0;   /* :2072-2075 */
+}
+
+static PairCount* count_slot(Topology* top, int32_t s, int32_t t, int insert) {
+    const uint64_t key = (((uint64_t)(uint32_t)s << 32) | (uint32_t)t) + 1;
+    size_t j = (size_t)(key * 0x9E3779B97F4A7C15ull) & (top->counts_cap - 1);
+    for (size_t probe = 0; probe < top->counts_cap; ++probe) {
+        uint64_t cur = __atomic_load_n(&top->counts[j].key, __ATOMIC_ACQUIRE);
+        if (cur == key) return &top->counts[j];
+        if (cur == 0) {
+            if (!insert) return NULL;
+            uint64_t expect = 0;
+            if (__atomic_compare_exchange_n(&top->counts[j].key, &expect, key, 0, __ATOMIC_ACQ_REL,
+                                            __ATOMIC_ACQUIRE))
+                return &top->counts[j];
+            if (expect == key) return &top->counts[j];
+        }
+        j = (j + 1) & (top->counts_cap - 1);
+    }
+    return NULL;
+}
+
+void topology_incrementPathPacketCounter(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {
+    int32_t s, t;
+    if (!top || !pair_slots(top, srcAddress, dstAddress, &s, &t)) {
+        if (top) tlog(top, LOG_ERROR, "unable to find path for packet counter");
+        return;
+    }
+    PairCount* pc = count_slot(top, s, t, 1);
+    if (pc) atomic_fetch_add_explicit(&pc->count, 1, memory_order_relaxed);
+}
+
+uint64_t topology_path_packet_count(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {
+    int32_t s, t;
+    if (!top || !pair_slots(top, srcAddress, dstAddress, &s, &t)) return 0;
+    PairCount* pc = count_slot(top, s, t, 0);
+    return pc ? atomic_load(&pc->count) : 0;
+}
+
+double topology_min_path_latency(Topology* top) {
+    if (!top || topology_seal(top) != SPE_OK) return 0.0;
+    return top->min_latency;
+}
+
+void topology_free(Topology* top) {
+    if (!top) return;
+    /* _topology_logAllCachedPaths (:1914-1950): the pairs that carried packets */
+    if (top->counts && top->lat)
+        for (size_t j = 0; j < top->counts_cap; ++j) {
+            const uint64_t key = top->counts[j].key;
+            if (!key) continue;
+            const int32_t s = (int32_t)((key - 1) >> 32), t = (int32_t)((key - 1) & 0xffffffffu);
+            const size_t o = (size_t)s * top->A + t;
+            tlog(top, LOG_INFO, "Found path %s%s%s in cache: SourceIndex=%d DestinationIndex=%d Latency=%f "
+                                "Reliability=%f PacketCount=%llu",
+                 top->vstr[VS_ID][top->attached[s]], top->directed ? "->" : "<->",
+                 top->vstr[VS_ID][top->attached[t]], top->attached[s], top->attached[t], top->lat[o], top->rel[o],
+                 (unsigned long long)atomic_load(&top->counts[j].count));
+        }
+    /* _topology_clearCache's timing line (:1262-1265) */
+    tlog(top, LOG_MESSAGE, "path cache cleared, spent %f seconds computing %lld shortest path rows on the GPU",
+         top->build_seconds, (long long)top->build_rows);
+    topo_release(top);
+}

@@ -58,7 +58,7 @@ class Entry(C.Structure):
                 ("hops", C.c_int32)]
 
 
-KERNELS = ["init", "seed", "compact", "relax", "rows", "direct"]
+KERNELS = ["init", "seed", "heavy", "relax", "rows", "direct"]
 
 
 class KernelProfile(C.Structure):
@@ -66,7 +66,7 @@ class KernelProfile(C.Structure):
 
 
 class BuildStats(C.Structure):
-    _fields_ = [("iterations", C.c_int64), ("frontier_total", C.c_int64), ("launches", C.c_int64),
+    _fields_ = [("iterations", C.c_int64), ("active_rounds", C.c_int64), ("launches", C.c_int64),
                 ("seconds", C.c_double)]
 
 
