@@ -81,6 +81,68 @@ def cpu_baseline(top, att, seconds: float, seed: int = 6):
             "cpu_model": model, "host_nproc": os.cpu_count()}
 
 
+def pmc_traffic(args, kernel):
+    """HBM bytes per dispatch of `kernel` from a committed PMC summary (separate
+    rocprofv3 --pmc passes of this same bench command), or None."""
+    path = args.pmc_json
+    if path is None:
+        cand = os.path.join(ROOT, "profiles", f"r01_pmc_{args.config}.json")
+        path = cand if os.path.exists(cand) else None
+    if not path:
+        return None
+    try:
+        k = json.load(open(path))["kernels"][kernel]
+        return {"hbm_bytes_per_launch": round(k["hbm_bytes_per_dispatch"]),
+                "fetch_bytes_per_launch": round(k["fetch_bytes_per_dispatch"]),
+                "write_bytes_per_launch": round(k["write_bytes_per_dispatch"]),
+                "source": os.path.relpath(path, ROOT)}
+    except (KeyError, OSError, ValueError):
+        return None
+
+
+def bench_lookup(args):
+    """C5: batched per-packet lookups (s_slot, t_slot) -> (latency, reliability, ok)
+    against the HBM-resident C3 table; 41 algorithmic bytes per query."""
+    import torch
+    from shadow_amd import spe
+    top, att, desc = workload("c3")
+    g = spe.Graph(top, device=0)
+    t = spe.PathTable(g, att)
+    t.build()
+    q = args.queries
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    pairs = torch.randint(0, t.A, (q, 2), dtype=torch.int32, device="cuda", generator=gen)
+    lat = torch.empty(q, dtype=torch.float64, device="cuda")
+    rel = torch.empty(q, dtype=torch.float64, device="cuda")
+    ok = torch.empty(q, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    steps = args.steps if args.steps > 0 else 10
+    for _ in range(args.warmup):
+        t.lookup_batch(pairs.data_ptr(), q, lat.data_ptr(), rel.data_ptr(), ok.data_ptr(), stream)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(steps):
+        t.lookup_batch(pairs.data_ptr(), q, lat.data_ptr(), rel.data_ptr(), ok.data_ptr(), stream)
+    ev1.record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kern_s = ev0.elapsed_time(ev1) / 1e3 / steps
+    assert bool(ok.all().item())
+    value = q * steps / el
+    ach = 41.0 * q / kern_s / 1e9
+    line = {"metric": "per-packet lookup queries/s against the GPU-resident path table (config C5)",
+            "value": round(value, 1), "unit": "queries/s", "n_gpus": 1, "steps": steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * el / steps, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"C5: {q} uniform (s,t) slot pairs (seed 5) on the {desc} table"},
+            "roofline": {"bound": "hbm", "kernel": "k_lookup", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, "k_lookup"),
+                         "algorithmic_bytes_per_query": 41}}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -92,7 +154,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
+    ap.add_argument("--queries", type=int, default=100_000_000, help="c5: lookups per step")
+    ap.add_argument("--pmc-json", default=None, help="per-dispatch HBM bytes from tools/pmc_to_json.py")
     args = ap.parse_args()
+    if args.config == "c5":
+        return bench_lookup(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -164,8 +230,9 @@ def main():
         rl = kp["relax"]
         relax_s = rl["ms"] / 1e3
         ach = b_relax * done / relax_s / 1e9 if relax_s > 0 else 0.0
+        traffic = pmc_traffic(args, "k_relax")
         roof = {"bound": "hbm", "kernel": "k_relax (SSSP stage)", "achieved": round(ach, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "launches": rl["launches"], "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
                 "algorithmic_bytes_per_source": b_relax}
         rw = kp["rows"]

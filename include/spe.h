@@ -95,6 +95,9 @@ typedef struct spe_table_opts {
     void* ext_reliability;          /* double   */
     void* ext_next_hop;             /* int32_t  */
     void* ext_hops;                 /* uint16_t */
+    int32_t ext_filled;             /* 1: the external storage already holds the rows (e.g. an
+                                     * RCCL all-gather of other tables' blocks): usable for
+                                     * get / download / lookup without spe_table_build */
 } spe_table_opts;
 
 /* Where a table keeps its rows.  Element (s_slot, t_slot) of a field lives at

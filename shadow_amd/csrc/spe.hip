@@ -36,6 +36,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -78,6 +79,9 @@ struct DevGraph {
     const double* owrep;
     const double* oarep;
     int32_t undirected;      // out-CSR == in-CSR
+    const uint8_t* heavy;    // [n] in-degree > 64
+    const uint8_t* oheavy;   // [out entry] heavy[target]: which frontier buffer it goes to
+    int32_t ablate;          // diagnostic only (SPE_ABLATE env): bit 0 = skip route records
     const double* vfac;
     const double* loop_w;
     const double* loop_a;
@@ -156,8 +160,10 @@ __global__ __launch_bounds__(BLOCK) void k_init_state(int32_t n, int32_t groups,
 // then sees WHICH of its in-neighbours changed with one coalesced byte load per
 // 64 in-edges, without dereferencing the neighbour ids first.
 struct Flags {
-    uint8_t* mark_cur;     // [group][vertex]   frontier of this round (consumed)
+    uint8_t* mark_cur;     // [group][vertex]   light-vertex frontier of this round (consumed)
     uint8_t* mark_next;
+    uint8_t* hmark_cur;    // [group][vertex]   heavy-vertex frontier (in-degree > 64)
+    uint8_t* hmark_next;
     uint8_t* in_cur;       // [group][in-CSR entry] changed in-neighbour (consumed)
     uint8_t* in_next;
     int32_t* any_changed;  // set when some vertex changed this round
@@ -165,14 +171,14 @@ struct Flags {
 
 __global__ __launch_bounds__(BLOCK) void k_seed(int32_t n, int32_t nrel, int32_t groups,
                                                 const int32_t* __restrict__ srcv, DevGraph G, uint8_t* mark,
-                                                uint8_t* in_flags) {
+                                                uint8_t* hmark, uint8_t* in_flags) {
     const int32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= groups * WAVE) return;
     const int32_t s = srcv[i];
     if (s < 0) return;
     const int32_t g = i / WAVE;
     for (int32_t k = G.optr[s]; k < G.optr[s + 1]; ++k) {
-        mark[(size_t)g * n + G.ocol[k]] = 1;
+        (G.oheavy[k] ? hmark : mark)[(size_t)g * n + G.ocol[k]] = 1;
         in_flags[(size_t)g * nrel + G.orev[k]] = 1;
     }
 }
@@ -278,6 +284,14 @@ __device__ __forceinline__ bool finish_vertex(Best& b, const DevGraph& G, const 
     bool changed = false;
     if (b.need) {
         if (b.bu < 0) b.bu = G.icol[b.bk];
+        if (G.ablate & 1) {
+            changed = (d_old == INF || b.bd != d_old || b.bk != p_old);
+            if (changed) {
+                st.D[rv] = b.bd;
+                st.P[rv] = b.bk;
+            }
+            return __ballot(changed) != 0;
+        }
         const size_t ru = (gbase + b.bu) * WAVE + lane;
         const Route pu = st.RT[ru];
         Route nr;
@@ -304,37 +318,63 @@ __device__ __forceinline__ void mark_out(const DevGraph& G, int32_t g, int32_t n
                                          const Flags& fl) {
     const int32_t o0 = G.optr[v], o1 = G.optr[v + 1];
     for (int32_t k = o0 + lane; k < o1; k += WAVE) {
-        fl.mark_next[(size_t)g * n + G.ocol[k]] = 1;
+        (G.oheavy[k] ? fl.hmark_next : fl.mark_next)[(size_t)g * n + G.ocol[k]] = 1;
         fl.in_next[(size_t)g * G.nrel + G.orev[k]] = 1;
+    }
+}
+
+// Everything a light vertex's relaxation loads before it can look at a single
+// candidate row -- issued one vertex ahead (software pipeline, see k_relax).
+struct Pre {
+    int32_t g, v, k0;
+    int32_t s;          // this lane's source
+    Seg sg;             // in-CSR slice (one entry per lane)
+    bool f;             // this lane's in-edge changed last round
+    int32_t orev_l;     // reverse entry of this lane's edge (undirected marking)
+    bool heavy_l;       // this lane's neighbour is heavy (undirected marking)
+    double d_old;
+    int32_t p_old;
+};
+
+__device__ __forceinline__ void prefetch_vertex(Pre& p, int32_t g, int32_t v, int32_t n, int32_t lane,
+                                                const int32_t* __restrict__ srcv, const DevGraph& G,
+                                                const State& st, const Flags& fl) {
+    p.g = g;
+    p.v = v;
+    p.k0 = G.iptr[v];
+    p.sg = load_segment(p.k0, G.iptr[v + 1], lane, G);
+    p.s = srcv[g * WAVE + lane];
+    const size_t rv = ((size_t)g * n + v) * WAVE + lane;
+    p.d_old = st.D[rv];
+    p.p_old = st.P[rv];
+    p.f = p.sg.valid && fl.in_cur[(size_t)g * G.nrel + p.k0 + lane] != 0;
+    p.orev_l = 0;
+    p.heavy_l = false;
+    if (G.undirected && p.sg.valid) {
+        p.orev_l = G.orev[p.k0 + lane];
+        p.heavy_l = G.oheavy[p.k0 + lane] != 0;
     }
 }
 
 // Relaxation of one light (in-degree <= 64) (group, v) for the 64 sources of
 // the group (lane = source).  Returns the wave-uniform "some lane changed".
-__device__ __forceinline__ bool relax_vertex(int32_t g, int32_t v, int32_t n, int32_t lane,
-                                             const int32_t* __restrict__ srcv, const DevGraph& G,
+__device__ __forceinline__ bool relax_vertex(const Pre& p, int32_t n, int32_t lane, const DevGraph& G,
                                              const State& st, const Flags& fl) {
+    const int32_t g = p.g, v = p.v;
     const size_t gbase = (size_t)g * n;
-    const int32_t s = srcv[g * WAVE + lane];
     const size_t rv = (gbase + v) * WAVE + lane;
-    const bool active = (s >= 0) && (s != v);
-    const int32_t k0 = G.iptr[v], k1 = G.iptr[v + 1];
-    const Seg sg = load_segment(k0, k1, lane, G);
-    const size_t fo = (size_t)g * G.nrel + k0 + lane;
-    const bool f = sg.valid && fl.in_cur[fo] != 0;
-    const double d_old = st.D[rv];
-    const int32_t p_old = st.P[rv];
-    const uint64_t cm = __ballot(f);
-    if (f) fl.in_cur[fo] = 0;   // consumed
-    Best b{d_old, p_old, -1, -1.0, false};
-    scan_changed(sg, cm, gbase, lane, active, st,
+    const bool active = (p.s >= 0) && (p.s != v);
+    const uint64_t cm = __ballot(p.f);
+    if (p.f) fl.in_cur[(size_t)g * G.nrel + p.k0 + lane] = 0;   // consumed
+    Best b{p.d_old, p.p_old, -1, -1.0, false};
+    scan_changed(p.sg, cm, gbase, lane, active, st,
                  [&](int32_t kk, int32_t u, double du, double alt) { offer(b, G, st, gbase, lane, kk, u, du, alt); });
-    const bool changed = finish_vertex(b, G, st, gbase, lane, v, s, rv, d_old, p_old);
+    const bool changed = finish_vertex(b, G, st, gbase, lane, v, p.s, rv, p.d_old, p.p_old);
     if (changed) {
         if (G.undirected) {   // out-list == in-list, already in registers
-            if (sg.valid) {
-                fl.mark_next[gbase + sg.u_l] = 1;
-                fl.in_next[(size_t)g * G.nrel + G.orev[k0 + lane]] = 1;
+            if (p.sg.valid) {
+                (p.heavy_l ? fl.hmark_next : fl.mark_next)[gbase + p.sg.u_l] = 1;
+                fl.in_next[(size_t)g * G.nrel + p.orev_l] = 1;
             }
         } else {
             mark_out(G, g, n, v, lane, fl);
@@ -343,39 +383,73 @@ __device__ __forceinline__ bool relax_vertex(int32_t g, int32_t v, int32_t n, in
     return changed;
 }
 
-// One relaxation round over a dense frontier bitmap.  Work unit = 8 consecutive
-// (group, vertex) flags read as one scalar 64-bit word, so marked vertices are
-// spread over the grid's waves (a 64-flag unit would serialise up to 64
-// vertices on one wave).  Heavy vertices (in-degree > 64) stay marked for
-// k_heavy_partial / k_heavy_combine.
-__global__ __launch_bounds__(BLOCK) void k_relax(int64_t total, int32_t n, const int32_t* __restrict__ srcv,
-                                                 DevGraph G, State st, const uint8_t* __restrict__ heavy, Flags fl) {
-    const int32_t lane = threadIdx.x & (WAVE - 1);
-    const int64_t wave = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
-    const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
-    const int64_t units = (total + 7) >> 3;   // mark buffers are padded to a multiple of 8 bytes
-    uint64_t* words = reinterpret_cast<uint64_t*>(fl.mark_cur);
-    bool wrote = false;
-    for (int64_t u8 = wave; u8 < units; u8 += nwaves) {
-        const uint64_t wl = words[u8];   // same address in every lane: make it wave-uniform
-        uint64_t w = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(wl >> 32)) << 32) |
-                     (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)wl);
-        if (!w) continue;
-        uint64_t keep = 0;
-        while (w) {
-            const int32_t bit = __builtin_ctzll(w) >> 3;           // byte index 0..7
-            w &= ~(0xFFull << (8 * bit));
-            const int64_t e = u8 * 8 + bit;
-            if (e >= total) break;
-            const int32_t g = (int32_t)(e / n);
-            const int32_t v = (int32_t)(e - (int64_t)g * n);
-            if (heavy[v]) {
-                keep |= 0x01ull << (8 * bit);
-                continue;
-            }
-            wrote |= relax_vertex(g, v, n, lane, srcv, G, st, fl);
+// Cursor over this wave's 8-flag units of the light frontier bitmap.  The next
+// unit's word is loaded one unit ahead; a unit is cleared as soon as it is taken.
+struct Cursor {
+    int64_t u8, stride, units;
+    uint64_t w, w_ahead;
+};
+
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+           (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+
+__device__ __forceinline__ bool cursor_next(Cursor& c, uint64_t* words, int32_t total, int32_t n, int32_t lane,
+                                            int32_t& g, int32_t& v) {
+    for (;;) {
+        if (c.w) {
+            const int32_t bit = __builtin_ctzll(c.w) >> 3;
+            c.w &= ~(0xFFull << (8 * bit));
+            const int32_t e = (int32_t)(c.u8 * 8) + bit;
+            if (e >= total) continue;
+            g = e / n;
+            v = e - g * n;
+            return true;
         }
-        if (lane == 0) words[u8] = keep;   // consumed (heavy marks kept for the heavy kernels)
+        c.u8 += c.stride;
+        if (c.u8 >= c.units) return false;
+        c.w = uniform_u64(c.w_ahead);
+        if (c.w && lane == 0) words[c.u8] = 0;   // taken
+        const int64_t ahead = c.u8 + c.stride;
+        c.w_ahead = ahead < c.units ? words[ahead] : 0;
+    }
+}
+
+// One relaxation round over the dense light-frontier bitmap.  Work unit = 8
+// consecutive (group, vertex) flags read as one 64-bit word (marked vertices
+// spread over the grid's waves).  Two-stage software pipeline per wave: the
+// CSR slice, change flags and state of the NEXT marked vertex are in flight
+// while the current one gathers its candidate rows and parent route.
+__global__ __launch_bounds__(BLOCK) void k_relax(int32_t total, int32_t n, const int32_t* __restrict__ srcv,
+                                                 DevGraph G, State st, Flags fl) {
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    uint64_t* words = reinterpret_cast<uint64_t*>(fl.mark_cur);
+    // XCD-aware split (speed only, never correctness): blocks are dealt round-robin
+    // over the 8 XCDs, so blocks with equal blockIdx % 8 share an L2.  Give each
+    // such class one contiguous eighth of the (group, vertex) space -- about G/8
+    // whole groups -- so a group's hot rows (hubs) live in one XCD's L2.
+    const int64_t all_units = ((int64_t)total + 7) >> 3;   // mark buffers padded to 8 bytes
+    const int32_t xcd = blockIdx.x & 7;
+    const int64_t waves_per_xcd = ((int64_t)(gridDim.x >> 3) * BLOCK) >> 6;
+    const int64_t wave = ((int64_t)(blockIdx.x >> 3) * BLOCK + threadIdx.x) >> 6;
+    const int64_t lo = all_units * xcd / 8, hi = all_units * (xcd + 1) / 8;
+    Cursor c;
+    c.stride = waves_per_xcd;
+    c.units = hi;
+    c.u8 = lo + wave - c.stride;
+    c.w = 0;
+    c.w_ahead = lo + wave < hi ? words[lo + wave] : 0;
+    bool wrote = false;
+    int32_t g, v;
+    Pre cur, nxt;
+    bool has = cursor_next(c, words, total, n, lane, g, v);
+    if (has) prefetch_vertex(nxt, g, v, n, lane, srcv, G, st, fl);
+    while (has) {
+        cur = nxt;
+        has = cursor_next(c, words, total, n, lane, g, v);
+        if (has) prefetch_vertex(nxt, g, v, n, lane, srcv, G, st, fl);
+        wrote |= relax_vertex(cur, n, lane, G, st, fl);
     }
     if (wrote && lane == 0) *fl.any_changed = 1;   // at most one plain store per wave
 }
@@ -408,7 +482,7 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_partial(int32_t groups, int32_t
         const int32_t sgi = (int32_t)(it - (int64_t)g * hp.nseg);
         const int32_t v = hp.seg_vertex[sgi];
         const size_t gbase = (size_t)g * n;
-        if (!fl.mark_cur[gbase + v]) continue;
+        if (!fl.hmark_cur[gbase + v]) continue;
         const int32_t s = srcv[g * WAVE + lane];
         const bool active = (s >= 0) && (s != v);
         const int32_t kb = hp.seg_begin[sgi];
@@ -446,7 +520,7 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_combine(int32_t groups, int32_t
         const int32_t h = (int32_t)(it - (int64_t)g * hp.nheavy);
         const int32_t v = hp.heavy_vertex[h];
         const size_t gbase = (size_t)g * n;
-        if (!fl.mark_cur[gbase + v]) continue;
+        if (!fl.hmark_cur[gbase + v]) continue;
         const int32_t s = srcv[g * WAVE + lane];
         const size_t rv = (gbase + v) * WAVE + lane;
         const double d_old = st.D[rv];
@@ -457,7 +531,7 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_combine(int32_t groups, int32_t
             const int2 uk = pp.uk[o];
             if (uk.x >= 0) offer(b, G, st, gbase, lane, uk.y, uk.x, pp.du[o], pp.alt[o]);
         }
-        if (lane == 0) fl.mark_cur[gbase + v] = 0;
+        if (lane == 0) fl.hmark_cur[gbase + v] = 0;
         if (finish_vertex(b, G, st, gbase, lane, v, s, rv, d_old, p_old)) {
             mark_out(G, g, n, v, lane, fl);
             wrote = true;
@@ -695,6 +769,7 @@ struct spe_table {
     State st{};
     uint8_t* inflag[2] = {nullptr, nullptr};
     uint8_t* mark[2] = {nullptr, nullptr};
+    uint8_t* hmark[2] = {nullptr, nullptr};
     Partial pp{};
     int32_t* counts = nullptr;   // per round: 1 if any vertex changed
     int32_t max_iters = 0;
@@ -794,6 +869,7 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
     DevGraph& d = g->dev;
     d.n = h.n;
     d.nrel = (int32_t)h.icol.size();
+    d.ablate = getenv("SPE_ABLATE") ? atoi(getenv("SPE_ABLATE")) : 0;
 #define UPBASE d
 #define UP(field, src)                                   \
     do {                                                 \
@@ -853,6 +929,15 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
         UP(heavy_seg0, heavy_seg0);
 #undef UPBASE
         r = dev_upload(g->allocs, heavy, &g->d_heavy);
+        if (r) {
+            spe_graph_free(g);
+            return r;
+        }
+        d.heavy = g->d_heavy;
+        const std::vector<int32_t>& oc = h.directed ? h.ocol : h.icol;
+        std::vector<uint8_t> oheavy(oc.size());
+        for (size_t k = 0; k < oc.size(); ++k) oheavy[k] = heavy[oc[k]];
+        r = dev_upload(g->allocs, oheavy, &d.oheavy);
         if (r) {
             spe_graph_free(g);
             return r;
@@ -943,6 +1028,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
             return fail(SPE_EINVAL, "external storage needs all four fields");
         }
         t->ext = true;
+        t->built = o.ext_filled != 0;
         t->tb.lat = (double*)o.ext_latency;
         t->tb.rel = (double*)o.ext_reliability;
         t->tb.next = (int32_t*)o.ext_next_hop;
@@ -970,6 +1056,8 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         TRY(dev_alloc(t->allocs, &t->inflag[1], G * nrel));
         TRY(dev_alloc(t->allocs, &t->mark[0], (G * n + 8) & ~(size_t)7));
         TRY(dev_alloc(t->allocs, &t->mark[1], (G * n + 8) & ~(size_t)7));
+        TRY(dev_alloc(t->allocs, &t->hmark[0], G * n));
+        TRY(dev_alloc(t->allocs, &t->hmark[1], G * n));
         const size_t pe = G * std::max<size_t>(1, (size_t)g->hp.nseg) * WAVE;
         TRY(dev_alloc(t->allocs, &t->pp.alt, pe));
         TRY(dev_alloc(t->allocs, &t->pp.du, pe));
@@ -1030,11 +1118,12 @@ static int relax_to_convergence(spe_table* t, int32_t groups, hipStream_t s) {
     const int32_t n = g->hg.n;
     const int32_t nrel = (int32_t)g->hg.icol.size();
     const int64_t total = (int64_t)groups * n;
-    const int relax_grid = grid_for((total + 7) / 8 * WAVE, BLOCK, 2048);   // waves stride over 8-flag units
+    const int relax_grid = (grid_for((total + 7) / 8 * WAVE, BLOCK, 2048) + 7) & ~7;   // multiple of 8 (XCD split)
     HIP_TRY(hipMemsetAsync(t->counts, 0, sizeof(int32_t) * ((size_t)t->max_iters + 2), s));
     for (int i = 0; i < 2; ++i) {   // consumers clear what they read; this only guards a failed batch
         HIP_TRY(hipMemsetAsync(t->inflag[i], 0, (size_t)groups * std::max(1, nrel), s));
         HIP_TRY(hipMemsetAsync(t->mark[i], 0, ((size_t)total + 8) & ~(size_t)7, s));
+        HIP_TRY(hipMemsetAsync(t->hmark[i], 0, (size_t)total, s));
     }
     {
         LaunchTimer lt(t, s, SPE_K_INIT);
@@ -1044,18 +1133,18 @@ static int relax_to_convergence(spe_table* t, int32_t groups, hipStream_t s) {
         LaunchTimer lt(t, s, SPE_K_SEED);
         // the sources "changed in round 0": their out-edges form round 1's frontier
         k_seed<<<(groups * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(n, nrel, groups, t->d_srcv, g->dev, t->mark[1],
-                                                                     t->inflag[1]);
+                                                                     t->hmark[1], t->inflag[1]);
     }
     int32_t it = 1;
     int32_t check_every = 8;
     for (;;) {
         for (int32_t q = 0; q < check_every; ++q, ++it) {
             if (it > t->max_iters) return fail(SPE_ESTATE, "relaxation did not converge");
-            Flags fl{t->mark[it & 1], t->mark[(it + 1) & 1], t->inflag[it & 1], t->inflag[(it + 1) & 1],
-                     t->counts + it};
+            Flags fl{t->mark[it & 1],   t->mark[(it + 1) & 1],   t->hmark[it & 1],
+                     t->hmark[(it + 1) & 1], t->inflag[it & 1], t->inflag[(it + 1) & 1], t->counts + it};
             {
                 LaunchTimer lt(t, s, SPE_K_RELAX);
-                k_relax<<<relax_grid, BLOCK, 0, s>>>(total, n, t->d_srcv, g->dev, t->st, g->d_heavy, fl);
+                k_relax<<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcv, g->dev, t->st, fl);
             }
             if (g->hp.nheavy > 0) {
                 LaunchTimer lt(t, s, SPE_K_HEAVY);

@@ -319,3 +319,36 @@ def gen_random_small(n: int, extra_edges: int, seed: int, integer_weights: bool 
     if integer_weights and self_loops:
         top.elat[-n:] = rng.integers(1, 3, size=n).astype(np.float64)
     return top
+
+
+def write_graphml(top: Topology, path: str, ips=None, bandwidth: int = 10240) -> None:
+    """Write a topology as GraphML the reference (and topology_new) accepts:
+    node attrs packetloss / bandwidthdown / bandwidthup (+ ip), edge latency /
+    packetloss; vertex i gets id "v{i}"."""
+    out = ['<?xml version="1.0" encoding="utf-8"?>',
+           '<graphml xmlns="http://graphml.graphdrawing.org/xmlns">',
+           '<key attr.name="packetloss" attr.type="double" for="edge" id="e1"/>',
+           '<key attr.name="latency" attr.type="double" for="edge" id="e0"/>',
+           '<key attr.name="ip" attr.type="string" for="node" id="n3"/>',
+           '<key attr.name="bandwidthup" attr.type="int" for="node" id="n2"/>',
+           '<key attr.name="bandwidthdown" attr.type="int" for="node" id="n1"/>',
+           '<key attr.name="packetloss" attr.type="double" for="node" id="n0"/>']
+    if top.prefer_direct:
+        out.insert(2, '<key attr.name="preferdirectpaths" attr.type="string" for="graph" id="g0"/>')
+    out.append(f'<graph edgedefault="{"directed" if top.directed else "undirected"}">')
+    if top.prefer_direct:
+        out.append('<data key="g0">true</data>')
+    for v in range(top.n):
+        d = [f'<data key="n1">{bandwidth}</data>', f'<data key="n2">{bandwidth}</data>']
+        if not math.isnan(top.vloss[v]):
+            d.append(f'<data key="n0">{repr(float(top.vloss[v]))}</data>')
+        if ips is not None and ips[v]:
+            d.append(f'<data key="n3">{ips[v]}</data>')
+        out.append(f'<node id="v{v}">{"".join(d)}</node>')
+    for e in range(top.m):
+        out.append(f'<edge source="v{int(top.esrc[e])}" target="v{int(top.edst[e])}">'
+                   f'<data key="e0">{repr(float(top.elat[e]))}</data>'
+                   f'<data key="e1">{repr(float(top.eloss[e]))}</data></edge>')
+    out.append("</graph></graphml>")
+    with open(path, "w") as f:
+        f.write("\n".join(out))

@@ -44,7 +44,7 @@ class TableOpts(C.Structure):
     _fields_ = [("self_mode", C.c_int32), ("force_sssp", C.c_int32), ("groups_per_launch", C.c_int32),
                 ("block_begin", C.c_int32), ("block_end", C.c_int32),
                 ("ext_latency", C.c_void_p), ("ext_reliability", C.c_void_p),
-                ("ext_next_hop", C.c_void_p), ("ext_hops", C.c_void_p)]
+                ("ext_next_hop", C.c_void_p), ("ext_hops", C.c_void_p), ("ext_filled", C.c_int32)]
 
 
 class TableLayout(C.Structure):
@@ -167,7 +167,7 @@ class PathTable:
     """spe_table: the per-(source, target) path table for attached vertices."""
 
     def __init__(self, graph: Graph, attached, self_mode: int = SPE_SELF_ROW, force_sssp: bool = False,
-                 groups: int = 0, blocks=None, ext=None):
+                 groups: int = 0, blocks=None, ext=None, ext_filled: bool = False):
         self.graph = graph
         self.attached = np.ascontiguousarray(attached, np.int32)
         self.A = int(self.attached.shape[0])
@@ -179,6 +179,7 @@ class PathTable:
             o.block_begin, o.block_end = int(blocks[0]), int(blocks[1])
         if ext is not None:  # four device pointers (ints)
             o.ext_latency, o.ext_reliability, o.ext_next_hop, o.ext_hops = [int(x) for x in ext]
+            o.ext_filled = int(bool(ext_filled))
         h = C.c_void_p()
         _check(lib().spe_table_create(graph.h, _p(self.attached), self.A, C.byref(o), C.byref(h)),
                "spe_table_create")

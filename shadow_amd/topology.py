@@ -1,0 +1,122 @@
+"""ctypes mirror of the drop-in topology API (include/shd_topology_spe.h,
+libshdtopo.so) -- the same entry points, argument meanings and error
+conventions as the reference's shd-topology.h; used by the tests."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import socket
+import struct
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libshdtopo.so")
+EXPORTS = ["topology_new", "topology_new_on_device", "topology_free", "topology_attach", "topology_detach",
+           "topology_isRoutable", "topology_getLatency", "topology_getReliability",
+           "topology_incrementPathPacketCounter", "topology_set_log_callback",
+           "topology_set_min_latency_callback", "topology_seal", "topology_vertex_count",
+           "topology_attached_vertex", "topology_path_packet_count", "topology_min_path_latency"]
+
+RANDOM_FN = C.CFUNCTYPE(C.c_double, C.c_void_p)
+MINLAT_FN = C.CFUNCTYPE(None, C.c_double, C.c_void_p)
+LOG_FN = C.CFUNCTYPE(None, C.c_int, C.c_char_p, C.c_void_p)
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        from . import spe
+        spe.lib()   # one HIP runtime per process (see spe.lib)
+        L = C.CDLL(LIB_PATH)
+        P, U = C.c_void_p, C.c_uint32
+        L.topology_new.restype = P
+        L.topology_new.argtypes = [C.c_char_p]
+        L.topology_new_on_device.restype = P
+        L.topology_new_on_device.argtypes = [C.c_char_p, C.c_int32]
+        L.topology_free.argtypes = [P]
+        L.topology_attach.argtypes = [P, U, RANDOM_FN, P, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
+                                      C.c_char_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.topology_detach.argtypes = [P, U]
+        for f in ("topology_getLatency", "topology_getReliability"):
+            getattr(L, f).argtypes = [P, U, U]
+            getattr(L, f).restype = C.c_double
+        L.topology_isRoutable.argtypes = [P, U, U]
+        L.topology_isRoutable.restype = C.c_int32
+        L.topology_incrementPathPacketCounter.argtypes = [P, U, U]
+        L.topology_set_log_callback.argtypes = [P, LOG_FN, P]
+        L.topology_set_min_latency_callback.argtypes = [P, MINLAT_FN, P]
+        L.topology_seal.argtypes = [P]
+        L.topology_seal.restype = C.c_int32
+        L.topology_vertex_count.argtypes = [P]
+        L.topology_vertex_count.restype = C.c_int32
+        L.topology_attached_vertex.argtypes = [P, U]
+        L.topology_attached_vertex.restype = C.c_int32
+        L.topology_path_packet_count.argtypes = [P, U, U]
+        L.topology_path_packet_count.restype = C.c_uint64
+        L.topology_min_path_latency.argtypes = [P]
+        L.topology_min_path_latency.restype = C.c_double
+        _lib = L
+    return _lib
+
+
+def ip(s: str) -> int:
+    """dotted quad -> in_addr_t value (network byte order, as address_toNetworkIP)."""
+    return struct.unpack("=I", socket.inet_aton(s))[0]
+
+
+class Topology:
+    def __init__(self, graph_path: str, device: int = 0):
+        self.h = lib().topology_new_on_device(graph_path.encode(), int(device))
+        if not self.h:
+            raise ValueError(f"topology_new failed for {graph_path}")
+        self._keep = []
+
+    def attach(self, address: int, rand=None, ip_hint=None, citycode=None, countrycode=None, geocode=None,
+               type_hint=None):
+        seq = list(rand) if rand is not None else [0.0]
+        state = {"i": 0}
+
+        def nxt(_ctx):
+            v = seq[state["i"] % len(seq)]
+            state["i"] += 1
+            return v
+
+        cb = RANDOM_FN(nxt)
+        self._keep.append(cb)
+        down, up = C.c_uint64(0), C.c_uint64(0)
+        enc = lambda x: x.encode() if x else None
+        lib().topology_attach(self.h, address, cb, None, enc(ip_hint), enc(citycode), enc(countrycode),
+                              enc(geocode), enc(type_hint), C.byref(down), C.byref(up))
+        return down.value, up.value
+
+    def detach(self, address: int):
+        lib().topology_detach(self.h, address)
+
+    def latency(self, a: int, b: int) -> float:
+        return lib().topology_getLatency(self.h, a, b)
+
+    def reliability(self, a: int, b: int) -> float:
+        return lib().topology_getReliability(self.h, a, b)
+
+    def routable(self, a: int, b: int) -> bool:
+        return bool(lib().topology_isRoutable(self.h, a, b))
+
+    def count_packet(self, a: int, b: int):
+        lib().topology_incrementPathPacketCounter(self.h, a, b)
+
+    def packets(self, a: int, b: int) -> int:
+        return int(lib().topology_path_packet_count(self.h, a, b))
+
+    def vertex_of(self, a: int) -> int:
+        return int(lib().topology_attached_vertex(self.h, a))
+
+    def min_latency(self) -> float:
+        return float(lib().topology_min_path_latency(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().topology_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()

@@ -208,3 +208,29 @@ def test_c3_sample_rows_full_size(spe):
     assert rows["ok"].all()
     # next hop of a multi-hop route is a neighbour of the source; hops >= 1
     assert (rows["hops"] >= 1).all()
+
+
+def test_external_storage_and_prefilled_table(spe):
+    """Caller-owned HBM (spe_table_opts.ext_*): rows land in torch tensors; a second
+    table adopting the filled buffers (ext_filled, the all-gather case) reads them back."""
+    import math
+    import torch
+    top = graphs.gen_random_small(200, 600, 47)
+    A = np.arange(top.n, dtype=np.int32)
+    elems = math.ceil(top.n / 64) * top.n * 64
+    bufs = [torch.empty(elems, dtype=torch.float64, device="cuda"),
+            torch.empty(elems, dtype=torch.float64, device="cuda"),
+            torch.empty(elems, dtype=torch.int32, device="cuda"),
+            torch.empty(elems, dtype=torch.int16, device="cuda")]
+    g = spe.Graph(top)
+    t = spe.PathTable(g, A, ext=[b.data_ptr() for b in bufs])
+    t.build()
+    out = t.download()
+    compare(out, Oracle(top).rows(A, A), label="ext")
+    t2 = spe.PathTable(g, A, ext=[b.data_ptr() for b in bufs], ext_filled=True)
+    out2 = t2.download()
+    for k in ("lat", "rel", "next", "hops"):
+        np.testing.assert_array_equal(out2[k], out[k])
+    # the SB64 layout the header documents
+    s, tt = 77, 12
+    assert bufs[0][((s // 64) * top.n + tt) * 64 + s % 64].item() == out["lat"][s, tt]

@@ -1,0 +1,33 @@
+"""Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-kernel, per-dispatch
+HBM bytes (profiles/<round>_pmc_<config>.json), applying the gfx950 correction
+of MI355X_MICROARCH.md §HBM: FETCH_SIZE reads exactly half of the bytes of
+dwordx2/x4 loads -- confirmed here on k_rows_sssp, whose read volume is known
+(24 B x 64 lanes x targets x groups per launch: FETCH_SIZE reports 0.50 of it).
+WRITE_SIZE is exact (k_rows_sssp writes 22 B per pair: WRITE_SIZE = 1.00x)."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+root, out = sys.argv[1], sys.argv[2]
+acc = collections.defaultdict(lambda: {"fetch_kb": 0.0, "write_kb": 0.0, "dispatches": set()})
+for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+        if r["Counter_Name"] == "FETCH_SIZE":
+            acc[k]["fetch_kb"] += float(r["Counter_Value"])
+            acc[k]["dispatches"].add((f, r["Dispatch_Id"]))
+        elif r["Counter_Name"] == "WRITE_SIZE":
+            acc[k]["write_kb"] += float(r["Counter_Value"])
+res = {}
+for k, v in acc.items():
+    nd = max(1, len(v["dispatches"]))
+    res[k] = {"dispatches": nd, "fetch_bytes_raw_per_dispatch": v["fetch_kb"] * 1024 / nd,
+              "fetch_bytes_per_dispatch": 2 * v["fetch_kb"] * 1024 / nd,
+              "write_bytes_per_dispatch": v["write_kb"] * 1024 / nd}
+    res[k]["hbm_bytes_per_dispatch"] = res[k]["fetch_bytes_per_dispatch"] + res[k]["write_bytes_per_dispatch"]
+json.dump({"note": "FETCH_SIZE x2 (gfx950 correction, calibrated on k_rows_sssp); WRITE_SIZE x1",
+           "kernels": res}, open(out, "w"), indent=1)
+print(json.dumps(res, indent=1))
