@@ -98,6 +98,8 @@ typedef struct spe_table_opts {
     int32_t ext_filled;             /* 1: the external storage already holds the rows (e.g. an
                                      * RCCL all-gather of other tables' blocks): usable for
                                      * get / download / lookup without spe_table_build */
+    int32_t lanes_per_group;        /* sources sharing one relaxation frontier: 16, 32 or 64;
+                                     * 0 = default (64: measured fastest on C3) */
 } spe_table_opts;
 
 /* Where a table keeps its rows.  Element (s_slot, t_slot) of a field lives at

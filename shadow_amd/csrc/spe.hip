@@ -99,14 +99,17 @@ struct RowMode {
 
 // Per-lane route record carried with the distance: the path-order reliability
 // fold (starting at the source factor) and (hops, first hop).  16 B so a parent
-// lookup is ONE scattered 16-B access per lane.
+// lookup is ONE 16-B access per lane (lanes with the same parent coalesce).
 struct alignas(16) Route {
     double r;
     int32_t h;
     int32_t f;
 };
 
-struct State {        // [group][vertex][64 lanes]
+// Relaxation state of one batch, [lane group][vertex][L lanes] (lane = source).
+// A lane group of L sources is the unit that shares a frontier; a wave holds
+// 64/L subgroups and so relaxes 64/L (group, vertex) items at once.
+struct State {
     double* D;        // distance
     int32_t* P;       // in-CSR index of the chosen parent edge, -1 none
     Route* RT;        // route record
@@ -126,19 +129,45 @@ __device__ __forceinline__ size_t tidx(int32_t sb_local, int32_t A, int32_t j, i
     return ((size_t)sb_local * (size_t)A + (size_t)j) * WAVE + (size_t)lane;
 }
 
+template <int L>
+struct Sub {
+    static constexpr int V = WAVE / L;                                   // subgroups per wave
+    static constexpr uint64_t MASK = (L == 64) ? ~0ull : ((1ull << L) - 1);
+    static constexpr int INFL = (L == 64) ? 8 : (L == 32 ? 6 : 4);       // neighbour rows in flight per subgroup
+};
+
+template <int L>
+__device__ __forceinline__ size_t sidx(int32_t g, int32_t n, int32_t v, int32_t j) {
+    return ((size_t)g * (size_t)n + (size_t)v) * L + (size_t)j;
+}
+
+// value of `x` held by lane `src` (same subgroup, active)
+template <int L>
+__device__ __forceinline__ int32_t sub_get(int32_t x, int32_t src) {
+    if constexpr (L == 64) return __builtin_amdgcn_readlane(x, src);
+    else return __shfl(x, src);
+}
+
+template <int L>
+__device__ __forceinline__ double sub_get_d(double x, int32_t src) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    const uint32_t lo = (uint32_t)sub_get<L>((int32_t)(uint32_t)b, src);
+    const uint32_t hi = (uint32_t)sub_get<L>((int32_t)(uint32_t)(b >> 32), src);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // ----------------------------------------------------------------- kernels
 
-__global__ __launch_bounds__(BLOCK) void k_init_state(int32_t n, int32_t groups,
-                                                      const int32_t* __restrict__ srcv,
+template <int L>
+__global__ __launch_bounds__(BLOCK) void k_init_state(int32_t n, int32_t groups, const int32_t* __restrict__ srcv,
                                                       const double* __restrict__ vfac, State st) {
-    const size_t total = (size_t)groups * n * WAVE;
-    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < total;
-         i += (size_t)gridDim.x * BLOCK) {
-        const int32_t lane = (int32_t)(i & (WAVE - 1));
-        const size_t gv = i >> 6;
+    const size_t total = (size_t)groups * n * L;
+    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < total; i += (size_t)gridDim.x * BLOCK) {
+        const int32_t j = (int32_t)(i % L);
+        const size_t gv = i / L;
         const int32_t g = (int32_t)(gv / n);
         const int32_t v = (int32_t)(gv - (size_t)g * n);
-        const int32_t s = srcv[g * WAVE + lane];
+        const int32_t s = srcv[g * L + j];
         if (v == s) {
             st.D[i] = 0.0;
             const double fs = vfac[s];
@@ -158,7 +187,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_state(int32_t n, int32_t groups,
 // out-edge u -> x, the frontier mark of (group, x) and the in-edge flag of the
 // mirrored in-CSR entry (reverse index G.orev) in round r+1's buffers.  A vertex
 // then sees WHICH of its in-neighbours changed with one coalesced byte load per
-// 64 in-edges, without dereferencing the neighbour ids first.
+// L in-edges, without dereferencing the neighbour ids first.
 struct Flags {
     uint8_t* mark_cur;     // [group][vertex]   light-vertex frontier of this round (consumed)
     uint8_t* mark_next;
@@ -169,28 +198,19 @@ struct Flags {
     int32_t* any_changed;  // set when some vertex changed this round
 };
 
-__global__ __launch_bounds__(BLOCK) void k_seed(int32_t n, int32_t nrel, int32_t groups,
-                                                const int32_t* __restrict__ srcv, DevGraph G, uint8_t* mark,
-                                                uint8_t* hmark, uint8_t* in_flags) {
+template <int L>
+__global__ __launch_bounds__(BLOCK) void k_seed(int32_t n, int32_t groups, const int32_t* __restrict__ srcv,
+                                                DevGraph G, uint8_t* mark, uint8_t* hmark, uint8_t* in_flags) {
     const int32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= groups * WAVE) return;
+    if (i >= groups * L) return;
     const int32_t s = srcv[i];
     if (s < 0) return;
-    const int32_t g = i / WAVE;
+    const int32_t g = i / L;
     for (int32_t k = G.optr[s]; k < G.optr[s + 1]; ++k) {
         (G.oheavy[k] ? hmark : mark)[(size_t)g * n + G.ocol[k]] = 1;
-        in_flags[(size_t)g * nrel + G.orev[k]] = 1;
+        in_flags[(size_t)g * G.nrel + G.orev[k]] = 1;
     }
 }
-
-__device__ __forceinline__ double readlane_d(double x, int32_t l) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
-constexpr int INFLIGHT = 8;   // independent 512-B row gathers in flight per wave
 
 // Lexicographic candidate update (alt, d[u], u) against the running best of one
 // lane.  Ties against the current parent resolve with the parent's CURRENT
@@ -203,7 +223,8 @@ struct Best {
     bool need;     // the parent's (R, H, F) must be (re)gathered
 };
 
-__device__ __forceinline__ void offer(Best& b, const DevGraph& G, const State& st, size_t gbase, int32_t lane,
+template <int L>
+__device__ __forceinline__ void offer(Best& b, const DevGraph& G, const State& st, int32_t g, int32_t n, int32_t j,
                                       int32_t kk, int32_t u, double du, double alt) {
     bool better = false;
     if (alt < b.bd) {
@@ -215,7 +236,7 @@ __device__ __forceinline__ void offer(Best& b, const DevGraph& G, const State& s
             b.bu = u;
         } else {
             if (b.bu < 0) b.bu = G.icol[b.bk];
-            if (b.bdu < 0.0) b.bdu = st.D[(gbase + b.bu) * WAVE + lane];
+            if (b.bdu < 0.0) b.bdu = st.D[sidx<L>(g, n, b.bu, j)];
             better = (du < b.bdu) || (du == b.bdu && u < b.bu);
         }
     }
@@ -228,48 +249,32 @@ __device__ __forceinline__ void offer(Best& b, const DevGraph& G, const State& s
     }
 }
 
-// In-CSR entries [kb, ke) (at most 64) of one vertex, one entry per lane.
-struct Seg {
-    int32_t kb;
-    bool valid;
-    int32_t u_l;    // neighbour id of this lane's entry
-    double w_l;     // relaxation weight of this lane's entry
-};
-
-__device__ __forceinline__ Seg load_segment(int32_t kb, int32_t ke, int32_t lane, const DevGraph& G) {
-    Seg sg;
-    sg.kb = kb;
-    const int32_t k = kb + lane;
-    sg.valid = k < ke;
-    sg.u_l = sg.valid ? G.icol[k] : 0;
-    sg.w_l = sg.valid ? G.iw[k] : 0.0;
-    return sg;
-}
-
-// Candidates of a segment whose in-edge flag is set: rows gathered INFLIGHT at a
-// time, `f(kk, u, du, alt)` called for lanes where it is a valid candidate.
-template <typename F>
-__device__ __forceinline__ void scan_changed(const Seg& sg, uint64_t cm, size_t gbase, int32_t lane, bool active,
-                                             const State& st, F&& f) {
-    while (cm) {
-        int32_t us[INFLIGHT], ks[INFLIGHT];
-        double ws[INFLIGHT], dus[INFLIGHT];
+// Flagged candidates of one L-entry chunk [c0, c0+L) of a vertex's in-list.
+// `sm` = subgroup-relative mask of flagged entries (subgroup-uniform); rows of
+// the flagged neighbours are gathered INFL at a time; f(kk, u, du, alt) is
+// called for lanes where the candidate is a valid improvement path.
+template <int L, int INFL, typename F>
+__device__ __forceinline__ void scan_chunk(uint64_t sm, int32_t c0, int32_t base, int32_t u_j, double w_j, int32_t g,
+                                           int32_t n, int32_t j, bool active, const State& st, F&& f) {
+    while (sm) {
+        int32_t us[INFL], ks[INFL];
+        double ws[INFL], dus[INFL];
 #pragma unroll
-        for (int q = 0; q < INFLIGHT; ++q) {
+        for (int q = 0; q < INFL; ++q) {
             us[q] = -1;
-            if (cm) {
-                const int32_t b = __builtin_ctzll(cm);
-                cm &= cm - 1;
-                us[q] = __builtin_amdgcn_readlane(sg.u_l, b);
-                ks[q] = sg.kb + b;
-                ws[q] = readlane_d(sg.w_l, b);
+            if (sm) {
+                const int32_t b = __builtin_ctzll(sm);
+                sm &= sm - 1;
+                us[q] = sub_get<L>(u_j, base + b);
+                ws[q] = sub_get_d<L>(w_j, base + b);
+                ks[q] = c0 + b;
             }
         }
 #pragma unroll
-        for (int q = 0; q < INFLIGHT; ++q)
-            if (us[q] >= 0) dus[q] = st.D[(gbase + us[q]) * WAVE + lane];
+        for (int q = 0; q < INFL; ++q)
+            if (us[q] >= 0) dus[q] = st.D[sidx<L>(g, n, us[q], j)];
 #pragma unroll
-        for (int q = 0; q < INFLIGHT; ++q) {
+        for (int q = 0; q < INFL; ++q) {
             if (us[q] < 0) continue;
             const double alt = dus[q] + ws[q];
             if (active && alt > dus[q]) f(ks[q], us[q], dus[q], alt);
@@ -278,22 +283,14 @@ __device__ __forceinline__ void scan_changed(const Seg& sg, uint64_t cm, size_t 
 }
 
 // Gather the chosen parent's (R, H, F), write the lane's state if it changed.
-__device__ __forceinline__ bool finish_vertex(Best& b, const DevGraph& G, const State& st, size_t gbase,
-                                              int32_t lane, int32_t v, int32_t s, size_t rv, double d_old,
+template <int L>
+__device__ __forceinline__ bool finish_vertex(Best& b, const DevGraph& G, const State& st, int32_t g, int32_t n,
+                                              int32_t j, int32_t v, int32_t s, size_t rv, double d_old,
                                               int32_t p_old) {
     bool changed = false;
     if (b.need) {
         if (b.bu < 0) b.bu = G.icol[b.bk];
-        if (G.ablate & 1) {
-            changed = (d_old == INF || b.bd != d_old || b.bk != p_old);
-            if (changed) {
-                st.D[rv] = b.bd;
-                st.P[rv] = b.bk;
-            }
-            return __ballot(changed) != 0;
-        }
-        const size_t ru = (gbase + b.bu) * WAVE + lane;
-        const Route pu = st.RT[ru];
+        const Route pu = st.RT[sidx<L>(g, n, b.bu, j)];
         Route nr;
         nr.r = pu.r * G.ia[b.bk];
         nr.h = pu.h + 1;
@@ -310,153 +307,146 @@ __device__ __forceinline__ bool finish_vertex(Best& b, const DevGraph& G, const 
             st.RT[rv] = nr;
         }
     }
-    return __ballot(changed) != 0;
+    return changed;
 }
 
-// (group, v) changed: flag its out-edges for the next round.
-__device__ __forceinline__ void mark_out(const DevGraph& G, int32_t g, int32_t n, int32_t v, int32_t lane,
+// (group, v) changed: flag its out-edges for the next round (L lanes of the subgroup).
+template <int L>
+__device__ __forceinline__ void mark_out(const DevGraph& G, int32_t g, int32_t n, int32_t v, int32_t j,
                                          const Flags& fl) {
     const int32_t o0 = G.optr[v], o1 = G.optr[v + 1];
-    for (int32_t k = o0 + lane; k < o1; k += WAVE) {
+    for (int32_t k = o0 + j; k < o1; k += L) {
         (G.oheavy[k] ? fl.hmark_next : fl.mark_next)[(size_t)g * n + G.ocol[k]] = 1;
         fl.in_next[(size_t)g * G.nrel + G.orev[k]] = 1;
     }
 }
 
-// Everything a light vertex's relaxation loads before it can look at a single
-// candidate row -- issued one vertex ahead (software pipeline, see k_relax).
-struct Pre {
-    int32_t g, v, k0;
-    int32_t s;          // this lane's source
-    Seg sg;             // in-CSR slice (one entry per lane)
-    bool f;             // this lane's in-edge changed last round
-    int32_t orev_l;     // reverse entry of this lane's edge (undirected marking)
-    bool heavy_l;       // this lane's neighbour is heavy (undirected marking)
-    double d_old;
-    int32_t p_old;
-};
-
-__device__ __forceinline__ void prefetch_vertex(Pre& p, int32_t g, int32_t v, int32_t n, int32_t lane,
-                                                const int32_t* __restrict__ srcv, const DevGraph& G,
-                                                const State& st, const Flags& fl) {
-    p.g = g;
-    p.v = v;
-    p.k0 = G.iptr[v];
-    p.sg = load_segment(p.k0, G.iptr[v + 1], lane, G);
-    p.s = srcv[g * WAVE + lane];
-    const size_t rv = ((size_t)g * n + v) * WAVE + lane;
-    p.d_old = st.D[rv];
-    p.p_old = st.P[rv];
-    p.f = p.sg.valid && fl.in_cur[(size_t)g * G.nrel + p.k0 + lane] != 0;
-    p.orev_l = 0;
-    p.heavy_l = false;
-    if (G.undirected && p.sg.valid) {
-        p.orev_l = G.orev[p.k0 + lane];
-        p.heavy_l = G.oheavy[p.k0 + lane] != 0;
+// Relaxation of one light (in-degree <= 64) item e = g * n + v by one subgroup
+// (lane j = source g*L + j); e < 0: this subgroup has no item (it still takes
+// part in the wave-wide ballots).  Returns this lane's "changed".
+template <int L, int INFL>
+__device__ __forceinline__ bool relax_item(int64_t e, int32_t n, int32_t j, int32_t base,
+                                           const int32_t* __restrict__ srcv, const DevGraph& G, const State& st,
+                                           const Flags& fl) {
+    int32_t g = 0, v = 0, k0 = 0, k1 = 0, s = -1;
+    double d_old = INF;
+    int32_t p_old = -1;
+    if (e >= 0) {
+        g = (int32_t)(e / n);
+        v = (int32_t)(e - (int64_t)g * n);
+        k0 = G.iptr[v];
+        k1 = G.iptr[v + 1];
+        s = srcv[g * L + j];
     }
-}
-
-// Relaxation of one light (in-degree <= 64) (group, v) for the 64 sources of
-// the group (lane = source).  Returns the wave-uniform "some lane changed".
-__device__ __forceinline__ bool relax_vertex(const Pre& p, int32_t n, int32_t lane, const DevGraph& G,
-                                             const State& st, const Flags& fl) {
-    const int32_t g = p.g, v = p.v;
-    const size_t gbase = (size_t)g * n;
-    const size_t rv = (gbase + v) * WAVE + lane;
-    const bool active = (p.s >= 0) && (p.s != v);
-    const uint64_t cm = __ballot(p.f);
-    if (p.f) fl.in_cur[(size_t)g * G.nrel + p.k0 + lane] = 0;   // consumed
-    Best b{p.d_old, p.p_old, -1, -1.0, false};
-    scan_changed(p.sg, cm, gbase, lane, active, st,
-                 [&](int32_t kk, int32_t u, double du, double alt) { offer(b, G, st, gbase, lane, kk, u, du, alt); });
-    const bool changed = finish_vertex(b, G, st, gbase, lane, v, p.s, rv, p.d_old, p.p_old);
-    if (changed) {
-        if (G.undirected) {   // out-list == in-list, already in registers
-            if (p.sg.valid) {
-                (p.heavy_l ? fl.hmark_next : fl.mark_next)[gbase + p.sg.u_l] = 1;
-                fl.in_next[(size_t)g * G.nrel + p.orev_l] = 1;
+    const size_t rv = sidx<L>(g, n, v, j);
+    if (e >= 0) {
+        d_old = st.D[rv];
+        p_old = st.P[rv];
+    }
+    const bool active = (e >= 0) && (s >= 0) && (s != v);
+    Best b{d_old, p_old, -1, -1.0, false};
+    // undirected graphs: the out-list IS the in-list; a single-chunk vertex keeps
+    // what marking needs (neighbour, reverse entry, heavy bit) in registers
+    int32_t u_last = 0, orev_last = 0;
+    bool heavy_last = false, ok_last = false;
+    for (int32_t c0 = k0; c0 < k1; c0 += L) {   // subgroup-uniform trip count
+        const int32_t k = c0 + j;
+        const bool ok = k < k1;
+        const int32_t u_j = ok ? G.icol[k] : 0;
+        const double w_j = ok ? G.iw[k] : 0.0;
+        const size_t fo = (size_t)g * G.nrel + k;
+        const bool f = ok && fl.in_cur[fo] != 0;
+        if (G.undirected && ok) {
+            orev_last = G.orev[k];
+            heavy_last = G.oheavy[k] != 0;
+        }
+        u_last = u_j;
+        ok_last = ok;
+        if (f) fl.in_cur[fo] = 0;   // consumed
+        const uint64_t sm = (__ballot(f) >> base) & Sub<L>::MASK;
+        scan_chunk<L, INFL>(sm, c0, base, u_j, w_j, g, n, j, active, st,
+                            [&](int32_t kk, int32_t u, double du, double alt) { offer<L>(b, G, st, g, n, j, kk, u, du, alt); });
+    }
+    bool changed = false;
+    if (e >= 0) changed = finish_vertex<L>(b, G, st, g, n, j, v, s, rv, d_old, p_old);
+    const bool any = ((__ballot(changed) >> base) & Sub<L>::MASK) != 0;
+    if (any) {
+        if (G.undirected && k1 - k0 <= L) {
+            if (ok_last) {
+                (heavy_last ? fl.hmark_next : fl.mark_next)[(size_t)g * n + u_last] = 1;
+                fl.in_next[(size_t)g * G.nrel + orev_last] = 1;
             }
         } else {
-            mark_out(G, g, n, v, lane, fl);
+            mark_out<L>(G, g, n, v, j, fl);
         }
     }
     return changed;
 }
-
-// Cursor over this wave's 8-flag units of the light frontier bitmap.  The next
-// unit's word is loaded one unit ahead; a unit is cleared as soon as it is taken.
-struct Cursor {
-    int64_t u8, stride, units;
-    uint64_t w, w_ahead;
-};
 
 __device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
     return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
            (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 
-__device__ __forceinline__ bool cursor_next(Cursor& c, uint64_t* words, int32_t total, int32_t n, int32_t lane,
-                                            int32_t& g, int32_t& v) {
-    for (;;) {
-        if (c.w) {
-            const int32_t bit = __builtin_ctzll(c.w) >> 3;
-            c.w &= ~(0xFFull << (8 * bit));
-            const int32_t e = (int32_t)(c.u8 * 8) + bit;
-            if (e >= total) continue;
-            g = e / n;
-            v = e - g * n;
-            return true;
-        }
-        c.u8 += c.stride;
-        if (c.u8 >= c.units) return false;
-        c.w = uniform_u64(c.w_ahead);
-        if (c.w && lane == 0) words[c.u8] = 0;   // taken
-        const int64_t ahead = c.u8 + c.stride;
-        c.w_ahead = ahead < c.units ? words[ahead] : 0;
-    }
+// nonzero bytes of w -> bit per byte
+__device__ __forceinline__ uint32_t byte_mask(uint64_t w) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) m |= ((w >> (8 * q)) & 0xFF) ? (1u << q) : 0u;
+    return m;
 }
 
 // One relaxation round over the dense light-frontier bitmap.  Work unit = 8
-// consecutive (group, vertex) flags read as one 64-bit word (marked vertices
-// spread over the grid's waves).  Two-stage software pipeline per wave: the
-// CSR slice, change flags and state of the NEXT marked vertex are in flight
-// while the current one gathers its candidate rows and parent route.
+// consecutive (group, vertex) flags read as one 64-bit word; the wave's V
+// subgroups take its marked items V at a time (V = 64/L items in flight per
+// wave).  XCD-aware split (speed only, never correctness): blocks are dealt
+// round-robin over the 8 XCDs, so blocks with equal blockIdx % 8 share an L2;
+// each such class gets one contiguous eighth of the (group, vertex) space.
+template <int L, int INFL>
 __global__ __launch_bounds__(BLOCK) void k_relax(int32_t total, int32_t n, const int32_t* __restrict__ srcv,
                                                  DevGraph G, State st, Flags fl) {
+    constexpr int V = Sub<L>::V;
     const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int32_t sub = lane / L, j = lane % L, base = sub * L;
     uint64_t* words = reinterpret_cast<uint64_t*>(fl.mark_cur);
-    // XCD-aware split (speed only, never correctness): blocks are dealt round-robin
-    // over the 8 XCDs, so blocks with equal blockIdx % 8 share an L2.  Give each
-    // such class one contiguous eighth of the (group, vertex) space -- about G/8
-    // whole groups -- so a group's hot rows (hubs) live in one XCD's L2.
     const int64_t all_units = ((int64_t)total + 7) >> 3;   // mark buffers padded to 8 bytes
     const int32_t xcd = blockIdx.x & 7;
     const int64_t waves_per_xcd = ((int64_t)(gridDim.x >> 3) * BLOCK) >> 6;
     const int64_t wave = ((int64_t)(blockIdx.x >> 3) * BLOCK + threadIdx.x) >> 6;
     const int64_t lo = all_units * xcd / 8, hi = all_units * (xcd + 1) / 8;
-    Cursor c;
-    c.stride = waves_per_xcd;
-    c.units = hi;
-    c.u8 = lo + wave - c.stride;
-    c.w = 0;
-    c.w_ahead = lo + wave < hi ? words[lo + wave] : 0;
     bool wrote = false;
-    int32_t g, v;
-    Pre cur, nxt;
-    bool has = cursor_next(c, words, total, n, lane, g, v);
-    if (has) prefetch_vertex(nxt, g, v, n, lane, srcv, G, st, fl);
-    while (has) {
-        cur = nxt;
-        has = cursor_next(c, words, total, n, lane, g, v);
-        if (has) prefetch_vertex(nxt, g, v, n, lane, srcv, G, st, fl);
-        wrote |= relax_vertex(cur, n, lane, G, st, fl);
+    int64_t u8 = lo + wave;
+    uint64_t w_ahead = u8 < hi ? words[u8] : 0;
+    for (; u8 < hi; u8 += waves_per_xcd) {
+        const uint64_t w = uniform_u64(w_ahead);
+        const int64_t nx = u8 + waves_per_xcd;
+        w_ahead = nx < hi ? words[nx] : 0;
+        if (!w) continue;
+        if (lane == 0) words[u8] = 0;   // taken
+        uint32_t bm = byte_mask(w);
+        while (bm) {
+            // subgroup `sub` takes the sub-th marked byte of the next V
+            uint32_t t = bm;
+            int32_t mine = -1;
+#pragma unroll
+            for (int q = 0; q < V; ++q) {
+                if (!t) break;
+                const int32_t bit = __builtin_ctz(t);
+                t &= t - 1;
+                if (q == sub) mine = bit;
+            }
+            bm = t;
+            int64_t e = mine >= 0 ? u8 * 8 + mine : -1;
+            if (e >= total) e = -1;
+            wrote |= relax_item<L, INFL>(e, n, j, base, srcv, G, st, fl);
+        }
     }
-    if (wrote && lane == 0) *fl.any_changed = 1;   // at most one plain store per wave
+    if (__ballot(wrote) && lane == 0) *fl.any_changed = 1;   // at most one plain store per wave
 }
 
 // Heavy vertices: their in-neighbour lists are cut into 64-entry segments; one
-// wave per (group, segment) computes the lexicographic best changed candidate
-// of its segment (no comparison with the stored state).
+// subgroup per (group, segment) computes the lexicographic best changed
+// candidate of its segment (no comparison with the stored state).
 struct HeavyPlan {
     int32_t nseg;                 // segments over all heavy vertices
     int32_t nheavy;
@@ -466,82 +456,117 @@ struct HeavyPlan {
     const int32_t* heavy_seg0;    // [nheavy + 1] segment range of each heavy vertex
 };
 
-struct Partial {                  // [group][segment][lane]
+struct Partial {                  // [group][segment][L]
     double* alt;
     double* du;
     int2* uk;                     // (u, k), u = -1: no candidate
 };
 
+template <int L, int INFL = Sub<L>::INFL>
 __global__ __launch_bounds__(BLOCK) void k_heavy_partial(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
                                                          DevGraph G, State st, HeavyPlan hp, Partial pp, Flags fl) {
+    constexpr int V = Sub<L>::V;
     const int32_t lane = threadIdx.x & (WAVE - 1);
-    const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
+    const int32_t sub = lane / L, j = lane % L, base = sub * L;
+    const int64_t nsub = (((int64_t)gridDim.x * BLOCK) >> 6) * V;
     const int64_t items = (int64_t)groups * hp.nseg;
-    for (int64_t it = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it < items; it += nwaves) {
-        const int32_t g = (int32_t)(it / hp.nseg);
-        const int32_t sgi = (int32_t)(it - (int64_t)g * hp.nseg);
-        const int32_t v = hp.seg_vertex[sgi];
-        const size_t gbase = (size_t)g * n;
-        if (!fl.hmark_cur[gbase + v]) continue;
-        const int32_t s = srcv[g * WAVE + lane];
-        const bool active = (s >= 0) && (s != v);
-        const int32_t kb = hp.seg_begin[sgi];
-        const Seg sg = load_segment(kb, min(kb + WAVE, G.iptr[v + 1]), lane, G);
-        const size_t fo = (size_t)g * G.nrel + kb + lane;
-        const bool f = sg.valid && fl.in_cur[fo] != 0;
-        const uint64_t cm = __ballot(f);
-        if (f) fl.in_cur[fo] = 0;
+    const int64_t first = ((((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6) * V) + sub;
+    const int64_t rounds = (items + nsub - 1) / nsub;   // wave-uniform loop count
+    for (int64_t r = 0; r < rounds; ++r) {
+        const int64_t it = first + r * nsub;
+        bool item = it < items;
+        int32_t g = 0, sgi = 0, v = 0;
+        if (item) {
+            g = (int32_t)(it / hp.nseg);
+            sgi = (int32_t)(it - (int64_t)g * hp.nseg);
+            v = hp.seg_vertex[sgi];
+            item = fl.hmark_cur[(size_t)g * n + v] != 0;
+        }
+        int32_t kb = 0, ke = 0, s = -1;
+        if (item) {
+            kb = hp.seg_begin[sgi];
+            ke = min(kb + WAVE, G.iptr[v + 1]);
+            s = srcv[g * L + j];
+        }
+        const bool active = item && (s >= 0) && (s != v);
         double ba = INF, bdu = INF;
         int32_t bu = -1, bk = -1;
-        scan_changed(sg, cm, gbase, lane, active, st, [&](int32_t kk, int32_t u, double du, double alt) {
-            if (alt < ba || (alt == ba && (du < bdu || (du == bdu && u < bu)))) {
-                ba = alt;
-                bdu = du;
-                bu = u;
-                bk = kk;
-            }
-        });
-        const size_t o = ((size_t)g * hp.nseg + sgi) * WAVE + lane;
-        pp.alt[o] = ba;
-        pp.du[o] = bdu;
-        pp.uk[o] = make_int2(bu, bk);
+        for (int32_t c0 = kb; c0 < ke; c0 += L) {
+            const int32_t k = c0 + j;
+            const bool ok = k < ke;
+            const int32_t u_j = ok ? G.icol[k] : 0;
+            const double w_j = ok ? G.iw[k] : 0.0;
+            const size_t fo = (size_t)g * G.nrel + k;
+            const bool f = ok && fl.in_cur[fo] != 0;
+            if (f) fl.in_cur[fo] = 0;
+            const uint64_t sm = (__ballot(f) >> base) & Sub<L>::MASK;
+            scan_chunk<L, INFL>(sm, c0, base, u_j, w_j, g, n, j, active, st,
+                          [&](int32_t kk, int32_t u, double du, double alt) {
+                              if (alt < ba || (alt == ba && (du < bdu || (du == bdu && u < bu)))) {
+                                  ba = alt;
+                                  bdu = du;
+                                  bu = u;
+                                  bk = kk;
+                              }
+                          });
+        }
+        if (item) {
+            const size_t o = ((size_t)g * hp.nseg + sgi) * L + j;
+            pp.alt[o] = ba;
+            pp.du[o] = bdu;
+            pp.uk[o] = make_int2(bu, bk);
+        }
     }
 }
 
 // Combine the segment partials of each marked heavy (group, v) into its state.
+template <int L>
 __global__ __launch_bounds__(BLOCK) void k_heavy_combine(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
                                                          DevGraph G, State st, HeavyPlan hp, Partial pp, Flags fl) {
+    constexpr int V = Sub<L>::V;
     const int32_t lane = threadIdx.x & (WAVE - 1);
-    const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
+    const int32_t sub = lane / L, j = lane % L, base = sub * L;
+    const int64_t nsub = (((int64_t)gridDim.x * BLOCK) >> 6) * V;
     const int64_t items = (int64_t)groups * hp.nheavy;
+    const int64_t first = ((((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6) * V) + sub;
+    const int64_t rounds = (items + nsub - 1) / nsub;
     bool wrote = false;
-    for (int64_t it = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it < items; it += nwaves) {
-        const int32_t g = (int32_t)(it / hp.nheavy);
-        const int32_t h = (int32_t)(it - (int64_t)g * hp.nheavy);
-        const int32_t v = hp.heavy_vertex[h];
-        const size_t gbase = (size_t)g * n;
-        if (!fl.hmark_cur[gbase + v]) continue;
-        const int32_t s = srcv[g * WAVE + lane];
-        const size_t rv = (gbase + v) * WAVE + lane;
-        const double d_old = st.D[rv];
-        const int32_t p_old = st.P[rv];
-        Best b{d_old, p_old, -1, -1.0, false};
-        for (int32_t sgi = hp.heavy_seg0[h]; sgi < hp.heavy_seg0[h + 1]; ++sgi) {
-            const size_t o = ((size_t)g * hp.nseg + sgi) * WAVE + lane;
-            const int2 uk = pp.uk[o];
-            if (uk.x >= 0) offer(b, G, st, gbase, lane, uk.y, uk.x, pp.du[o], pp.alt[o]);
+    for (int64_t r = 0; r < rounds; ++r) {
+        const int64_t it = first + r * nsub;
+        bool item = it < items;
+        int32_t g = 0, h = 0, v = 0;
+        if (item) {
+            g = (int32_t)(it / hp.nheavy);
+            h = (int32_t)(it - (int64_t)g * hp.nheavy);
+            v = hp.heavy_vertex[h];
+            item = fl.hmark_cur[(size_t)g * n + v] != 0;
         }
-        if (lane == 0) fl.hmark_cur[gbase + v] = 0;
-        if (finish_vertex(b, G, st, gbase, lane, v, s, rv, d_old, p_old)) {
-            mark_out(G, g, n, v, lane, fl);
+        bool changed = false;
+        if (item) {
+            const int32_t s = srcv[g * L + j];
+            const size_t rv = sidx<L>(g, n, v, j);
+            const double d_old = st.D[rv];
+            const int32_t p_old = st.P[rv];
+            Best b{d_old, p_old, -1, -1.0, false};
+            for (int32_t sgi = hp.heavy_seg0[h]; sgi < hp.heavy_seg0[h + 1]; ++sgi) {
+                const size_t o = ((size_t)g * hp.nseg + sgi) * L + j;
+                const int2 uk = pp.uk[o];
+                if (uk.x >= 0) offer<L>(b, G, st, g, n, j, uk.y, uk.x, pp.du[o], pp.alt[o]);
+            }
+            if (j == 0) fl.hmark_cur[(size_t)g * n + v] = 0;
+            changed = finish_vertex<L>(b, G, st, g, n, j, v, s, rv, d_old, p_old);
+        }
+        const bool any = ((__ballot(changed) >> base) & Sub<L>::MASK) != 0;
+        if (any) {
+            mark_out<L>(G, g, n, v, j, fl);
             wrote = true;
         }
     }
-    if (wrote && lane == 0) *fl.any_changed = 1;
+    if (__ballot(wrote) && lane == 0) *fl.any_changed = 1;
 }
 
 // (s, s) entry: DIRECT self-loop, the row's [s] path, or the SELF rule.
-__device__ __forceinline__ void self_entry(const DevGraph& G, const RowMode& md, int32_t s, double& L,
+__device__ __forceinline__ void self_entry(const DevGraph& G, const RowMode& md, int32_t s, double& L_,
                                            double& R, int32_t& N, int32_t& H) {
     const double fs = G.vfac[s];
     const double lw = G.loop_w[s];
@@ -552,7 +577,7 @@ __device__ __forceinline__ void self_entry(const DevGraph& G, const RowMode& md,
         if (has_attr(fs)) r *= fs;
         if (has_attr(fs)) r *= fs;
         r *= G.loop_a[s];
-        L = 0.0 + lw;
+        L_ = 0.0 + lw;
         R = r;
         N = s;
         H = 1;
@@ -562,12 +587,12 @@ __device__ __forceinline__ void self_entry(const DevGraph& G, const RowMode& md,
         r *= G.loop_a[s];
         double l = 0.0 + lw;
         if (l == 0) l = 1;
-        L = l;
+        L_ = l;
         R = r;
         N = s;
         H = 1;
     } else if (G.self_other[s] >= 0) {                   // SELF rule
-        L = G.self_w2[s];
+        L_ = G.self_w2[s];
         R = G.self_a2[s];
         N = G.self_other[s];
         H = 2;
@@ -575,7 +600,7 @@ __device__ __forceinline__ void self_entry(const DevGraph& G, const RowMode& md,
 }
 
 // DIRECT (s, t != s): first edge s->t in the out-CSR (merged, get_eid's edge).
-__device__ __forceinline__ bool direct_entry(const DevGraph& G, int32_t s, int32_t t, double& L, double& R,
+__device__ __forceinline__ bool direct_entry(const DevGraph& G, int32_t s, int32_t t, double& L_, double& R,
                                              int32_t& N, int32_t& H) {
     int32_t lo = G.optr[s], hi = G.optr[s + 1];
     while (lo < hi) {
@@ -589,40 +614,43 @@ __device__ __forceinline__ bool direct_entry(const DevGraph& G, int32_t s, int32
     if (has_attr(fs)) r *= fs;
     if (has_attr(ft)) r *= ft;
     r *= G.oarep[lo];
-    L = 0.0 + G.owrep[lo];
+    L_ = 0.0 + G.owrep[lo];
     R = r;
     N = t;
     H = 1;
     return true;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t groups, int32_t sb0,
+// State -> table rows.  One wave per (64-source block of the batch, target
+// slot): lane l = source b*64 + l, i.e. lane group b*(64/L) + l/L, lane l%L.
+template <int L>
+__global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, int32_t sb0,
                                                      const int32_t* __restrict__ srcv,
                                                      const int32_t* __restrict__ slot_vertex, DevGraph G,
                                                      RowMode md, State st, Table tb) {
     const int32_t lane = threadIdx.x & (WAVE - 1);
     const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
-    const int64_t items = (int64_t)groups * tb.A;
+    const int64_t items = (int64_t)blocks * tb.A;
     for (int64_t it = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it < items; it += nwaves) {
-        const int32_t g = (int32_t)(it / tb.A);
-        const int32_t j = (int32_t)(it - (int64_t)g * tb.A);
-        const int32_t t = slot_vertex[j];
-        const int32_t s = srcv[g * WAVE + lane];
-        double L = -1.0, R = -1.0;
+        const int32_t b = (int32_t)(it / tb.A);
+        const int32_t jt = (int32_t)(it - (int64_t)b * tb.A);
+        const int32_t t = slot_vertex[jt];
+        const int32_t g = b * (WAVE / L) + lane / L, j = lane % L;
+        const int32_t s = srcv[b * WAVE + lane];
+        double Lt = -1.0, R = -1.0;
         int32_t N = -1, H = 0;
         if (s >= 0) {
             if (t == s) {
-                self_entry(G, md, s, L, R, N, H);
+                self_entry(G, md, s, Lt, R, N, H);
             } else {
-                const size_t gbase = (size_t)g * n;
-                const size_t rt = (gbase + t) * WAVE + lane;
+                const size_t rt = sidx<L>(g, n, t, j);
                 const double d = st.D[rt];
                 if (d < INF) {
                     const Route rr = st.RT[rt];
                     const double ft = G.vfac[t];
                     const bool fast = (!has_attr(ft) || ft == 1.0) && !md.multi_rep;
                     if (fast) {
-                        L = d;
+                        Lt = d;
                         R = rr.r;
                     } else {
                         // path-order re-fold, shd-topology.c:1413-1493 (rare: vertex loss on
@@ -634,27 +662,28 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t groups, 
                         const int32_t h = rr.h;
                         for (int32_t i = 1; i <= h; ++i) {
                             int32_t x = t;
-                            for (int32_t q = 0; q < h - i; ++q) x = G.icol[st.P[(gbase + x) * WAVE + lane]];
-                            const int32_t k = st.P[(gbase + x) * WAVE + lane];
+                            for (int32_t q = 0; q < h - i; ++q) x = G.icol[st.P[sidx<L>(g, n, x, j)]];
+                            const int32_t k = st.P[sidx<L>(g, n, x, j)];
                             l += G.iwrep[k];
                             r *= G.ia[k];
                         }
-                        L = l;
+                        Lt = l;
                         R = r;
                     }
-                    if (L == 0) L = 1;   // shd-topology.c:1833-1837
+                    if (Lt == 0) Lt = 1;   // shd-topology.c:1833-1837
                     N = rr.f;
                     H = rr.h;
                 }
             }
         }
-        const size_t o = tidx(sb0 + g, tb.A, j, lane);
-        tb.lat[o] = L;
+        const size_t o = tidx(sb0 + b, tb.A, jt, lane);
+        tb.lat[o] = Lt;
         tb.rel[o] = R;
         tb.next[o] = N;
         tb.hops[o] = (uint16_t)(H > 65535 ? 65535 : H);
     }
 }
+
 
 __global__ __launch_bounds__(BLOCK) void k_rows_direct(int32_t groups, int32_t sb0,
                                                        const int32_t* __restrict__ srcv,
@@ -757,7 +786,9 @@ struct spe_table {
     spe_graph* g = nullptr;
     int32_t A = 0;
     int32_t blk0 = 0, blk1 = 0;
-    int32_t groups = 8;
+    int32_t groups = 8;            // 64-source blocks per batch
+    int32_t lanes = 16;            // sources per lane group (L)
+    int32_t infl = 8;              // neighbour rows in flight per subgroup (4 or 8)
     RowMode md{};
     bool ext = false;
     bool built = false;
@@ -1011,6 +1042,16 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         groups = (int32_t)std::max(1.0, std::min(16.0, 4.0e9 / per_group));
     }
     t->groups = std::max(1, std::min(groups, std::max(1, t->blk1 - t->blk0)));
+    // sources per lane group (shared frontier); 64/L groups per 64-source block
+    int32_t lanes = o.lanes_per_group;
+    if (lanes <= 0 && getenv("SPE_LANES")) lanes = atoi(getenv("SPE_LANES"));
+    if (lanes <= 0) lanes = 64;
+    if (lanes != 16 && lanes != 32 && lanes != 64) {
+        delete t;
+        return fail(SPE_EINVAL, "lanes_per_group must be 16, 32 or 64");
+    }
+    t->lanes = lanes;
+    t->infl = (getenv("SPE_INFL") && atoi(getenv("SPE_INFL")) == 4) ? 4 : (getenv("SPE_INFL") ? 8 : (lanes == 64 ? 8 : 4));
     t->tb.A = n_attached;
     const size_t elems = (size_t)(t->blk1 - t->blk0) * n_attached * WAVE;
     int r = SPE_OK;
@@ -1046,18 +1087,19 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     TRY(dev_upload(t->allocs, vslot, &tmp));
     t->d_vertex_slot = const_cast<int32_t*>(tmp);
     const size_t G = (size_t)t->groups;
+    const size_t GL = G * (WAVE / t->lanes);   // lane groups per batch
     if (!t->md.complete) {
         const size_t se = G * n * WAVE;
         TRY(dev_alloc(t->allocs, &t->st.D, se));
         TRY(dev_alloc(t->allocs, &t->st.P, se));
         TRY(dev_alloc(t->allocs, &t->st.RT, se));
         const size_t nrel = std::max<size_t>(1, g->hg.icol.size());
-        TRY(dev_alloc(t->allocs, &t->inflag[0], G * nrel));
-        TRY(dev_alloc(t->allocs, &t->inflag[1], G * nrel));
-        TRY(dev_alloc(t->allocs, &t->mark[0], (G * n + 8) & ~(size_t)7));
-        TRY(dev_alloc(t->allocs, &t->mark[1], (G * n + 8) & ~(size_t)7));
-        TRY(dev_alloc(t->allocs, &t->hmark[0], G * n));
-        TRY(dev_alloc(t->allocs, &t->hmark[1], G * n));
+        TRY(dev_alloc(t->allocs, &t->inflag[0], GL * nrel));
+        TRY(dev_alloc(t->allocs, &t->inflag[1], GL * nrel));
+        TRY(dev_alloc(t->allocs, &t->mark[0], (GL * n + 8) & ~(size_t)7));
+        TRY(dev_alloc(t->allocs, &t->mark[1], (GL * n + 8) & ~(size_t)7));
+        TRY(dev_alloc(t->allocs, &t->hmark[0], GL * n));
+        TRY(dev_alloc(t->allocs, &t->hmark[1], GL * n));
         const size_t pe = G * std::max<size_t>(1, (size_t)g->hp.nseg) * WAVE;
         TRY(dev_alloc(t->allocs, &t->pp.alt, pe));
         TRY(dev_alloc(t->allocs, &t->pp.du, pe));
@@ -1113,12 +1155,20 @@ static int resolve_profile(spe_table* t) {
     return SPE_OK;
 }
 
-static int relax_to_convergence(spe_table* t, int32_t groups, hipStream_t s) {
+extern "C++" {
+template <int L, int INFL>
+static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     const spe_graph* g = t->g;
     const int32_t n = g->hg.n;
     const int32_t nrel = (int32_t)g->hg.icol.size();
+    const int32_t groups = blocks * (WAVE / L);    // lane groups
     const int64_t total = (int64_t)groups * n;
-    const int relax_grid = (grid_for((total + 7) / 8 * WAVE, BLOCK, 2048) + 7) & ~7;   // multiple of 8 (XCD split)
+    // one resident wave per hardware slot (no second wave of late blocks), multiple of 8 (XCD split)
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_relax<L, INFL>, BLOCK, 0) != hipSuccess || per_cu < 1)
+        per_cu = 4;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus < 1) cus = 256;
+    const int relax_grid = (grid_for((total + 7) / 8 * WAVE, BLOCK, per_cu * cus) + 7) & ~7;
     HIP_TRY(hipMemsetAsync(t->counts, 0, sizeof(int32_t) * ((size_t)t->max_iters + 2), s));
     for (int i = 0; i < 2; ++i) {   // consumers clear what they read; this only guards a failed batch
         HIP_TRY(hipMemsetAsync(t->inflag[i], 0, (size_t)groups * std::max(1, nrel), s));
@@ -1127,14 +1177,15 @@ static int relax_to_convergence(spe_table* t, int32_t groups, hipStream_t s) {
     }
     {
         LaunchTimer lt(t, s, SPE_K_INIT);
-        k_init_state<<<grid_for(total * WAVE, BLOCK, 8192), BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev.vfac, t->st);
+        k_init_state<L><<<grid_for(total * L, BLOCK, 8192), BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev.vfac, t->st);
     }
     {
         LaunchTimer lt(t, s, SPE_K_SEED);
         // the sources "changed in round 0": their out-edges form round 1's frontier
-        k_seed<<<(groups * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(n, nrel, groups, t->d_srcv, g->dev, t->mark[1],
+        k_seed<L><<<(groups * L + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev, t->mark[1],
                                                                      t->hmark[1], t->inflag[1]);
     }
+    const int64_t subs_per_wave = WAVE / L;
     int32_t it = 1;
     int32_t check_every = 8;
     for (;;) {
@@ -1144,14 +1195,16 @@ static int relax_to_convergence(spe_table* t, int32_t groups, hipStream_t s) {
                      t->hmark[(it + 1) & 1], t->inflag[it & 1], t->inflag[(it + 1) & 1], t->counts + it};
             {
                 LaunchTimer lt(t, s, SPE_K_RELAX);
-                k_relax<<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcv, g->dev, t->st, fl);
+                k_relax<L, INFL><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcv, g->dev, t->st, fl);
             }
             if (g->hp.nheavy > 0) {
                 LaunchTimer lt(t, s, SPE_K_HEAVY);
-                k_heavy_partial<<<grid_for((int64_t)groups * g->hp.nseg * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
-                    groups, n, t->d_srcv, g->dev, t->st, g->hp, t->pp, fl);
-                k_heavy_combine<<<grid_for((int64_t)groups * g->hp.nheavy * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
-                    groups, n, t->d_srcv, g->dev, t->st, g->hp, t->pp, fl);
+                const int64_t pw = ((int64_t)groups * g->hp.nseg + subs_per_wave - 1) / subs_per_wave;
+                const int64_t cw = ((int64_t)groups * g->hp.nheavy + subs_per_wave - 1) / subs_per_wave;
+                k_heavy_partial<L><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcv, g->dev,
+                                                                                      t->st, g->hp, t->pp, fl);
+                k_heavy_combine<L><<<grid_for(cw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcv, g->dev,
+                                                                                      t->st, g->hp, t->pp, fl);
             }
         }
         HIP_TRY(hipMemcpyAsync(t->h_counts, t->counts + it - 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -1170,6 +1223,28 @@ static int relax_to_convergence(spe_table* t, int32_t groups, hipStream_t s) {
     t->stats.iterations += it - 1;
     return SPE_OK;
 }
+
+static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
+    const bool deep = t->infl == 8;
+    switch (t->lanes) {
+        case 16: return deep ? relax_to_convergence_l<16, 8>(t, blocks, s) : relax_to_convergence_l<16, 4>(t, blocks, s);
+        case 32: return deep ? relax_to_convergence_l<32, 8>(t, blocks, s) : relax_to_convergence_l<32, 4>(t, blocks, s);
+        default: return deep ? relax_to_convergence_l<64, 8>(t, blocks, s) : relax_to_convergence_l<64, 4>(t, blocks, s);
+    }
+}
+
+static void launch_rows_sssp(spe_table* t, int grid, int32_t blocks, int32_t sb0, hipStream_t s) {
+    const spe_graph* g = t->g;
+#define ROWS(LL) k_rows_sssp<LL><<<grid, BLOCK, 0, s>>>(g->hg.n, blocks, sb0, t->d_srcv, t->d_slot_vertex, g->dev, \
+                                                         t->md, t->st, t->tb)
+    switch (t->lanes) {
+        case 16: ROWS(16); break;
+        case 32: ROWS(32); break;
+        default: ROWS(64); break;
+    }
+#undef ROWS
+}
+}  // extern "C++"
 
 int spe_table_build(spe_table* t, void* stream) {
     if (!t) return fail(SPE_EINVAL, "NULL table");
@@ -1205,8 +1280,7 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
             if (r) return r;
             {
                 LaunchTimer lt(t, s, SPE_K_ROWS);
-                k_rows_sssp<<<row_grid, BLOCK, 0, s>>>(g->hg.n, groups, sb0, t->d_srcv, t->d_slot_vertex, g->dev,
-                                                       t->md, t->st, t->tb);
+                launch_rows_sssp(t, row_grid, groups, sb0, s);
             }
             if (t->md.prefer) {
                 LaunchTimer lt(t, s, SPE_K_DIRECT);
@@ -1358,3 +1432,4 @@ void spe_table_free(spe_table* t) {
 }
 
 }  // extern "C"
+

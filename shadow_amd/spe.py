@@ -44,7 +44,8 @@ class TableOpts(C.Structure):
     _fields_ = [("self_mode", C.c_int32), ("force_sssp", C.c_int32), ("groups_per_launch", C.c_int32),
                 ("block_begin", C.c_int32), ("block_end", C.c_int32),
                 ("ext_latency", C.c_void_p), ("ext_reliability", C.c_void_p),
-                ("ext_next_hop", C.c_void_p), ("ext_hops", C.c_void_p), ("ext_filled", C.c_int32)]
+                ("ext_next_hop", C.c_void_p), ("ext_hops", C.c_void_p), ("ext_filled", C.c_int32),
+                ("lanes_per_group", C.c_int32)]
 
 
 class TableLayout(C.Structure):
@@ -167,7 +168,7 @@ class PathTable:
     """spe_table: the per-(source, target) path table for attached vertices."""
 
     def __init__(self, graph: Graph, attached, self_mode: int = SPE_SELF_ROW, force_sssp: bool = False,
-                 groups: int = 0, blocks=None, ext=None, ext_filled: bool = False):
+                 groups: int = 0, blocks=None, ext=None, ext_filled: bool = False, lanes: int = 0):
         self.graph = graph
         self.attached = np.ascontiguousarray(attached, np.int32)
         self.A = int(self.attached.shape[0])
@@ -175,6 +176,7 @@ class PathTable:
         o.self_mode = int(self_mode)
         o.force_sssp = int(bool(force_sssp))
         o.groups_per_launch = int(groups)
+        o.lanes_per_group = int(lanes)
         if blocks is not None:
             o.block_begin, o.block_end = int(blocks[0]), int(blocks[1])
         if ext is not None:  # four device pointers (ints)
