@@ -290,6 +290,14 @@ __device__ __forceinline__ bool finish_vertex(Best& b, const DevGraph& G, const 
     bool changed = false;
     if (b.need) {
         if (b.bu < 0) b.bu = G.icol[b.bk];
+        if (G.ablate & 1) {   // diagnostic only: distances + parents, no route records
+            changed = (d_old == INF || b.bd != d_old || b.bk != p_old);
+            if (changed) {
+                st.D[rv] = b.bd;
+                st.P[rv] = b.bk;
+            }
+            return changed;
+        }
         const Route pu = st.RT[sidx<L>(g, n, b.bu, j)];
         Route nr;
         nr.r = pu.r * G.ia[b.bk];
@@ -402,8 +410,8 @@ __device__ __forceinline__ uint32_t byte_mask(uint64_t w) {
 // wave).  XCD-aware split (speed only, never correctness): blocks are dealt
 // round-robin over the 8 XCDs, so blocks with equal blockIdx % 8 share an L2;
 // each such class gets one contiguous eighth of the (group, vertex) space.
-template <int L, int INFL>
-__global__ __launch_bounds__(BLOCK) void k_relax(int32_t total, int32_t n, const int32_t* __restrict__ srcv,
+template <int L, int INFL, int OCC = 1>
+__global__ __launch_bounds__(BLOCK, OCC) void k_relax(int32_t total, int32_t n, const int32_t* __restrict__ srcv,
                                                  DevGraph G, State st, Flags fl) {
     constexpr int V = Sub<L>::V;
     const int32_t lane = threadIdx.x & (WAVE - 1);
@@ -789,6 +797,8 @@ struct spe_table {
     int32_t groups = 8;            // 64-source blocks per batch
     int32_t lanes = 16;            // sources per lane group (L)
     int32_t infl = 8;              // neighbour rows in flight per subgroup (4 or 8)
+    bool trace = getenv("SPE_TRACE") != nullptr;   // diagnostic: per-launch times to stderr
+    int32_t occ = 0;               // diagnostic: forced waves/SIMD of k_relax (0 = compiler's choice)
     RowMode md{};
     bool ext = false;
     bool built = false;
@@ -1051,7 +1061,12 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         return fail(SPE_EINVAL, "lanes_per_group must be 16, 32 or 64");
     }
     t->lanes = lanes;
-    t->infl = (getenv("SPE_INFL") && atoi(getenv("SPE_INFL")) == 4) ? 4 : (getenv("SPE_INFL") ? 8 : (lanes == 64 ? 8 : 4));
+    t->infl = lanes == 64 ? 8 : 4;
+    if (getenv("SPE_INFL")) {
+        const int want = atoi(getenv("SPE_INFL"));
+        if (want == 4 || want == 8 || (lanes == 64 && want == 6)) t->infl = want;
+    }
+    t->occ = getenv("SPE_OCC") ? atoi(getenv("SPE_OCC")) : 0;
     t->tb.A = n_attached;
     const size_t elems = (size_t)(t->blk1 - t->blk0) * n_attached * WAVE;
     int r = SPE_OK;
@@ -1149,6 +1164,7 @@ static int resolve_profile(spe_table* t) {
         HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
         t->kp.ms[r.kind] += ms;
         t->kp.launches[r.kind] += 1;
+        if (t->trace) fprintf(stderr, "spe-trace %d %.4f\n", r.kind, ms);
     }
     t->pending.clear();
     t->ev_next = 0;
@@ -1156,7 +1172,7 @@ static int resolve_profile(spe_table* t) {
 }
 
 extern "C++" {
-template <int L, int INFL>
+template <int L, int INFL, int OCC = 1>
 static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     const spe_graph* g = t->g;
     const int32_t n = g->hg.n;
@@ -1165,7 +1181,8 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     const int64_t total = (int64_t)groups * n;
     // one resident wave per hardware slot (no second wave of late blocks), multiple of 8 (XCD split)
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_relax<L, INFL>, BLOCK, 0) != hipSuccess || per_cu < 1)
+    const void* kfn = (const void*)k_relax<L, INFL, OCC>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, BLOCK, 0) != hipSuccess || per_cu < 1)
         per_cu = 4;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus < 1) cus = 256;
     const int relax_grid = (grid_for((total + 7) / 8 * WAVE, BLOCK, per_cu * cus) + 7) & ~7;
@@ -1195,7 +1212,7 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
                      t->hmark[(it + 1) & 1], t->inflag[it & 1], t->inflag[(it + 1) & 1], t->counts + it};
             {
                 LaunchTimer lt(t, s, SPE_K_RELAX);
-                k_relax<L, INFL><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcv, g->dev, t->st, fl);
+                k_relax<L, INFL, OCC><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcv, g->dev, t->st, fl);
             }
             if (g->hp.nheavy > 0) {
                 LaunchTimer lt(t, s, SPE_K_HEAVY);
@@ -1229,7 +1246,11 @@ static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
     switch (t->lanes) {
         case 16: return deep ? relax_to_convergence_l<16, 8>(t, blocks, s) : relax_to_convergence_l<16, 4>(t, blocks, s);
         case 32: return deep ? relax_to_convergence_l<32, 8>(t, blocks, s) : relax_to_convergence_l<32, 4>(t, blocks, s);
-        default: return deep ? relax_to_convergence_l<64, 8>(t, blocks, s) : relax_to_convergence_l<64, 4>(t, blocks, s);
+        default:
+            if (t->occ == 7) return relax_to_convergence_l<64, 8, 7>(t, blocks, s);
+            if (t->occ == 8) return relax_to_convergence_l<64, 8, 8>(t, blocks, s);
+            if (t->infl == 6) return relax_to_convergence_l<64, 6>(t, blocks, s);
+            return deep ? relax_to_convergence_l<64, 8>(t, blocks, s) : relax_to_convergence_l<64, 4>(t, blocks, s);
     }
 }
 
