@@ -74,13 +74,17 @@ typedef struct spe_graph_desc {
 typedef struct spe_graph_info {
     int32_t n_vertices;
     int64_t n_edges;
-    int64_t n_relax_entries;        /* directed adjacency entries after merging parallel edges */
+    int64_t n_relax_entries;        /* directed adjacency entries after merging parallel edges
+                                     * (of the relaxation graph: pendants pruned) */
     int32_t directed;
     int32_t prefer_direct;
     int32_t complete;               /* _topology_isComplete */
     int32_t parallel_latency_differs; /* multigraph whose get_eid edge is not the lightest */
     int32_t weight_floor_ok;        /* every fl(d + w) > d is guaranteed (no absorbed edges) */
     int32_t device;
+    int32_t n_relax_vertices;       /* vertices the relaxation runs on: undirected pendant
+                                     * vertices (one neighbour) are one edge off their anchor
+                                     * and need no relaxation state */
 } spe_graph_info;
 
 typedef struct spe_table_opts {

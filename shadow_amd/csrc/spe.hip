@@ -66,8 +66,9 @@ int fail(int code, const std::string& msg) {
 constexpr double INF = __builtin_inf();
 
 struct DevGraph {
-    int32_t n;
+    int32_t n;               // relaxation vertices (the core when pendants are pruned)
     int32_t nrel;
+    int32_t n_full;          // all vertices (original ids)
     const int32_t* iptr;
     const int32_t* icol;
     const double* iw;
@@ -88,6 +89,18 @@ struct DevGraph {
     const double* self_w2;
     const double* self_a2;
     const int32_t* self_other;
+    // original <-> relaxation ids and the full in-CSR (pendant edges, DIRECT lookups)
+    const int32_t* core_id;      // [n_full] -1 = pruned pendant
+    const int32_t* corev;        // [n]
+    const int32_t* anchor_core;  // [n_full]
+    const int32_t* fiptr;
+    const double* fiw;
+    const double* fia;
+    const double* fiwrep;
+    const int32_t* dptr;         // DIRECT lookups: full out-CSR
+    const int32_t* dcol;
+    const double* dwrep;
+    const double* darep;
 };
 
 struct RowMode {
@@ -160,26 +173,39 @@ __device__ __forceinline__ double sub_get_d(double x, int32_t src) {
 
 template <int L>
 __global__ __launch_bounds__(BLOCK) void k_init_state(int32_t n, int32_t groups, const int32_t* __restrict__ srcv,
-                                                      const double* __restrict__ vfac, State st) {
+                                                      const double* __restrict__ vfac, DevGraph G, State st) {
     const size_t total = (size_t)groups * n * L;
     for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < total; i += (size_t)gridDim.x * BLOCK) {
         const int32_t j = (int32_t)(i % L);
         const size_t gv = i / L;
         const int32_t g = (int32_t)(gv / n);
         const int32_t v = (int32_t)(gv - (size_t)g * n);
-        const int32_t s = srcv[g * L + j];
-        if (v == s) {
+        const int32_t s = srcv[g * L + j];   // original id, -1 = padding lane
+        st.P[i] = -1;
+        st.D[i] = INF;
+        if (s < 0) continue;
+        const double fs = vfac[s];
+        const double r0 = has_attr(fs) ? 1.0 * fs : 1.0;  // (1 * (1 - p_src)), shd-topology.c:1428-1430
+        const int32_t sc = G.core_id[s];
+        if (v == sc) {
             st.D[i] = 0.0;
-            const double fs = vfac[s];
             Route rt;
-            rt.r = has_attr(fs) ? 1.0 * fs : 1.0;  // (1 * (1 - p_src)), shd-topology.c:1428-1430
+            rt.r = r0;
             rt.h = 0;
             rt.f = -1;
             st.RT[i] = rt;
-        } else {
-            st.D[i] = INF;
+        } else if (sc < 0 && v == G.anchor_core[s]) {
+            // pruned pendant source: Dijkstra's first step s -> anchor, fixed (every
+            // path leaves through it); P = -2 marks "parent is the pendant source"
+            const int32_t kx = G.fiptr[s];
+            st.D[i] = 0.0 + G.fiw[kx];
+            st.P[i] = -2;
+            Route rt;
+            rt.r = r0 * G.fia[kx];
+            rt.h = 1;
+            rt.f = G.corev[v];
+            st.RT[i] = rt;
         }
-        st.P[i] = -1;
     }
 }
 
@@ -203,8 +229,10 @@ __global__ __launch_bounds__(BLOCK) void k_seed(int32_t n, int32_t groups, const
                                                 DevGraph G, uint8_t* mark, uint8_t* hmark, uint8_t* in_flags) {
     const int32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= groups * L) return;
-    const int32_t s = srcv[i];
-    if (s < 0) return;
+    const int32_t s0 = srcv[i];
+    if (s0 < 0) return;
+    const int32_t sc = G.core_id[s0];
+    const int32_t s = sc >= 0 ? sc : G.anchor_core[s0];
     const int32_t g = i / L;
     for (int32_t k = G.optr[s]; k < G.optr[s + 1]; ++k) {
         (G.oheavy[k] ? hmark : mark)[(size_t)g * n + G.ocol[k]] = 1;
@@ -234,7 +262,7 @@ __device__ __forceinline__ void offer(Best& b, const DevGraph& G, const State& s
             b.need = true;
             b.bdu = du;
             b.bu = u;
-        } else {
+        } else if (b.bk >= 0) {   // (bk = -2: fixed seed from a pendant source, never tied)
             if (b.bu < 0) b.bu = G.icol[b.bk];
             if (b.bdu < 0.0) b.bdu = st.D[sidx<L>(g, n, b.bu, j)];
             better = (du < b.bdu) || (du == b.bdu && u < b.bu);
@@ -302,7 +330,7 @@ __device__ __forceinline__ bool finish_vertex(Best& b, const DevGraph& G, const 
         Route nr;
         nr.r = pu.r * G.ia[b.bk];
         nr.h = pu.h + 1;
-        nr.f = (b.bu == s) ? v : pu.f;
+        nr.f = (b.bu == s) ? G.corev[v] : pu.f;
         if (d_old == INF || b.bd != d_old || b.bk != p_old) {
             changed = true;
         } else {   // same parent, same distance: did the parent's route change?
@@ -351,7 +379,7 @@ __device__ __forceinline__ bool relax_item(int64_t e, int32_t n, int32_t j, int3
         d_old = st.D[rv];
         p_old = st.P[rv];
     }
-    const bool active = (e >= 0) && (s >= 0) && (s != v);
+    const bool active = (e >= 0) && (s != -1) && (s != v);
     Best b{d_old, p_old, -1, -1.0, false};
     // undirected graphs: the out-list IS the in-list; a single-chunk vertex keeps
     // what marking needs (neighbour, reverse entry, heavy bit) in registers
@@ -496,7 +524,7 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_partial(int32_t groups, int32_t
             ke = min(kb + WAVE, G.iptr[v + 1]);
             s = srcv[g * L + j];
         }
-        const bool active = item && (s >= 0) && (s != v);
+        const bool active = item && (s != -1) && (s != v);
         double ba = INF, bdu = INF;
         int32_t bu = -1, bk = -1;
         for (int32_t c0 = kb; c0 < ke; c0 += L) {
@@ -610,19 +638,19 @@ __device__ __forceinline__ void self_entry(const DevGraph& G, const RowMode& md,
 // DIRECT (s, t != s): first edge s->t in the out-CSR (merged, get_eid's edge).
 __device__ __forceinline__ bool direct_entry(const DevGraph& G, int32_t s, int32_t t, double& L_, double& R,
                                              int32_t& N, int32_t& H) {
-    int32_t lo = G.optr[s], hi = G.optr[s + 1];
+    int32_t lo = G.dptr[s], hi = G.dptr[s + 1];
     while (lo < hi) {
         const int32_t mid = lo + ((hi - lo) >> 1);
-        if (G.ocol[mid] < t) lo = mid + 1;
+        if (G.dcol[mid] < t) lo = mid + 1;
         else hi = mid;
     }
-    if (lo >= G.optr[s + 1] || G.ocol[lo] != t) return false;
+    if (lo >= G.dptr[s + 1] || G.dcol[lo] != t) return false;
     const double fs = G.vfac[s], ft = G.vfac[t];
     double r = 1.0;
     if (has_attr(fs)) r *= fs;
     if (has_attr(ft)) r *= ft;
-    r *= G.oarep[lo];
-    L_ = 0.0 + G.owrep[lo];
+    r *= G.darep[lo];
+    L_ = 0.0 + G.dwrep[lo];
     R = r;
     N = t;
     H = 1;
@@ -651,10 +679,23 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
             if (t == s) {
                 self_entry(G, md, s, Lt, R, N, H);
             } else {
-                const size_t rt = sidx<L>(g, n, t, j);
-                const double d = st.D[rt];
-                if (d < INF) {
-                    const Route rr = st.RT[rt];
+                // a pruned pendant target is one edge past its anchor: Dijkstra's
+                // d[t] = d[c] + w, parent c (its only candidate)
+                const int32_t tc = G.core_id[t];
+                const int32_t c = tc >= 0 ? tc : G.anchor_core[t];
+                const int32_t kt = tc >= 0 ? -1 : G.fiptr[t];
+                const size_t rt = sidx<L>(g, n, c, j);
+                const double dc = st.D[rt];
+                if (dc < INF) {
+                    const Route rc = st.RT[rt];
+                    double d = dc;
+                    Route rr = rc;
+                    if (kt >= 0) {
+                        d = dc + G.fiw[kt];
+                        rr.r = rc.r * G.fia[kt];
+                        rr.h = rc.h + 1;
+                        rr.f = (rc.h == 0) ? t : rc.f;   // c is the source itself
+                    }
                     const double ft = G.vfac[t];
                     const bool fast = (!has_attr(ft) || ft == 1.0) && !md.multi_rep;
                     if (fast) {
@@ -662,18 +703,34 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
                         R = rr.r;
                     } else {
                         // path-order re-fold, shd-topology.c:1413-1493 (rare: vertex loss on
-                        // the target, or multigraph get_eid latencies)
+                        // the target, or multigraph get_eid latencies).  Edge i of the path
+                        // (1 = leaves the source) is found by walking back from t.
                         const double fs = G.vfac[s];
                         double l = 0.0, r = 1.0;
                         if (has_attr(fs)) r *= fs;
                         if (has_attr(ft)) r *= ft;
                         const int32_t h = rr.h;
                         for (int32_t i = 1; i <= h; ++i) {
-                            int32_t x = t;
-                            for (int32_t q = 0; q < h - i; ++q) x = G.icol[st.P[sidx<L>(g, n, x, j)]];
-                            const int32_t k = st.P[sidx<L>(g, n, x, j)];
-                            l += G.iwrep[k];
-                            r *= G.ia[k];
+                            int32_t back = h - i;   // edges to step over from the end
+                            double ew, ea;
+                            if (kt >= 0 && back == 0) {
+                                ew = G.fiwrep[kt];
+                                ea = G.fia[kt];
+                            } else {
+                                int32_t x = c;
+                                if (kt >= 0) back -= 1;
+                                for (int32_t q = 0; q < back; ++q) x = G.icol[st.P[sidx<L>(g, n, x, j)]];
+                                const int32_t k = st.P[sidx<L>(g, n, x, j)];
+                                if (k >= 0) {
+                                    ew = G.iwrep[k];
+                                    ea = G.ia[k];
+                                } else {   // -2: the pendant source's edge into its anchor
+                                    ew = G.fiwrep[G.fiptr[s]];
+                                    ea = G.fia[G.fiptr[s]];
+                                }
+                            }
+                            l += ew;
+                            r *= ea;
                         }
                         Lt = l;
                         R = r;
@@ -730,17 +787,17 @@ __global__ __launch_bounds__(BLOCK) void k_direct_overlay(int32_t groups, int32_
     const int32_t s = srcv[i];
     if (s < 0) return;
     const double fs = G.vfac[s];
-    for (int32_t k = G.optr[s]; k < G.optr[s + 1]; ++k) {
-        const int32_t t = G.ocol[k];
+    for (int32_t k = G.dptr[s]; k < G.dptr[s + 1]; ++k) {
+        const int32_t t = G.dcol[k];
         const int32_t j = vertex_slot[t];
         if (j < 0) continue;
         const double ft = G.vfac[t];
         double r = 1.0;
         if (has_attr(fs)) r *= fs;
         if (has_attr(ft)) r *= ft;
-        r *= G.oarep[k];
+        r *= G.darep[k];
         const size_t o = tidx(sb0 + g, tb.A, j, lane);
-        tb.lat[o] = 0.0 + G.owrep[k];
+        tb.lat[o] = 0.0 + G.dwrep[k];
         tb.rel[o] = r;
         tb.next[o] = t;
         tb.hops[o] = 1;
@@ -814,8 +871,9 @@ struct spe_table {
     Partial pp{};
     int32_t* counts = nullptr;   // per round: 1 if any vertex changed
     int32_t max_iters = 0;
-    int32_t* d_srcv = nullptr;
-    int32_t* h_srcv = nullptr;
+    int32_t* d_srcv = nullptr;     // batch sources, original ids (-1 = padding)
+    int32_t* d_srcc = nullptr;     // relaxation ids (-2 = pruned pendant source, -1 = padding)
+    int32_t* h_srcv = nullptr;     // pinned staging for both
     int32_t* h_counts = nullptr;
     unsigned long long* d_min = nullptr;
     hipStream_t stream = nullptr;
@@ -906,9 +964,11 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
         return r;
     }
     g->device = device;
+    spe::prune_pendants(&g->hg, getenv("SPE_NO_PRUNE") == nullptr);
     const spe::HostGraph& h = g->hg;
     DevGraph& d = g->dev;
-    d.n = h.n;
+    d.n = h.nc;
+    d.n_full = h.n;
     d.nrel = (int32_t)h.icol.size();
     d.ablate = getenv("SPE_ABLATE") ? atoi(getenv("SPE_ABLATE")) : 0;
 #define UPBASE d
@@ -945,10 +1005,33 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
     UP(self_w2, h.self_w2);
     UP(self_a2, h.self_a2);
     UP(self_other, h.self_other);
-    {   // heavy-vertex segment plan (in-degree > 64)
-        std::vector<uint8_t> heavy(h.n, 0);
+    UP(core_id, h.core_id);
+    UP(corev, h.corev);
+    UP(anchor_core, h.anchor_core);
+    UP(fiptr, h.fiptr);
+    UP(fiw, h.fiw);
+    UP(fia, h.fia);
+    UP(fiwrep, h.fiwrep);
+    if (h.directed) {
+        d.dptr = d.optr;
+        d.dcol = d.ocol;
+        d.dwrep = d.owrep;
+        d.darep = d.oarep;
+    } else if (!h.pruned) {
+        d.dptr = d.iptr;
+        d.dcol = d.icol;
+        d.dwrep = d.iwrep;
+        d.darep = d.ia;
+    } else {
+        d.dptr = d.fiptr;
+        UP(dcol, h.ficol);
+        d.dwrep = d.fiwrep;
+        d.darep = d.fia;
+    }
+    {   // heavy-vertex segment plan (in-degree > 64), over the relaxation graph
+        std::vector<uint8_t> heavy(h.nc, 0);
         std::vector<int32_t> seg_vertex, seg_begin, heavy_vertex, heavy_seg0;
-        for (int32_t v = 0; v < h.n; ++v) {
+        for (int32_t v = 0; v < h.nc; ++v) {
             const int32_t k0 = h.iptr[v], k1 = h.iptr[v + 1];
             if (k1 - k0 <= WAVE) continue;
             heavy[v] = 1;
@@ -994,6 +1077,7 @@ int spe_graph_info_get(const spe_graph* g, spe_graph_info* out) {
     out->n_vertices = g->hg.n;
     out->n_edges = g->hg.m;
     out->n_relax_entries = (int64_t)g->hg.icol.size();
+    out->n_relax_vertices = g->hg.nc;
     out->directed = g->hg.directed;
     out->prefer_direct = g->hg.prefer_direct;
     out->complete = g->hg.complete;
@@ -1015,11 +1099,12 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     if (!g || !attached || n_attached <= 0 || !out) return fail(SPE_EINVAL, "spe_table_create: bad arguments");
     *out = nullptr;
     HIP_TRY(hipSetDevice(g->device));
-    const int32_t n = g->hg.n;
-    std::vector<int32_t> vslot(n, -1);
+    const int32_t n_full = g->hg.n;
+    const int32_t n = g->hg.nc;   // relaxation state is over the core
+    std::vector<int32_t> vslot(n_full, -1);
     for (int32_t i = 0; i < n_attached; ++i) {
         const int32_t v = attached[i];
-        if (v < 0 || v >= n) return fail(SPE_EINVAL, "attached vertex out of range");
+        if (v < 0 || v >= n_full) return fail(SPE_EINVAL, "attached vertex out of range");
         if (vslot[v] >= 0) return fail(SPE_EINVAL, "attached vertices must be unique");
         vslot[v] = i;
     }
@@ -1123,9 +1208,10 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         TRY(dev_alloc(t->allocs, &t->counts, (size_t)t->max_iters + 2));
     }
     TRY(dev_alloc(t->allocs, &t->d_srcv, G * WAVE));
+    TRY(dev_alloc(t->allocs, &t->d_srcc, G * WAVE));
     TRY(dev_alloc(t->allocs, &t->d_min, 1));
 #undef TRY
-    HIP_TRY(hipHostMalloc((void**)&t->h_srcv, G * WAVE * sizeof(int32_t), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&t->h_srcv, 2 * G * WAVE * sizeof(int32_t), hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void**)&t->h_counts, 64 * sizeof(int32_t), hipHostMallocDefault));
     HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
     *out = t;
@@ -1175,7 +1261,7 @@ extern "C++" {
 template <int L, int INFL, int OCC = 1>
 static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     const spe_graph* g = t->g;
-    const int32_t n = g->hg.n;
+    const int32_t n = g->hg.nc;
     const int32_t nrel = (int32_t)g->hg.icol.size();
     const int32_t groups = blocks * (WAVE / L);    // lane groups
     const int64_t total = (int64_t)groups * n;
@@ -1194,7 +1280,8 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     }
     {
         LaunchTimer lt(t, s, SPE_K_INIT);
-        k_init_state<L><<<grid_for(total * L, BLOCK, 8192), BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev.vfac, t->st);
+        k_init_state<L><<<grid_for(total * L, BLOCK, 8192), BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev.vfac, g->dev,
+                                                                            t->st);
     }
     {
         LaunchTimer lt(t, s, SPE_K_SEED);
@@ -1212,15 +1299,15 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
                      t->hmark[(it + 1) & 1], t->inflag[it & 1], t->inflag[(it + 1) & 1], t->counts + it};
             {
                 LaunchTimer lt(t, s, SPE_K_RELAX);
-                k_relax<L, INFL, OCC><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcv, g->dev, t->st, fl);
+                k_relax<L, INFL, OCC><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev, t->st, fl);
             }
             if (g->hp.nheavy > 0) {
                 LaunchTimer lt(t, s, SPE_K_HEAVY);
                 const int64_t pw = ((int64_t)groups * g->hp.nseg + subs_per_wave - 1) / subs_per_wave;
                 const int64_t cw = ((int64_t)groups * g->hp.nheavy + subs_per_wave - 1) / subs_per_wave;
-                k_heavy_partial<L><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcv, g->dev,
+                k_heavy_partial<L><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcc, g->dev,
                                                                                       t->st, g->hp, t->pp, fl);
-                k_heavy_combine<L><<<grid_for(cw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcv, g->dev,
+                k_heavy_combine<L><<<grid_for(cw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcc, g->dev,
                                                                                       t->st, g->hp, t->pp, fl);
             }
         }
@@ -1256,7 +1343,7 @@ static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
 
 static void launch_rows_sssp(spe_table* t, int grid, int32_t blocks, int32_t sb0, hipStream_t s) {
     const spe_graph* g = t->g;
-#define ROWS(LL) k_rows_sssp<LL><<<grid, BLOCK, 0, s>>>(g->hg.n, blocks, sb0, t->d_srcv, t->d_slot_vertex, g->dev, \
+#define ROWS(LL) k_rows_sssp<LL><<<grid, BLOCK, 0, s>>>(g->hg.nc, blocks, sb0, t->d_srcv, t->d_slot_vertex, g->dev, \
                                                          t->md, t->st, t->tb)
     switch (t->lanes) {
         case 16: ROWS(16); break;
@@ -1287,9 +1374,13 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
         for (int32_t gi = 0; gi < groups; ++gi)
             for (int32_t l = 0; l < WAVE; ++l) {
                 const int32_t slot = (b + gi) * WAVE + l;
-                t->h_srcv[gi * WAVE + l] = slot < t->A ? t->attached[slot] : -1;
+                const int32_t v = slot < t->A ? t->attached[slot] : -1;
+                t->h_srcv[gi * WAVE + l] = v;
+                t->h_srcv[(groups + gi) * WAVE + l] = v < 0 ? -1 : (g->hg.core_id[v] >= 0 ? g->hg.core_id[v] : -2);
             }
         HIP_TRY(hipMemcpyAsync(t->d_srcv, t->h_srcv, sizeof(int32_t) * groups * WAVE, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(t->d_srcc, t->h_srcv + groups * WAVE, sizeof(int32_t) * groups * WAVE,
+                               hipMemcpyHostToDevice, s));
         const int32_t sb0 = b - t->blk0;
         const int64_t items = (int64_t)groups * t->A;
         const int row_grid = grid_for(items * WAVE, BLOCK, 8192);

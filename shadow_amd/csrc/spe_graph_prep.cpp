@@ -216,4 +216,68 @@ int prepare_graph(const spe_graph_desc* d, HostGraph* hg, std::string* err) {
     return SPE_OK;
 }
 
+void prune_pendants(HostGraph* hg, bool enable) {
+    const int32_t n = hg->n;
+    hg->fiptr = hg->iptr;
+    hg->ficol = hg->icol;
+    hg->fiw = hg->iw;
+    hg->fia = hg->ia;
+    hg->fiwrep = hg->iwrep;
+    hg->core_id.resize(n);
+    hg->anchor_core.assign(n, -1);
+    std::vector<uint8_t> pend(n, 0);
+    hg->pruned = false;
+    if (enable && !hg->directed && n > 2) {
+        for (int32_t v = 0; v < n; ++v) {
+            if (hg->iptr[v + 1] - hg->iptr[v] != 1) continue;
+            const int32_t c = hg->icol[hg->iptr[v]];
+            if (hg->iptr[c + 1] - hg->iptr[c] >= 2) pend[v] = 1;   // anchor is not itself pendant
+        }
+        for (int32_t v = 0; v < n; ++v) hg->pruned |= pend[v] != 0;
+    }
+    if (!hg->pruned) {
+        hg->nc = n;
+        hg->corev.resize(n);
+        for (int32_t v = 0; v < n; ++v) hg->core_id[v] = hg->corev[v] = v;
+        return;
+    }
+    hg->corev.clear();
+    for (int32_t v = 0; v < n; ++v) {
+        hg->core_id[v] = pend[v] ? -1 : (int32_t)hg->corev.size();
+        if (!pend[v]) hg->corev.push_back(v);
+    }
+    hg->nc = (int32_t)hg->corev.size();
+    for (int32_t v = 0; v < n; ++v)
+        if (pend[v]) hg->anchor_core[v] = hg->core_id[hg->icol[hg->iptr[v]]];
+    // core in-CSR: core vertices, core neighbours only (relaxation ids; the
+    // neighbour order is unchanged, so lists stay sorted by original = core id)
+    std::vector<int32_t> iptr(1, 0), icol;
+    std::vector<double> iw, ia, iwrep;
+    for (int32_t c = 0; c < hg->nc; ++c) {
+        const int32_t v = hg->corev[c];
+        for (int32_t k = hg->fiptr[v]; k < hg->fiptr[v + 1]; ++k) {
+            const int32_t u = hg->ficol[k];
+            if (pend[u]) continue;
+            icol.push_back(hg->core_id[u]);
+            iw.push_back(hg->fiw[k]);
+            ia.push_back(hg->fia[k]);
+            iwrep.push_back(hg->fiwrep[k]);
+        }
+        iptr.push_back((int32_t)icol.size());
+    }
+    hg->iptr.swap(iptr);
+    hg->icol.swap(icol);
+    hg->iw.swap(iw);
+    hg->ia.swap(ia);
+    hg->iwrep.swap(iwrep);
+    hg->orev.resize(hg->icol.size());
+    for (int32_t x = 0; x < hg->nc; ++x)
+        for (int32_t k = hg->iptr[x]; k < hg->iptr[x + 1]; ++k) {
+            const int32_t y = hg->icol[k];
+            const int32_t* b = hg->icol.data() + hg->iptr[y];
+            const int32_t* e = hg->icol.data() + hg->iptr[y + 1];
+            hg->orev[k] = (int32_t)(std::lower_bound(b, e, x) - hg->icol.data());
+        }
+}
+
 }  // namespace spe

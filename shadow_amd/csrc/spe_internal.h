@@ -19,7 +19,20 @@ struct HostGraph {
     bool multi_rep = false;        // some merged pair's get_eid latency != relaxation latency
     bool weight_floor_ok = true;
 
-    // relaxation in-CSR: entries u -> v grouped by v, sorted by u
+    // Pendant pruning (undirected graphs): a vertex whose only non-loop neighbour
+    // is its anchor c (itself not pendant) never lies inside a shortest path, so
+    // the relaxation runs on the remaining "core" and pendant rows/targets are
+    // one edge away from their anchor.  nc = relaxation vertex count.
+    bool pruned = false;
+    int32_t nc = 0;
+    std::vector<int32_t> core_id;      // [n] relaxation id, -1 for a pruned pendant
+    std::vector<int32_t> corev;        // [nc] original id
+    std::vector<int32_t> anchor_core;  // [n] relaxation id of a pendant's anchor, -1 otherwise
+    // full in-CSR (original ids): DIRECT lookups and the pendant edges
+    std::vector<int32_t> fiptr, ficol;
+    std::vector<double> fiw, fia, fiwrep;
+
+    // relaxation in-CSR (relaxation ids): entries u -> v grouped by v, sorted by u
     std::vector<int32_t> iptr, icol;
     std::vector<double> iw;        // min latency over parallel u->v edges (what Dijkstra relaxes)
     std::vector<double> ia;        // 1 - loss of the get_eid edge
@@ -37,5 +50,8 @@ struct HostGraph {
 };
 
 int prepare_graph(const spe_graph_desc* d, HostGraph* hg, std::string* err);
+// Restrict the relaxation CSR to the core (no-op for directed graphs or when
+// `enable` is false); keeps the full CSR in hg->f*.
+void prune_pendants(HostGraph* hg, bool enable);
 
 }  // namespace spe

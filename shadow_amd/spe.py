@@ -37,7 +37,8 @@ class GraphDesc(C.Structure):
 class GraphInfo(C.Structure):
     _fields_ = [("n_vertices", C.c_int32), ("n_edges", C.c_int64), ("n_relax_entries", C.c_int64),
                 ("directed", C.c_int32), ("prefer_direct", C.c_int32), ("complete", C.c_int32),
-                ("parallel_latency_differs", C.c_int32), ("weight_floor_ok", C.c_int32), ("device", C.c_int32)]
+                ("parallel_latency_differs", C.c_int32), ("weight_floor_ok", C.c_int32), ("device", C.c_int32),
+                ("n_relax_vertices", C.c_int32)]
 
 
 class TableOpts(C.Structure):

@@ -1,0 +1,89 @@
+"""GPU parity of pendant pruning: undirected vertices with a single neighbour
+(C4's stubs) get no relaxation state; their rows start one edge into the core
+and their entries are one edge past their anchor.  Results must be identical
+to the oracle and to the unpruned engine (SPE_NO_PRUNE)."""
+import os
+
+import numpy as np
+import pytest
+
+from shadow_amd import graphs
+from oracle import Oracle
+from test_gpu_parity import compare
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def spe():
+    from shadow_amd import spe as m
+    assert m.device_count() > 0, "no GPU visible"
+    return m
+
+
+def build(spe, top, A, prune=True, **kw):
+    if prune:
+        os.environ.pop("SPE_NO_PRUNE", None)
+    else:
+        os.environ["SPE_NO_PRUNE"] = "1"
+    try:
+        g = spe.Graph(top)
+    finally:
+        os.environ.pop("SPE_NO_PRUNE", None)
+    t = spe.PathTable(g, A, **kw)
+    t.build()
+    return t.download(), g.info()
+
+
+def tiered_small(seed, vloss=False):
+    top = graphs.gen_tiered(n_core=300, n_stub=700, n_attached=400, seed=seed)
+    if vloss:
+        rng = np.random.default_rng(seed)
+        top.vloss = np.where(rng.random(top.n) < 0.3, rng.uniform(0, 0.02, top.n), 0.0)
+    return top
+
+
+@pytest.mark.parametrize("vloss", [False, True])
+def test_tiered_pendant_rows(spe, vloss):
+    top = tiered_small(11, vloss)
+    # attached: the 400 stubs with self-loops plus 50 core vertices (core has no loops)
+    A = np.concatenate([np.arange(300, 700), np.arange(0, 300, 6)]).astype(np.int32)
+    ora = Oracle(top).rows(A, A)
+    out, info = build(spe, top, A)
+    assert info["n_relax_vertices"] == 300, info
+    compare(out, ora, label=f"tiered vloss={vloss}")
+    out2, info2 = build(spe, top, A, prune=False)
+    assert info2["n_relax_vertices"] == top.n
+    for k in ("lat", "rel", "next", "hops", "ok"):
+        np.testing.assert_array_equal(out[k], out2[k], err_msg=k)
+
+
+def test_tree_like_pendants_self_rule(spe):
+    """Random spanning tree + few chords: many leaves (pendant sources, targets and
+    pairs sharing an anchor), vertex loss on every vertex, both self modes."""
+    top = graphs.gen_random_small(600, 40, 51, vloss_nonzero=True)
+    A = np.arange(top.n, dtype=np.int32)
+    for self_mode in (0, 1):
+        ora = Oracle(top).rows(A, A, self_mode=self_mode)
+        out, info = build(spe, top, A, self_mode=self_mode)
+        assert info["n_relax_vertices"] < top.n
+        compare(out, ora, label=f"tree self_mode={self_mode}")
+
+
+def test_pendant_multigraph_edges(spe):
+    """Parallel edges between a pendant and its anchor: still one neighbour (pruned);
+    reported latency follows get_eid's edge (slow path re-fold)."""
+    top = graphs.gen_random_small(300, 30, 52, multi=200)
+    A = np.arange(top.n, dtype=np.int32)
+    ora = Oracle(top).rows(A, A, tie_mode=1)
+    out, info = build(spe, top, A)
+    assert info["n_relax_vertices"] < top.n
+    compare(out, ora, label="pendant multigraph")
+
+
+def test_directed_graph_not_pruned(spe):
+    top = graphs.gen_random_small(300, 200, 53, directed=True)
+    A = np.arange(top.n, dtype=np.int32)
+    out, info = build(spe, top, A)
+    assert info["n_relax_vertices"] == top.n
+    compare(out, Oracle(top).rows(A, A), label="directed")
