@@ -143,6 +143,78 @@ def bench_lookup(args):
     print(json.dumps(line), flush=True)
 
 
+def bench_full_table(args, rank, world, local, dist):
+    """Whole path-table precompute (BASELINE north star: C4 on 8 GPUs in < 10 s).
+    Rank r owns the contiguous source-block range r of `shares` (= world, or more to
+    emulate one rank of a larger job on fewer GPUs); with --gather and world > 1 the
+    latency and reliability fields are then all-gathered over RCCL into a full
+    replicated table on every GPU (one contiguous SB64 span per rank)."""
+    import torch
+    from shadow_amd import spe
+    top, att, desc = workload(args.config)
+    g = spe.Graph(top, device=local)
+    info = g.info()
+    A = int(att.shape[0])
+    nblk = (A + 63) // 64
+    shares = max(world, args.shares)
+    share = rank if shares == world else args.share_index
+    cb = (nblk + shares - 1) // shares
+    b0, b1 = min(nblk, share * cb), min(nblk, (share + 1) * cb)
+    elems = cb * A * 64
+    dev = torch.device("cuda", local)
+    bufs = [torch.empty(elems, dtype=torch.float64, device=dev), torch.empty(elems, dtype=torch.float64, device=dev),
+            torch.empty(elems, dtype=torch.int32, device=dev), torch.empty(elems, dtype=torch.int16, device=dev)]
+    t = None
+    if b1 > b0:   # (a rank past the last block owns nothing but still joins the gather)
+        t = spe.PathTable(g, att, blocks=(b0, b1), ext=[b.data_ptr() for b in bufs], groups=args.groups)
+    if t is not None:   # warm-up: one batch (kernel code objects, first-touch of the state)
+        t.build_blocks(b0, min(b1, b0 + 1))
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    if t is not None:
+        t.build()
+    torch.cuda.synchronize(dev)
+    t_build = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    t_all = time.perf_counter() - t0
+    gather = None
+    if args.gather and dist is not None:
+        full_lat = torch.empty(world * elems, dtype=torch.float64, device=dev)
+        full_rel = torch.empty(world * elems, dtype=torch.float64, device=dev)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        tg = time.perf_counter()
+        dist.all_gather_into_tensor(full_lat, bufs[0])
+        dist.all_gather_into_tensor(full_rel, bufs[1])
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t_gather = time.perf_counter() - tg
+        t_all = time.perf_counter() - t0
+        gather = {"bytes_per_gpu_received": int(2 * (world - 1) * elems * 8), "seconds": round(t_gather, 3),
+                  "GBps_per_gpu": round(2 * (world - 1) * elems * 8 / t_gather / 1e9, 1)}
+    x = torch.tensor([t_build, t_all], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+    t_build, t_all = float(x[0]), float(x[1])
+    if rank == 0:
+        srcs = min(A, b1 * 64) - b0 * 64 if shares != world else A
+        line = {"metric": "full path-table precompute time (north star: C4 on 8 GPUs < 10 s)",
+                "value": round(t_all, 3), "unit": "s", "higher_is_better": False, "n_gpus": world,
+                "dtype": "f64", "data": "synthetic",
+                "config": {"workload": desc, "n": info["n_vertices"], "relax_vertices": info["n_relax_vertices"],
+                           "m_dir_relax": info["n_relax_entries"], "attached": A,
+                           "shares": shares, "share_built": [b0, b1] if shares != world else "all",
+                           "table_bytes_per_gpu": int(elems * 22)},
+                "build_s": round(t_build, 3), "sources_per_s_per_gpu": round(srcs / max(t_build, 1e-9) / (1 if shares != world else world), 1),
+                "gather": gather,
+                "note": ("emulated: this run built ONE share of a %d-way split (weak-scaling equivalent of one rank); "
+                         "no all-gather measured" % shares) if shares != world else None}
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -156,6 +228,10 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--queries", type=int, default=100_000_000, help="c5: lookups per step")
     ap.add_argument("--pmc-json", default=None, help="per-dispatch HBM bytes from tools/pmc_to_json.py")
+    ap.add_argument("--full-table", action="store_true", help="time one whole path-table precompute")
+    ap.add_argument("--gather", action="store_true", help="--full-table: RCCL all-gather of latency/reliability")
+    ap.add_argument("--shares", type=int, default=1, help="--full-table: split into this many source shares")
+    ap.add_argument("--share-index", type=int, default=0, help="--full-table: the share this run builds")
     args = ap.parse_args()
     if args.config == "c5":
         return bench_lookup(args)
@@ -169,6 +245,12 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    if args.full_table:
+        bench_full_table(args, rank, world, local, dist)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     from shadow_amd import spe
     top, att, desc = workload(args.config)

@@ -87,3 +87,19 @@ def test_directed_graph_not_pruned(spe):
     out, info = build(spe, top, A)
     assert info["n_relax_vertices"] == top.n
     compare(out, Oracle(top).rows(A, A), label="directed")
+
+
+def test_c4_sample_rows_full_size(spe):
+    """C4 (200k vertices, 180k stubs, A = 100k stubs) at full size: two source
+    blocks, sampled rows bit-exact against the oracle; every entry routable."""
+    top = graphs.gen_tiered()
+    A = graphs.tiered_attached(top)
+    g = spe.Graph(top)
+    assert g.info()["n_relax_vertices"] == 20000
+    t = spe.PathTable(g, A, blocks=(7, 9))
+    t.build()
+    rows = t.download(448, 576)
+    assert rows["ok"].all()
+    sample = np.arange(448, 576, 17)
+    ora = Oracle(top).rows(A[sample], A)
+    compare({k: v[sample - 448] for k, v in rows.items()}, ora, label="C4")
