@@ -102,6 +102,13 @@ typedef struct spe_table_opts {
     int32_t ext_filled;             /* 1: the external storage already holds the rows (e.g. an
                                      * RCCL all-gather of other tables' blocks): usable for
                                      * get / download / lookup without spe_table_build */
+    const int32_t* owner_rank;      /* host array [n_attached] or NULL.  Non-NULL: compat mode that
+                                     * replays the reference's first-writer-wins path cache
+                                     * (shd-topology.c:1292-1321, 1952-2034) as if every source
+                                     * slot had run its Dijkstra in increasing owner_rank order:
+                                     * entry (s,t) then answers the path stored for {s,t} in
+                                     * either direction.  Needs a table owning all blocks; applied
+                                     * by spe_table_build (not spe_table_build_blocks). */
     int32_t lanes_per_group;        /* sources sharing one relaxation frontier: 16, 32 or 64;
                                      * 0 = default (64: measured fastest on C3) */
 } spe_table_opts;

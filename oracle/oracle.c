@@ -560,7 +560,7 @@ static int64_t build_path(const orc_graph* g, const orc_rowws* r, int32_t tie_mo
 
 static void row_one(const orc_graph* g, const orc_opts* opts, orc_rowws* r, int32_t s,
                     const int32_t* targets, int32_t A, double* lat, double* rel, int32_t* next,
-                    int32_t* hops, uint8_t* kind, int64_t* ties, double* dj_seconds) {
+                    int32_t* hops, uint8_t* kind, int32_t* prev, int64_t* ties, double* dj_seconds) {
     int32_t j, v;
     int need_sssp = 0;
     int tie_mode = opts ? opts->tie_mode : 0;
@@ -594,7 +594,7 @@ static void row_one(const orc_graph* g, const orc_opts* opts, orc_rowws* r, int3
         int32_t t = targets[j];
         uint8_t k;
         double L = -1.0, R = -1.0;
-        int32_t N = -1, H = 0;
+        int32_t N = -1, H = 0, PV = s;   /* PV: vertex before the target on the path */
         if (complete || (prefer && orc_get_eid(g, s, t) >= 0)) {
             k = rule_direct(g, s, t, &L, &R, &N, &H);
         } else if (t == s) {
@@ -603,16 +603,19 @@ static void row_one(const orc_graph* g, const orc_opts* opts, orc_rowws* r, int3
                 k = rule_path(g, s, r->path, 1, &L, &R, &N, &H);
             } else {
                 k = rule_self(g, s, &L, &R, &N, &H);
+                PV = N;
             }
         } else if (r->dist[t] < 0) {
             k = ORC_FAIL;
         } else {
             int64_t np = build_path(g, r, tie_mode, t);
             k = rule_path(g, s, r->path, np, &L, &R, &N, &H);
+            if (np >= 2) PV = r->path[np - 2];
         }
         if (k == ORC_FAIL) {
-            L = -1.0; R = -1.0; N = -1; H = 0;
+            L = -1.0; R = -1.0; N = -1; H = 0; PV = -1;
         }
+        if (prev) prev[j] = PV;
         lat[j] = L;
         rel[j] = R;
         next[j] = N;
@@ -621,10 +624,10 @@ static void row_one(const orc_graph* g, const orc_opts* opts, orc_rowws* r, int3
     }
 }
 
-int32_t orc_rows(const orc_graph* g, const orc_opts* opts, const int32_t* sources, int32_t nsrc,
-                 const int32_t* targets, int32_t A, double* lat, double* rel, int32_t* next,
-                 int32_t* hops, uint8_t* kind, int64_t* double_ties, double* dijkstra_seconds,
-                 int32_t nthreads) {
+int32_t orc_rows2(const orc_graph* g, const orc_opts* opts, const int32_t* sources, int32_t nsrc,
+                  const int32_t* targets, int32_t A, double* lat, double* rel, int32_t* next,
+                  int32_t* hops, uint8_t* kind, int32_t* prev, int64_t* double_ties,
+                  double* dijkstra_seconds, int32_t nthreads) {
     int64_t ties = 0;
     double djs = 0.0;
     int32_t i;
@@ -634,7 +637,8 @@ int32_t orc_rows(const orc_graph* g, const orc_opts* opts, const int32_t* source
         for (i = 0; i < nsrc; i++) {
             size_t off = (size_t)i * (size_t)A;
             row_one(g, opts, &r, sources[i], targets, A, lat + off, rel + off, next + off, hops + off,
-                    kind + off, double_ties ? &ties : NULL, dijkstra_seconds ? &djs : NULL);
+                    kind + off, prev ? prev + off : NULL, double_ties ? &ties : NULL,
+                    dijkstra_seconds ? &djs : NULL);
         }
         rowws_free(&r);
     } else {
@@ -647,7 +651,7 @@ int32_t orc_rows(const orc_graph* g, const orc_opts* opts, const int32_t* source
             for (i = 0; i < nsrc; i++) {
                 size_t off = (size_t)i * (size_t)A;
                 row_one(g, opts, &r, sources[i], targets, A, lat + off, rel + off, next + off,
-                        hops + off, kind + off, double_ties ? &ties : NULL,
+                        hops + off, kind + off, prev ? prev + off : NULL, double_ties ? &ties : NULL,
                         dijkstra_seconds ? &djs : NULL);
             }
             rowws_free(&r);
@@ -659,4 +663,12 @@ int32_t orc_rows(const orc_graph* g, const orc_opts* opts, const int32_t* source
     if (double_ties) *double_ties += ties;
     if (dijkstra_seconds) *dijkstra_seconds += djs;
     return 0;
+}
+
+int32_t orc_rows(const orc_graph* g, const orc_opts* opts, const int32_t* sources, int32_t nsrc,
+                 const int32_t* targets, int32_t A, double* lat, double* rel, int32_t* next,
+                 int32_t* hops, uint8_t* kind, int64_t* double_ties, double* dijkstra_seconds,
+                 int32_t nthreads) {
+    return orc_rows2(g, opts, sources, nsrc, targets, A, lat, rel, next, hops, kind, NULL, double_ties,
+                     dijkstra_seconds, nthreads);
 }

@@ -68,6 +68,12 @@ int32_t orc_rows(const orc_graph* g, const orc_opts* opts,
                  const int32_t* sources, int32_t nsrc, const int32_t* targets, int32_t A,
                  double* lat, double* rel, int32_t* next, int32_t* hops, uint8_t* kind,
                  int64_t* double_ties, double* dijkstra_seconds, int32_t nthreads);
+/* orc_rows plus prev[] (optional): the vertex before the target on each path
+ * (the source for one-edge and [s] paths, the other endpoint for SELF, -1 on failure). */
+int32_t orc_rows2(const orc_graph* g, const orc_opts* opts,
+                  const int32_t* sources, int32_t nsrc, const int32_t* targets, int32_t A,
+                  double* lat, double* rel, int32_t* next, int32_t* hops, uint8_t* kind, int32_t* prev,
+                  int64_t* double_ties, double* dijkstra_seconds, int32_t nthreads);
 
 #ifdef __cplusplus
 }

@@ -41,6 +41,9 @@ def lib():
         L.orc_dijkstra.restype = C.c_int32
         L.orc_rows.argtypes = [P, P, P, C.c_int32, P, C.c_int32, P, P, P, P, P, P, P, C.c_int32]
         L.orc_rows.restype = C.c_int32
+        L.orc_rows2.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32] + [C.c_void_p] * 8 \
+            + [C.c_int32]
+        L.orc_rows2.restype = C.c_int32
         _lib = L
     return _lib
 
@@ -94,7 +97,7 @@ class Oracle:
         return dist, peid, rank
 
     def rows(self, sources, targets, self_mode: int = 0, tie_mode: int = 0, nthreads: int = 1, force_sssp: bool = False,
-             want_ties: bool = False, want_dijkstra_time: bool = False):
+             want_ties: bool = False, want_dijkstra_time: bool = False, want_prev: bool = False):
         src = np.ascontiguousarray(sources, dtype=np.int32)
         tg = np.ascontiguousarray(targets, dtype=np.int32)
         ns, A = src.shape[0], tg.shape[0]
@@ -105,16 +108,62 @@ class Oracle:
             "hops": np.empty((ns, A), np.int32),
             "kind": np.empty((ns, A), np.uint8),
         }
+        if want_prev:
+            out["prev"] = np.empty((ns, A), np.int32)
         ties = np.zeros(1, np.int64)
         djs = np.zeros(1, np.float64)
         opts = _Opts(int(self_mode), int(tie_mode), int(force_sssp))
-        r = lib().orc_rows(self.g, C.byref(opts), _ptr(src), ns, _ptr(tg), A,
-                           _ptr(out["lat"]), _ptr(out["rel"]), _ptr(out["next"]), _ptr(out["hops"]),
-                           _ptr(out["kind"]), _ptr(ties) if want_ties else None,
-                           _ptr(djs) if want_dijkstra_time else None, int(nthreads))
+        r = lib().orc_rows2(self.g, C.byref(opts), _ptr(src), ns, _ptr(tg), A,
+                            _ptr(out["lat"]), _ptr(out["rel"]), _ptr(out["next"]), _ptr(out["hops"]),
+                            _ptr(out["kind"]), _ptr(out["prev"]) if want_prev else None,
+                            _ptr(ties) if want_ties else None,
+                            _ptr(djs) if want_dijkstra_time else None, int(nthreads))
         if r != 0:
             raise RuntimeError(f"orc_rows failed: {r}")
         out["ok"] = out["kind"] != KIND_FAIL
         out["double_ties"] = int(ties[0])
         out["dijkstra_seconds"] = float(djs[0])
+        return out
+
+    def rows_owner(self, attached, order, self_mode: int = 0, tie_mode: int = 0):
+        """The reference's answers when every attached source has run its Dijkstra
+        in `order` (slot indices), replaying the path cache: a computed path (s, t)
+        is stored only if neither (s, t) nor (t, s) is cached yet
+        (_topology_shouldStorePath, shd-topology.c:1292-1321); DIRECT pairs are
+        never stored from a Dijkstra row (:1305-1316) and are recomputed on lookup;
+        a lookup tries (s, t) then (t, s) whatever the direction (:1970-1973,
+        :2017-2020).  Pure-Python cache simulation: small graphs only.
+        Next hop of an entry answered by the reverse path: the vertex before s on
+        the owner's path t -> s when undirected, -1 when directed (the reference's
+        Path has no next hop; ours is the first hop of the path it returns)."""
+        A_ = np.ascontiguousarray(attached, np.int32)
+        r = self.rows(A_, A_, self_mode=self_mode, tie_mode=tie_mode, want_prev=True)
+        A = A_.shape[0]
+        cache = {}
+        for s in order:
+            for t in range(A):
+                if r["kind"][s, t] != KIND_SSSP or s == t:
+                    continue
+                if (s, t) in cache or (t, s) in cache:
+                    continue
+                cache[(s, t)] = s
+        out = {k: r[k].copy() for k in ("lat", "rel", "next", "hops", "kind")}
+        for s in range(A):
+            for t in range(A):
+                if s == t or r["kind"][s, t] in (KIND_DIRECT,):
+                    continue
+                if (s, t) in cache:
+                    continue
+                if (t, s) in cache:
+                    out["lat"][s, t] = r["lat"][t, s]
+                    out["rel"][s, t] = r["rel"][t, s]
+                    out["hops"][s, t] = r["hops"][t, s]
+                    out["next"][s, t] = -1 if self.top.directed else r["prev"][t, s]
+                    out["kind"][s, t] = KIND_SSSP
+                else:   # neither direction stored: the lookup fails
+                    out["lat"][s, t] = out["rel"][s, t] = -1.0
+                    out["next"][s, t] = -1
+                    out["hops"][s, t] = 0
+                    out["kind"][s, t] = KIND_FAIL
+        out["ok"] = out["kind"] != KIND_FAIL
         return out

@@ -108,6 +108,7 @@ struct RowMode {
     int32_t prefer;
     int32_t self_mode;
     int32_t multi_rep;
+    int32_t directed;
 };
 
 // Per-lane route record carried with the distance: the path-order reliability
@@ -134,6 +135,7 @@ struct Table {
     int32_t* next;
     uint16_t* hops;
     int32_t A;
+    int32_t* prev;    // owner-replay mode only: vertex before the target on the path
 };
 
 __device__ __forceinline__ bool has_attr(double x) { return !__builtin_isnan(x); }
@@ -674,10 +676,11 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
         const int32_t g = b * (WAVE / L) + lane / L, j = lane % L;
         const int32_t s = srcv[b * WAVE + lane];
         double Lt = -1.0, R = -1.0;
-        int32_t N = -1, H = 0;
+        int32_t N = -1, H = 0, PV = -1;
         if (s >= 0) {
             if (t == s) {
                 self_entry(G, md, s, Lt, R, N, H);
+                PV = (H == 2) ? N : (H > 0 ? s : -1);
             } else {
                 // a pruned pendant target is one edge past its anchor: Dijkstra's
                 // d[t] = d[c] + w, parent c (its only candidate)
@@ -738,6 +741,14 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
                     if (Lt == 0) Lt = 1;   // shd-topology.c:1833-1837
                     N = rr.f;
                     H = rr.h;
+                    if (tb.prev) {
+                        if (kt >= 0) {
+                            PV = G.corev[c];
+                        } else {
+                            const int32_t pk = st.P[rt];
+                            PV = pk >= 0 ? G.corev[G.icol[pk]] : s;   // -2: parent is the pendant source
+                        }
+                    }
                 }
             }
         }
@@ -746,6 +757,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
         tb.rel[o] = R;
         tb.next[o] = N;
         tb.hops[o] = (uint16_t)(H > 65535 ? 65535 : H);
+        if (tb.prev) tb.prev[o] = PV;
     }
 }
 
@@ -773,6 +785,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_direct(int32_t groups, int32_t s
         tb.rel[o] = R;
         tb.next[o] = N;
         tb.hops[o] = (uint16_t)H;
+        if (tb.prev) tb.prev[o] = (H == 2) ? N : (H > 0 ? s : -1);
     }
 }
 
@@ -801,6 +814,67 @@ __global__ __launch_bounds__(BLOCK) void k_direct_overlay(int32_t groups, int32_
         tb.rel[o] = r;
         tb.next[o] = t;
         tb.hops[o] = 1;
+        if (tb.prev) tb.prev[o] = s;
+    }
+}
+
+// Owner replay (compat with the reference's first-writer-wins path cache,
+// _topology_shouldStorePath shd-topology.c:1292-1321 + the either-direction
+// lookup of _topology_getPathEntry :1952-2034): for each unordered slot pair,
+// the source that ran first stores its path if it is not DIRECT and routable,
+// the second stores only if the first did not; a non-DIRECT query answers its
+// own stored path, else the reverse one (same latency / reliability / hops; next
+// hop = the vertex before the querier on the owner's path when undirected, -1
+// when directed), else fails.  One lane per pair (i < j): lane = i of a
+// 64-slot block, wave = (block, j).
+__device__ __forceinline__ bool has_edge(const DevGraph& G, int32_t a, int32_t b) {
+    int32_t lo = G.dptr[a], hi = G.dptr[a + 1];
+    while (lo < hi) {
+        const int32_t mid = lo + ((hi - lo) >> 1);
+        if (G.dcol[mid] < b) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < G.dptr[a + 1] && G.dcol[lo] == b;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_owner_replay(int32_t A, const int32_t* __restrict__ rank,
+                                                        const int32_t* __restrict__ slot_vertex, DevGraph G,
+                                                        RowMode md, Table tb) {
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int64_t nblk = (A + WAVE - 1) / WAVE;
+    const int64_t items = nblk * A;
+    const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
+    for (int64_t it = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it < items; it += nwaves) {
+        const int32_t bi = (int32_t)(it / A);
+        const int32_t j = (int32_t)(it - (int64_t)bi * A);
+        const int32_t i = bi * WAVE + lane;
+        if (i >= A || i >= j) continue;
+        const int32_t vi = slot_vertex[i], vj = slot_vertex[j];
+        const bool dij = md.prefer && has_edge(G, vi, vj);   // DIRECT, never cached
+        const bool dji = md.prefer && has_edge(G, vj, vi);
+        const size_t oij = tidx(bi, A, j, lane);
+        const size_t oji = tidx(j / WAVE, A, i, j % WAVE);
+        const bool i_first = rank[i] < rank[j];
+        const size_t of = i_first ? oij : oji, oo = i_first ? oji : oij;
+        const bool dfo = i_first ? dij : dji, dof = i_first ? dji : dij;
+        const double lf = tb.lat[of], lo_ = tb.lat[oo];
+        const bool sf = !dfo && lf > -1.0;                 // first runner stored (f, o)
+        const bool so = !dof && lo_ > -1.0 && !sf;         // second stored (o, f)
+        const double rf = tb.rel[of], ro = tb.rel[oo];
+        const uint16_t hf = tb.hops[of], ho = tb.hops[oo];
+        const int32_t pf = tb.prev[of], po = tb.prev[oo];
+        if (!dfo && !sf) {   // (f, o) answers the reverse path or fails
+            tb.lat[of] = so ? lo_ : -1.0;
+            tb.rel[of] = so ? ro : -1.0;
+            tb.hops[of] = so ? ho : 0;
+            tb.next[of] = (so && !md.directed) ? po : -1;
+        }
+        if (!dof && !so) {   // (o, f)
+            tb.lat[oo] = sf ? lf : -1.0;
+            tb.rel[oo] = sf ? rf : -1.0;
+            tb.hops[oo] = sf ? hf : 0;
+            tb.next[oo] = (sf && !md.directed) ? pf : -1;
+        }
     }
 }
 
@@ -861,6 +935,7 @@ struct spe_table {
     bool built = false;
     Table tb{};
     int32_t* d_slot_vertex = nullptr;
+    int32_t* d_rank = nullptr;     // owner replay: position of each slot in the source-run order
     int32_t* d_vertex_slot = nullptr;
     std::vector<int32_t> attached;
     // workspace
@@ -1130,6 +1205,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     t->md.prefer = g->hg.prefer_direct && !force;
     t->md.self_mode = o.self_mode;
     t->md.multi_rep = g->hg.multi_rep;
+    t->md.directed = g->hg.directed;
     // state per group = n * 64 * 28 B; keep the batch's working set within a few GB
     int32_t groups = o.groups_per_launch;
     if (groups <= 0) {
@@ -1179,6 +1255,17 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         TRY(dev_alloc(t->allocs, &t->tb.rel, elems));
         TRY(dev_alloc(t->allocs, &t->tb.next, elems));
         TRY(dev_alloc(t->allocs, &t->tb.hops, elems));
+    }
+    if (o.owner_rank) {   // owner replay needs every source row in this table
+        if (t->blk0 != 0 || t->blk1 != nblk_all) {
+            delete t;
+            return fail(SPE_EUNSUPPORTED, "owner replay needs a table that owns every source block");
+        }
+        std::vector<int32_t> rk(o.owner_rank, o.owner_rank + n_attached);
+        const int32_t* tmpr = nullptr;
+        TRY(dev_upload(t->allocs, rk, &tmpr));
+        t->d_rank = const_cast<int32_t*>(tmpr);
+        TRY(dev_alloc(t->allocs, &t->tb.prev, elems));
     }
     const std::vector<int32_t> sv(attached, attached + n_attached);
     const int32_t* tmp = nullptr;
@@ -1356,7 +1443,15 @@ static void launch_rows_sssp(spe_table* t, int grid, int32_t blocks, int32_t sb0
 
 int spe_table_build(spe_table* t, void* stream) {
     if (!t) return fail(SPE_EINVAL, "NULL table");
-    return spe_table_build_blocks(t, t->blk0, t->blk1, stream);
+    int r = spe_table_build_blocks(t, t->blk0, t->blk1, stream);
+    if (r || !t->d_rank || t->md.complete) return r;
+    hipStream_t s = stream ? (hipStream_t)stream : t->stream;
+    const int64_t items = (int64_t)((t->A + WAVE - 1) / WAVE) * t->A;
+    k_owner_replay<<<grid_for(items * WAVE, BLOCK, 8192), BLOCK, 0, s>>>(t->A, t->d_rank, t->d_slot_vertex,
+                                                                        t->g->dev, t->md, t->tb);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    return SPE_OK;
 }
 
 int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end, void* stream) {

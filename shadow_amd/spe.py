@@ -46,7 +46,7 @@ class TableOpts(C.Structure):
                 ("block_begin", C.c_int32), ("block_end", C.c_int32),
                 ("ext_latency", C.c_void_p), ("ext_reliability", C.c_void_p),
                 ("ext_next_hop", C.c_void_p), ("ext_hops", C.c_void_p), ("ext_filled", C.c_int32),
-                ("lanes_per_group", C.c_int32)]
+                ("owner_rank", C.c_void_p), ("lanes_per_group", C.c_int32)]
 
 
 class TableLayout(C.Structure):
@@ -169,7 +169,8 @@ class PathTable:
     """spe_table: the per-(source, target) path table for attached vertices."""
 
     def __init__(self, graph: Graph, attached, self_mode: int = SPE_SELF_ROW, force_sssp: bool = False,
-                 groups: int = 0, blocks=None, ext=None, ext_filled: bool = False, lanes: int = 0):
+                 groups: int = 0, blocks=None, ext=None, ext_filled: bool = False, lanes: int = 0,
+                 owner_order=None):
         self.graph = graph
         self.attached = np.ascontiguousarray(attached, np.int32)
         self.A = int(self.attached.shape[0])
@@ -178,6 +179,10 @@ class PathTable:
         o.force_sssp = int(bool(force_sssp))
         o.groups_per_launch = int(groups)
         o.lanes_per_group = int(lanes)
+        if owner_order is not None:   # source-run order (slots) -> rank of each slot
+            self._rank = np.empty(self.A, np.int32)
+            self._rank[np.asarray(owner_order, np.int64)] = np.arange(self.A, dtype=np.int32)
+            o.owner_rank = self._rank.ctypes.data
         if blocks is not None:
             o.block_begin, o.block_end = int(blocks[0]), int(blocks[1])
         if ext is not None:  # four device pointers (ints)
