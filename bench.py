@@ -223,6 +223,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--blocks-per-step", type=int, default=16)
     ap.add_argument("--groups", type=int, default=0)
+    ap.add_argument("--engine", type=int, default=0, help="0 auto, 1 batch (64-lane HBM state), 2 LDS-resident rows")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
@@ -256,7 +257,7 @@ def main():
     top, att, desc = workload(args.config)
     g = spe.Graph(top, device=local)
     info = g.info()
-    t = spe.PathTable(g, att, groups=args.groups)
+    t = spe.PathTable(g, att, groups=args.groups, engine=args.engine)
     A = t.A
     nblk = t.nblocks
     bps = max(1, args.blocks_per_step)
@@ -308,12 +309,17 @@ def main():
     b_rows = 22.0 * A
     roof = None
     extra = {}
+    lds = kp is not None and kp["lds"]["launches"] > 0
+    if lds:   # one fused kernel: relaxation in LDS + row writes
+        b_relax += b_rows
     if kp is not None:
-        rl = kp["relax"]
+        kname = "k_sssp_lds" if lds else "k_relax"
+        rl = kp["lds" if lds else "relax"]
         relax_s = rl["ms"] / 1e3
         ach = b_relax * done / relax_s / 1e9 if relax_s > 0 else 0.0
-        traffic = pmc_traffic(args, "k_relax")
-        roof = {"bound": "hbm", "kernel": "k_relax (SSSP stage)", "achieved": round(ach, 1),
+        traffic = pmc_traffic(args, kname)
+        roof = {"bound": "hbm", "kernel": kname + (" (SSSP + rows, LDS-resident state)" if lds else " (SSSP stage)"),
+                "achieved": round(ach, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "launches": rl["launches"], "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
                 "algorithmic_bytes_per_source": b_relax}
@@ -325,7 +331,8 @@ def main():
                                   "algorithmic_bytes_per_source": b_rows}
         extra["kernel_ms"] = {k: round(v["ms"], 3) for k, v in kp.items()}
         extra["kernel_launches"] = {k: v["launches"] for k, v in kp.items()}
-        extra["pipeline_frac_of_hbm"] = round((b_relax + b_rows) * value / 1e9 / HBM_PEAK_GBS, 4)
+        extra["pipeline_frac_of_hbm"] = round((b_relax + (0 if lds else b_rows)) * value / 1e9 / HBM_PEAK_GBS, 4)
+        extra["engine"] = "lds" if lds else "batch"
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(top, att, args.cpu_seconds)

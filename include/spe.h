@@ -52,6 +52,10 @@ extern "C" {
 #define SPE_SELF_ROW 0       /* (s,s) from the Dijkstra row's [s] path (igraph 0.7-0.9) */
 #define SPE_SELF_RULE 1      /* (s,s) = 2 x min incident edge (shd-topology.c:1530-1638) */
 
+#define SPE_ENGINE_AUTO 0    /* LDS engine when the relaxation graph fits one CU's LDS, else BATCH */
+#define SPE_ENGINE_BATCH 1   /* 64-source lane groups, HBM-resident state, frontier rounds */
+#define SPE_ENGINE_LDS 2     /* one workgroup per source row, state resident in LDS (<= ~11k vertices) */
+
 typedef struct spe_graph spe_graph;
 typedef struct spe_table spe_table;
 
@@ -109,6 +113,7 @@ typedef struct spe_table_opts {
                                      * entry (s,t) then answers the path stored for {s,t} in
                                      * either direction.  Needs a table owning all blocks; applied
                                      * by spe_table_build (not spe_table_build_blocks). */
+    int32_t engine;                 /* SPE_ENGINE_* */
     int32_t lanes_per_group;        /* sources sharing one relaxation frontier: 16, 32 or 64;
                                      * 0 = default (64: measured fastest on C3) */
 } spe_table_opts;
@@ -160,7 +165,8 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
 
 /* Per-kernel device time, from HIP events recorded around every launch on the
  * build stream while profiling is enabled (costs one event pair per launch). */
-enum { SPE_K_INIT = 0, SPE_K_SEED, SPE_K_HEAVY, SPE_K_RELAX, SPE_K_ROWS, SPE_K_DIRECT, SPE_K_COUNT };
+enum { SPE_K_INIT = 0, SPE_K_SEED, SPE_K_HEAVY, SPE_K_RELAX, SPE_K_ROWS, SPE_K_DIRECT, SPE_K_LDS, SPE_K_FW,
+       SPE_K_COUNT };
 typedef struct spe_kernel_profile {
     double ms[SPE_K_COUNT];
     int64_t launches[SPE_K_COUNT];

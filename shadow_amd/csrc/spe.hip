@@ -818,6 +818,271 @@ __global__ __launch_bounds__(BLOCK) void k_direct_overlay(int32_t groups, int32_
     }
 }
 
+// ------------------------------------------------------------------------
+// LDS engine: one workgroup per source row with the row's whole relaxation
+// state resident in LDS (D f64, parent entry i32, hops u16 + two frontier
+// bitsets = 14.25 B per relaxation vertex: up to ~11k vertices in 160 KB).
+// For such graphs (Shadow's own topologies, C2) this replaces the 64-lane
+// HBM-resident batch relaxation:
+//   1. push Bellman-Ford with LDS 64-bit atomic min on the distance bits
+//      (non-negative doubles order as integers) over a changed-vertex bitset;
+//   2. canonical parent = argmin (d[u], u) over {u : fl(d[u] + w) == d[v]};
+//   3. level sweeps over the parent tree: hops, then the path-order
+//      reliability fold and the first hop (each (v) once, in hop order);
+//   4. the row's entries are written straight into the SB64 table.
+// Distances are the least fixpoint of d[v] = min fl(d[u] + w) exactly as in the
+// batch engine, so rows are bit-identical.
+constexpr int LDS_T = 1024;                 // threads per workgroup (16 waves)
+constexpr int LDS_MAX_BYTES = 160 * 1024;
+
+__host__ __device__ constexpr size_t lds_bytes(int32_t nc) {
+    return (size_t)nc * 14 + 2 * (size_t)((nc + 31) / 32) * 4 + 64;
+}
+
+__device__ __forceinline__ int32_t par_vertex(const DevGraph& G, int32_t k) { return G.icol[k]; }
+
+__global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1, const int32_t* __restrict__ slot_vertex,
+                                                     int32_t blk0, DevGraph G, RowMode md, Table tb) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int32_t nc = G.n;
+    const int32_t nw = (nc + 31) / 32;
+    double* D = reinterpret_cast<double*>(smem);
+    unsigned long long* Db = reinterpret_cast<unsigned long long*>(smem);
+    int32_t* P = reinterpret_cast<int32_t*>(D + nc);
+    uint32_t* F0 = reinterpret_cast<uint32_t*>(P + nc);
+    uint32_t* F1 = F0 + nw;
+    uint16_t* H = reinterpret_cast<uint16_t*>(F1 + nw);
+    const int32_t tid = threadIdx.x;
+    const unsigned long long INF_BITS = 0x7FF0000000000000ull;
+    // Workgroups are dealt round-robin over the 8 XCDs; give the workgroups of
+    // one XCD consecutive slots so the partial 512-B SB64 segments each row
+    // writes meet in the same L2 before write-back.
+    const int32_t gx = gridDim.x;
+    const int32_t bx = (gx % 8 == 0) ? (blockIdx.x % 8) * (gx / 8) + blockIdx.x / 8 : blockIdx.x;
+    for (int32_t slot = slot0 + bx; slot < slot1; slot += gx) {
+        const int32_t s = slot_vertex[slot];
+        const int32_t sc = G.core_id[s];
+        const int32_t seed = sc >= 0 ? sc : G.anchor_core[s];
+        for (int32_t v = tid; v < nc; v += LDS_T) {
+            Db[v] = INF_BITS;
+            P[v] = -1;
+            H[v] = 0xFFFF;
+        }
+        for (int32_t w = tid; w < nw; w += LDS_T) {
+            F0[w] = 0;
+            F1[w] = 0;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            if (sc >= 0) {
+                D[sc] = 0.0;
+                H[sc] = 0;
+            } else {   // pruned pendant source: first step fixed (see k_init_state)
+                D[seed] = 0.0 + G.fiw[G.fiptr[s]];
+                P[seed] = -2;
+                H[seed] = 1;
+            }
+            F0[seed >> 5] = 1u << (seed & 31);
+        }
+        __syncthreads();
+        // 1. push relaxation to the fixpoint
+        uint32_t* cur = F0;
+        uint32_t* nxt = F1;
+        for (;;) {
+            bool any = false;
+            for (int32_t v = tid; v < nc; v += LDS_T) {
+                if (!((cur[v >> 5] >> (v & 31)) & 1u)) continue;
+                const double dv = D[v];
+                const int32_t o0 = G.optr[v], o1 = G.optr[v + 1];
+                for (int32_t k = o0; k < o1; ++k) {
+                    const int32_t x = G.ocol[k];
+                    const double w = G.undirected ? G.iw[k] : G.iw[G.orev[k]];
+                    const double cand = dv + w;
+                    const unsigned long long cb = (unsigned long long)__double_as_longlong(cand);
+                    const unsigned long long old = atomicMin(&Db[x], cb);
+                    if (cb < old) {
+                        atomicOr(&nxt[x >> 5], 1u << (x & 31));
+                        any = true;
+                    }
+                }
+            }
+            __syncthreads();
+            for (int32_t w = tid; w < nw; w += LDS_T) cur[w] = 0;
+            if (!__syncthreads_or(any)) break;
+            uint32_t* tmp = cur;
+            cur = nxt;
+            nxt = tmp;
+        }
+        // 2. canonical parents (the source and a pendant seed keep theirs)
+        for (int32_t v = tid; v < nc; v += LDS_T) {
+            if (v == sc || P[v] == -2) continue;
+            const double dv = D[v];
+            if (Db[v] == INF_BITS) continue;
+            double bdu = INF;
+            int32_t bu = -1, bk = -1;
+            for (int32_t k = G.iptr[v]; k < G.iptr[v + 1]; ++k) {
+                const int32_t u = G.icol[k];
+                const double du = D[u];
+                if (!(du < INF)) continue;
+                const double alt = du + G.iw[k];
+                if (alt == dv && alt > du && (du < bdu || (du == bdu && u < bu))) {
+                    bdu = du;
+                    bu = u;
+                    bk = k;
+                }
+            }
+            P[v] = bk;
+        }
+        __syncthreads();
+        // 3a. hops by level sweeps over the parent tree
+        for (int32_t lev = (sc >= 0 ? 1 : 2);; ++lev) {
+            bool any = false;
+            for (int32_t v = tid; v < nc; v += LDS_T) {
+                const int32_t k = P[v];
+                if (k < 0 || H[v] != 0xFFFF) continue;
+                if (H[par_vertex(G, k)] == lev - 1) {
+                    H[v] = (uint16_t)lev;
+                    any = true;
+                }
+            }
+            if (!__syncthreads_or(any)) break;
+        }
+        // 4a. latency (+ hops) of every target; slow path re-folds along the tree
+        const int32_t sb_local = slot / WAVE - blk0, lane = slot % WAVE;
+        const double fs = G.vfac[s];
+        for (int32_t j = tid; j < tb.A; j += LDS_T) {
+            const int32_t t = slot_vertex[j];
+            const size_t o = tidx(sb_local, tb.A, j, lane);
+            double Lt = -1.0, R = -1.0;
+            int32_t N = -1, Hh = 0;
+            if (t == s) {
+                self_entry(G, md, s, Lt, R, N, Hh);
+                tb.lat[o] = Lt;
+                tb.rel[o] = R;
+                tb.next[o] = N;
+                tb.hops[o] = (uint16_t)Hh;
+                if (tb.prev) tb.prev[o] = (Hh == 2) ? N : (Hh > 0 ? s : -1);
+                continue;
+            }
+            const int32_t tc = G.core_id[t];
+            const int32_t c = tc >= 0 ? tc : G.anchor_core[t];
+            const int32_t kt = tc >= 0 ? -1 : G.fiptr[t];
+            if (Db[c] != INF_BITS) {
+                Hh = H[c] + (kt >= 0 ? 1 : 0);
+                const double ft = G.vfac[t];
+                const bool fast = (!has_attr(ft) || ft == 1.0) && !md.multi_rep;
+                if (fast) {
+                    Lt = kt >= 0 ? D[c] + G.fiw[kt] : D[c];
+                } else {   // path-order re-fold (vertex loss on t / multigraph get_eid latencies)
+                    double l = 0.0;
+                    for (int32_t i = 1; i <= Hh; ++i) {
+                        int32_t back = Hh - i;
+                        double ew;
+                        if (kt >= 0 && back == 0) {
+                            ew = G.fiwrep[kt];
+                        } else {
+                            int32_t x = c;
+                            if (kt >= 0) back -= 1;
+                            for (int32_t q = 0; q < back; ++q) x = par_vertex(G, P[x]);
+                            ew = P[x] >= 0 ? G.iwrep[P[x]] : G.fiwrep[G.fiptr[s]];
+                        }
+                        l += ew;
+                    }
+                    Lt = l;
+                }
+                if (Lt == 0) Lt = 1;   // shd-topology.c:1833-1837
+                if (tb.prev) tb.prev[o] = kt >= 0 ? G.corev[c] : (P[c] >= 0 ? G.corev[par_vertex(G, P[c])] : s);
+            }
+            tb.lat[o] = Lt;
+            tb.hops[o] = (uint16_t)Hh;
+        }
+        __syncthreads();
+        // 3b. reliability fold by hop level, in D's space (D is no longer needed)
+        double* Rr = D;
+        const double r0 = has_attr(fs) ? 1.0 * fs : 1.0;   // shd-topology.c:1428-1430
+        for (int32_t v = tid; v < nc; v += LDS_T) {
+            if (v == sc) Rr[v] = r0;
+            else if (P[v] == -2) Rr[v] = r0 * G.fia[G.fiptr[s]];
+        }
+        __syncthreads();
+        for (int32_t lev = (sc >= 0 ? 1 : 2);; ++lev) {
+            bool any = false;
+            for (int32_t v = tid; v < nc; v += LDS_T) {
+                if (H[v] != lev || P[v] < 0) continue;
+                Rr[v] = Rr[par_vertex(G, P[v])] * G.ia[P[v]];
+                any = true;
+            }
+            if (!__syncthreads_or(any)) break;
+        }
+        for (int32_t j = tid; j < tb.A; j += LDS_T) {
+            const int32_t t = slot_vertex[j];
+            if (t == s) continue;
+            const int32_t tc = G.core_id[t];
+            const int32_t c = tc >= 0 ? tc : G.anchor_core[t];
+            const int32_t kt = tc >= 0 ? -1 : G.fiptr[t];
+            if (H[c] == 0xFFFF) continue;   // unreachable (lat already -1)
+            const size_t o = tidx(sb_local, tb.A, j, lane);
+            const double ft = G.vfac[t];
+            double R;
+            if (!has_attr(ft) || ft == 1.0) {
+                R = kt >= 0 ? Rr[c] * G.fia[kt] : Rr[c];
+            } else {   // ((1 * fs) * ft) * a1 * a2 ... : the target factor comes second
+                const int32_t Hh = H[c] + (kt >= 0 ? 1 : 0);
+                double r = 1.0;
+                if (has_attr(fs)) r *= fs;
+                r *= ft;
+                for (int32_t i = 1; i <= Hh; ++i) {
+                    int32_t back = Hh - i;
+                    double ea;
+                    if (kt >= 0 && back == 0) {
+                        ea = G.fia[kt];
+                    } else {
+                        int32_t x = c;
+                        if (kt >= 0) back -= 1;
+                        for (int32_t q = 0; q < back; ++q) x = par_vertex(G, P[x]);
+                        ea = P[x] >= 0 ? G.ia[P[x]] : G.fia[G.fiptr[s]];
+                    }
+                    r *= ea;
+                }
+                R = r;
+            }
+            tb.rel[o] = R;
+        }
+        __syncthreads();
+        // 3c. first hop by hop level (original ids), in the same space
+        int32_t* Fh = reinterpret_cast<int32_t*>(D);
+        for (int32_t v = tid; v < nc; v += LDS_T) {
+            if (P[v] == -2) Fh[v] = G.corev[v];
+        }
+        __syncthreads();
+        for (int32_t lev = (sc >= 0 ? 1 : 2);; ++lev) {
+            bool any = false;
+            for (int32_t v = tid; v < nc; v += LDS_T) {
+                if (H[v] != lev || P[v] < 0) continue;
+                const int32_t u = par_vertex(G, P[v]);
+                Fh[v] = (u == sc) ? G.corev[v] : Fh[u];
+                any = true;
+            }
+            if (!__syncthreads_or(any)) break;
+        }
+        for (int32_t j = tid; j < tb.A; j += LDS_T) {
+            const int32_t t = slot_vertex[j];
+            if (t == s) continue;
+            const int32_t tc = G.core_id[t];
+            const int32_t c = tc >= 0 ? tc : G.anchor_core[t];
+            const size_t o = tidx(sb_local, tb.A, j, lane);
+            int32_t N = -1;
+            if (H[c] != 0xFFFF) N = tc >= 0 ? Fh[c] : (H[c] == 0 ? t : Fh[c]);
+            tb.next[o] = N;
+            if (N < 0) {
+                tb.rel[o] = -1.0;
+                if (tb.prev) tb.prev[o] = -1;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // Owner replay (compat with the reference's first-writer-wins path cache,
 // _topology_shouldStorePath shd-topology.c:1292-1321 + the either-direction
 // lookup of _topology_getPathEntry :1952-2034): for each unordered slot pair,
@@ -927,6 +1192,7 @@ struct spe_table {
     int32_t blk0 = 0, blk1 = 0;
     int32_t groups = 8;            // 64-source blocks per batch
     int32_t lanes = 16;            // sources per lane group (L)
+    int32_t engine = SPE_ENGINE_BATCH;   // resolved engine
     int32_t infl = 8;              // neighbour rows in flight per subgroup (4 or 8)
     bool trace = getenv("SPE_TRACE") != nullptr;   // diagnostic: per-launch times to stderr
     int32_t occ = 0;               // diagnostic: forced waves/SIMD of k_relax (0 = compiler's choice)
@@ -1222,6 +1488,29 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         return fail(SPE_EINVAL, "lanes_per_group must be 16, 32 or 64");
     }
     t->lanes = lanes;
+    {
+        const bool fits = lds_bytes(g->hg.nc) <= (size_t)LDS_MAX_BYTES;
+        int32_t e = o.engine;
+        bool from_env = false;
+        if (e == SPE_ENGINE_AUTO && getenv("SPE_ENGINE")) {   // test / diagnostic override
+            e = atoi(getenv("SPE_ENGINE"));
+            from_env = true;
+        }
+        if (e == SPE_ENGINE_LDS && !fits) {
+            if (!from_env) {
+                delete t;
+                return fail(SPE_EUNSUPPORTED, "relaxation graph too large for the LDS engine");
+            }
+            e = SPE_ENGINE_BATCH;
+        }
+        t->engine = (e == SPE_ENGINE_AUTO) ? (fits ? SPE_ENGINE_LDS : SPE_ENGINE_BATCH) : e;
+        if (t->engine == SPE_ENGINE_LDS && !t->md.complete) {
+            // no HBM state: one launch covers every owned block (unless asked otherwise)
+            if (o.groups_per_launch <= 0) t->groups = std::max(1, t->blk1 - t->blk0);
+            HIP_TRY(hipFuncSetAttribute((const void*)k_sssp_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds_bytes(g->hg.nc)));
+        }
+    }
     t->infl = lanes == 64 ? 8 : 4;
     if (getenv("SPE_INFL")) {
         const int want = atoi(getenv("SPE_INFL"));
@@ -1275,7 +1564,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     t->d_vertex_slot = const_cast<int32_t*>(tmp);
     const size_t G = (size_t)t->groups;
     const size_t GL = G * (WAVE / t->lanes);   // lane groups per batch
-    if (!t->md.complete) {
+    if (!t->md.complete && t->engine == SPE_ENGINE_BATCH) {
         const size_t se = G * n * WAVE;
         TRY(dev_alloc(t->allocs, &t->st.D, se));
         TRY(dev_alloc(t->allocs, &t->st.P, se));
@@ -1482,6 +1771,24 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
         if (t->md.complete) {
             LaunchTimer lt(t, s, SPE_K_DIRECT);
             k_rows_direct<<<row_grid, BLOCK, 0, s>>>(groups, sb0, t->d_srcv, t->d_slot_vertex, g->dev, t->md, t->tb);
+        } else if (t->engine == SPE_ENGINE_LDS) {
+            {
+                LaunchTimer lt(t, s, SPE_K_LDS);
+                const int32_t s0 = b * WAVE, s1 = std::min(t->A, (b + groups) * WAVE);
+                const size_t bytes = lds_bytes(g->hg.nc);
+                int cus = 256;
+                (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device);
+                const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, LDS_MAX_BYTES / bytes));
+                int grid = std::min(s1 - s0, cus * per_cu);
+                if (grid >= 8) grid -= grid % 8;   // whole XCD rounds (see k_sssp_lds's slot order)
+                k_sssp_lds<<<std::max(1, grid), LDS_T, bytes, s>>>(s0, s1, t->d_slot_vertex, t->blk0, g->dev, t->md,
+                                                                   t->tb);
+            }
+            if (t->md.prefer) {
+                LaunchTimer lt(t, s, SPE_K_DIRECT);
+                k_direct_overlay<<<(groups * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(
+                    groups, sb0, t->d_srcv, t->d_vertex_slot, g->dev, t->tb);
+            }
         } else {
             int r = relax_to_convergence(t, groups, s);
             if (r) return r;

@@ -20,6 +20,7 @@ LIB_PATH = os.path.join(_HERE, "libspe.so")
 SPE_OK = 0
 SPE_SELF_ROW = 0
 SPE_SELF_RULE = 1
+SPE_ENGINE_AUTO, SPE_ENGINE_BATCH, SPE_ENGINE_LDS = 0, 1, 2
 WAVE = 64
 
 
@@ -46,7 +47,7 @@ class TableOpts(C.Structure):
                 ("block_begin", C.c_int32), ("block_end", C.c_int32),
                 ("ext_latency", C.c_void_p), ("ext_reliability", C.c_void_p),
                 ("ext_next_hop", C.c_void_p), ("ext_hops", C.c_void_p), ("ext_filled", C.c_int32),
-                ("owner_rank", C.c_void_p), ("lanes_per_group", C.c_int32)]
+                ("owner_rank", C.c_void_p), ("engine", C.c_int32), ("lanes_per_group", C.c_int32)]
 
 
 class TableLayout(C.Structure):
@@ -60,11 +61,11 @@ class Entry(C.Structure):
                 ("hops", C.c_int32)]
 
 
-KERNELS = ["init", "seed", "heavy", "relax", "rows", "direct"]
+KERNELS = ["init", "seed", "heavy", "relax", "rows", "direct", "lds", "fw"]
 
 
 class KernelProfile(C.Structure):
-    _fields_ = [("ms", C.c_double * 6), ("launches", C.c_int64 * 6)]
+    _fields_ = [("ms", C.c_double * 8), ("launches", C.c_int64 * 8)]
 
 
 class BuildStats(C.Structure):
@@ -170,7 +171,7 @@ class PathTable:
 
     def __init__(self, graph: Graph, attached, self_mode: int = SPE_SELF_ROW, force_sssp: bool = False,
                  groups: int = 0, blocks=None, ext=None, ext_filled: bool = False, lanes: int = 0,
-                 owner_order=None):
+                 owner_order=None, engine: int = 0):
         self.graph = graph
         self.attached = np.ascontiguousarray(attached, np.int32)
         self.A = int(self.attached.shape[0])
@@ -179,6 +180,7 @@ class PathTable:
         o.force_sssp = int(bool(force_sssp))
         o.groups_per_launch = int(groups)
         o.lanes_per_group = int(lanes)
+        o.engine = int(engine)
         if owner_order is not None:   # source-run order (slots) -> rank of each slot
             self._rank = np.empty(self.A, np.int32)
             self._rank[np.asarray(owner_order, np.int64)] = np.arange(self.A, dtype=np.int32)

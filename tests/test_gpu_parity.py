@@ -103,7 +103,8 @@ def test_sssp_rows_match_igraph_restatement(spe, name):
     out, t, _ = run_gpu(spe, top, A)
     compare(out, ora, label=name)
     st = t.stats()
-    assert st["iterations"] > 0
+    if os.environ.get("SPE_ENGINE") != "2":   # the LDS engine converges inside one launch per block range
+        assert st["iterations"] > 0
 
 
 @pytest.mark.parametrize("self_mode", [0, 1])
