@@ -71,6 +71,7 @@ struct DevGraph {
     int32_t n_full;          // all vertices (original ids)
     const int32_t* iptr;
     const int32_t* icol;
+    const int32_t* irow;     // in-CSR entry -> its target vertex (flat edge passes)
     const double* iw;
     const double* ia;
     const double* iwrep;
@@ -79,6 +80,7 @@ struct DevGraph {
     const int32_t* orev;     // out-entry -> index of the same edge in the target's in-CSR list
     const double* owrep;
     const double* oarep;
+    const double* ow;        // relaxation (lightest) weight per out-entry (== iw when undirected)
     int32_t undirected;      // out-CSR == in-CSR
     const uint8_t* heavy;    // [n] in-degree > 64
     const uint8_t* oheavy;   // [out entry] heavy[target]: which frontier buffer it goes to
@@ -819,54 +821,142 @@ __global__ __launch_bounds__(BLOCK) void k_direct_overlay(int32_t groups, int32_
 }
 
 // ------------------------------------------------------------------------
-// LDS engine: one workgroup per source row with the row's whole relaxation
-// state resident in LDS (D f64, parent entry i32, hops u16 + two frontier
-// bitsets = 14.25 B per relaxation vertex: up to ~11k vertices in 160 KB).
-// For such graphs (Shadow's own topologies, C2) this replaces the 64-lane
-// HBM-resident batch relaxation:
-//   1. push Bellman-Ford with LDS 64-bit atomic min on the distance bits
-//      (non-negative doubles order as integers) over a changed-vertex bitset;
-//   2. canonical parent = argmin (d[u], u) over {u : fl(d[u] + w) == d[v]};
-//   3. level sweeps over the parent tree: hops, then the path-order
-//      reliability fold and the first hop (each (v) once, in hop order);
-//   4. the row's entries are written straight into the SB64 table.
-// Distances are the least fixpoint of d[v] = min fl(d[u] + w) exactly as in the
-// batch engine, so rows are bit-identical.
+// LDS engine: one workgroup per source row with the row's relaxation state
+// resident in LDS.  For graphs up to ~11k relaxation vertices (Shadow's own
+// topologies, C2) this replaces the 64-lane HBM-resident batch relaxation.
+// Per source row:
+//   1. push Bellman-Ford over a changed-vertex bitset: LDS 64-bit atomic min on
+//      the distance bits (non-negative doubles order as integers); a wave takes
+//      64 vertices and spreads their out-edges over its lanes (wave_expand), so
+//      a round costs one global round trip per 64 edges, not one per edge;
+//   2. canonical parent = argmin (d[u], u) over {u : fl(d[u] + w) == d[v]},
+//      in-edges spread over lanes the same way, per-vertex argmin in LDS;
+//   3. latencies of every target (d is final);
+//   4. child lists of the parent tree (count, scan, scatter in LDS), then one
+//      top-down pass over the tree by hop level: hops, the path-order
+//      reliability fold r(v) = r(parent) * (1 - p_e) and the first hop of every
+//      vertex, each computed once from its parent's final values;
+//   5. reliability / next hop / hops of every target into the SB64 table.
+// Distances are the least fixpoint of d[v] = min fl(d[u] + w), as in the batch
+// engine, so rows are bit-identical (tests/test_gpu_lds.py).
 constexpr int LDS_T = 1024;                 // threads per workgroup (16 waves)
-constexpr int LDS_MAX_BYTES = 160 * 1024;
+constexpr int LDS_WAVES = LDS_T / WAVE;
+constexpr int LDS_MAX_BYTES = 160 * 1024 - 1024;   // dynamic share; the rest covers static __shared__
+constexpr int LDS_CAND_BYTES = LDS_WAVES * WAVE * 16;   // per-wave argmin scratch of the parent pass
 
-__host__ __device__ constexpr size_t lds_bytes(int32_t nc) {
-    return (size_t)nc * 14 + 2 * (size_t)((nc + 31) / 32) * 4 + 64;
+__host__ __device__ constexpr size_t lds_align(size_t b) { return (b + 15) & ~(size_t)15; }
+// D f64 | X i32 (out-row starts, then parent entry) | H u16 / argmin scratch | 2 bitsets
+__host__ __device__ constexpr size_t lds_hs_bytes(int32_t nc) {
+    return lds_align((size_t)nc * 2) > (size_t)LDS_CAND_BYTES ? lds_align((size_t)nc * 2) : (size_t)LDS_CAND_BYTES;
 }
+__host__ __device__ constexpr size_t lds_bytes(int32_t nc) {
+    return lds_align((size_t)nc * 8) + lds_align((size_t)nc * 4) + lds_hs_bytes(nc) +
+           2 * lds_align((size_t)((nc + 31) / 32) * 4);
+}
+
+// per-target constants of the row passes (host-built, SlotInfo[A])
+struct alignas(16) SlotInfo {
+    int32_t t;      // attached vertex (original id)
+    int32_t c;      // relaxation vertex the row reads: t itself or its pendant anchor
+    int32_t kt;     // full in-CSR entry of t's pendant edge, -1 if t is a relaxation vertex
+    int32_t pad;
+    double pw;      // latency of the pendant edge (relaxation weight), 0 otherwise
+    double pa;      // 1 - p of the pendant edge (get_eid edge), 1 otherwise
+};
+
+// per-workgroup global scratch of the tree pass (L2-resident: 32 B per vertex)
+struct alignas(16) TreeItem {
+    int32_t v;
+    int32_t f;      // first hop (original id), -1 at a core source
+    double r;       // reliability fold up to v
+};
+struct LdsScratch {
+    int32_t* child;     // [grid][nc]
+    TreeItem* q;        // [grid][nc] vertices in hop-level order
+    double* r;          // [grid][nc]
+    int32_t* f;         // [grid][nc]
+};
 
 __device__ __forceinline__ int32_t par_vertex(const DevGraph& G, int32_t k) { return G.icol[k]; }
 
-__global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1, const int32_t* __restrict__ slot_vertex,
-                                                     int32_t blk0, DevGraph G, RowMode md, Table tb) {
+// Spread the edges of up to 64 owner lanes (lane l owns `deg` consecutive
+// items) over the wave's lanes, 64 at a time.  body(ok, o, off) runs with the
+// whole wave (so it may shuffle): item `off` of owner lane `o`, ok = a real item.
+template <typename F>
+__device__ __forceinline__ void wave_expand(int32_t lane, int32_t deg, F&& body) {
+    int32_t incl = deg;
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+        const int32_t y = __shfl_up(incl, d);
+        if (lane >= d) incl += y;
+    }
+    const int32_t total = __shfl(incl, WAVE - 1);
+    const int32_t excl = incl - deg;
+    for (int32_t base = 0; base < total; base += WAVE) {
+        const int32_t e = base + lane;
+        int32_t o = 0;
+#pragma unroll
+        for (int step = WAVE / 2; step; step >>= 1) {
+            const int32_t y = __shfl(incl, o + step - 1);
+            if (y <= e) o += step;
+        }
+        const int32_t off = e - __shfl(excl, o);
+        body(e < total, o, off, base, excl, incl);
+    }
+}
+
+__device__ __forceinline__ int32_t wave_append(bool ok, int32_t lane, int32_t* tail) {
+    const uint64_t m = __ballot(ok);
+    int32_t b = 0;
+    if (lane == 0 && m) b = atomicAdd(tail, __popcll(m));
+    b = __shfl(b, 0);
+    return b + __popcll(m & ((1ull << lane) - 1ull));
+}
+
+__global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1, const SlotInfo* __restrict__ slots,
+                                                     int32_t blk0, DevGraph G, RowMode md, Table tb, LdsScratch sc_,
+                                                     unsigned long long* __restrict__ dbg) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int32_t nc = G.n;
     const int32_t nw = (nc + 31) / 32;
     double* D = reinterpret_cast<double*>(smem);
     unsigned long long* Db = reinterpret_cast<unsigned long long*>(smem);
-    int32_t* P = reinterpret_cast<int32_t*>(D + nc);
-    uint32_t* F0 = reinterpret_cast<uint32_t*>(P + nc);
-    uint32_t* F1 = F0 + nw;
-    uint16_t* H = reinterpret_cast<uint16_t*>(F1 + nw);
-    const int32_t tid = threadIdx.x;
+    int32_t* X = reinterpret_cast<int32_t*>(smem + lds_align((size_t)nc * 8));
+    unsigned char* hs = smem + lds_align((size_t)nc * 8) + lds_align((size_t)nc * 4);
+    uint16_t* H = reinterpret_cast<uint16_t*>(hs);
+    uint32_t* F0 = reinterpret_cast<uint32_t*>(hs + lds_hs_bytes(nc));
+    uint32_t* F1 = F0 + lds_align((size_t)nw * 4) / 4;
+    // after the latency pass the distance space holds the tree's child offsets + parent ids
+    int32_t* coff = reinterpret_cast<int32_t*>(smem);
+    int32_t* pvt = coff + nc;
+    __shared__ int32_t s_tail, s_total, s_wsum[LDS_WAVES];
+    const int32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
+    const int32_t nchunk = (nc + WAVE - 1) / WAVE;
     const unsigned long long INF_BITS = 0x7FF0000000000000ull;
+    const int32_t oend = G.optr[nc];
     // Workgroups are dealt round-robin over the 8 XCDs; give the workgroups of
     // one XCD consecutive slots so the partial 512-B SB64 segments each row
     // writes meet in the same L2 before write-back.
     const int32_t gx = gridDim.x;
     const int32_t bx = (gx % 8 == 0) ? (blockIdx.x % 8) * (gx / 8) + blockIdx.x / 8 : blockIdx.x;
+    int32_t* child = sc_.child + (size_t)blockIdx.x * nc;
+    TreeItem* Q = sc_.q + (size_t)blockIdx.x * nc;
+    double* Rg = sc_.r + (size_t)blockIdx.x * nc;
+    int32_t* Fg = sc_.f + (size_t)blockIdx.x * nc;
     for (int32_t slot = slot0 + bx; slot < slot1; slot += gx) {
-        const int32_t s = slot_vertex[slot];
+        const int32_t s = slots[slot].t;
+        unsigned long long tph = dbg && tid == 0 ? wall_clock64() : 0, nround = 0, nlev = 0;
+#define LDS_PHASE(i)                                                        \
+    if (dbg && tid == 0) {                                                  \
+        const unsigned long long now = wall_clock64();                      \
+        atomicAdd(&dbg[i], now - tph);                                      \
+        tph = now;                                                          \
+    }
         const int32_t sc = G.core_id[s];
         const int32_t seed = sc >= 0 ? sc : G.anchor_core[s];
         for (int32_t v = tid; v < nc; v += LDS_T) {
             Db[v] = INF_BITS;
-            P[v] = -1;
-            H[v] = 0xFFFF;
+            X[v] = G.optr[v];
         }
         for (int32_t w = tid; w < nw; w += LDS_T) {
             F0[w] = 0;
@@ -874,50 +964,133 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
         }
         __syncthreads();
         if (tid == 0) {
-            if (sc >= 0) {
-                D[sc] = 0.0;
-                H[sc] = 0;
-            } else {   // pruned pendant source: first step fixed (see k_init_state)
-                D[seed] = 0.0 + G.fiw[G.fiptr[s]];
-                P[seed] = -2;
-                H[seed] = 1;
-            }
+            // pruned pendant source: its first step s -> anchor is fixed (see k_init_state)
+            D[seed] = sc >= 0 ? 0.0 : 0.0 + G.fiw[G.fiptr[s]];
             F0[seed >> 5] = 1u << (seed & 31);
         }
         __syncthreads();
-        // 1. push relaxation to the fixpoint
+        LDS_PHASE(0)
+        // 1. push relaxation to the fixpoint.  Each wave collects the marked
+        // vertices of its chunks into a 64-entry list, then spreads their
+        // out-edges over its lanes two windows (128 edges) per global round trip.
         uint32_t* cur = F0;
         uint32_t* nxt = F1;
+        int32_t* wl = reinterpret_cast<int32_t*>(hs) + wave * WAVE;   // argmin scratch is idle here
         for (;;) {
             bool any = false;
-            for (int32_t v = tid; v < nc; v += LDS_T) {
-                if (!((cur[v >> 5] >> (v & 31)) & 1u)) continue;
-                const double dv = D[v];
-                const int32_t o0 = G.optr[v], o1 = G.optr[v + 1];
-                for (int32_t k = o0; k < o1; ++k) {
-                    const int32_t x = G.ocol[k];
-                    const double w = G.undirected ? G.iw[k] : G.iw[G.orev[k]];
-                    const double cand = dv + w;
-                    const unsigned long long cb = (unsigned long long)__double_as_longlong(cand);
-                    const unsigned long long old = atomicMin(&Db[x], cb);
-                    if (cb < old) {
-                        atomicOr(&nxt[x >> 5], 1u << (x & 31));
-                        any = true;
+            int32_t cnt = 0;   // wave-uniform list length
+            auto flush = [&]() {
+                const int32_t v = lane < cnt ? wl[lane] : -1;
+                int32_t k0 = 0, deg = 0;
+                double dv = 0.0;
+                if (v >= 0) {
+                    k0 = X[v];
+                    deg = (v + 1 < nc ? X[v + 1] : oend) - k0;
+                    dv = D[v];
+                }
+                int32_t incl = deg;
+#pragma unroll
+                for (int d = 1; d < WAVE; d <<= 1) {
+                    const int32_t y = __shfl_up(incl, d);
+                    if (lane >= d) incl += y;
+                }
+                const int32_t total = __shfl(incl, WAVE - 1);
+                const int32_t excl = incl - deg;
+                for (int32_t base = 0; base < total; base += 2 * WAVE) {
+                    int32_t x[2];
+                    double cand[2];
+                    bool ok[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int32_t e = base + h * WAVE + lane;
+                        int32_t o = 0;
+#pragma unroll
+                        for (int step = WAVE / 2; step; step >>= 1) {
+                            const int32_t y = __shfl(incl, o + step - 1);
+                            if (y <= e) o += step;
+                        }
+                        const int32_t k = __shfl(k0, o) + e - __shfl(excl, o);
+                        const double du = __shfl(dv, o);
+                        ok[h] = e < total;
+                        x[h] = ok[h] ? G.ocol[k] : 0;
+                        cand[h] = ok[h] ? du + G.ow[k] : 0.0;
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        if (!ok[h]) continue;
+                        const unsigned long long cb = (unsigned long long)__double_as_longlong(cand[h]);
+                        if (cb < atomicMin(&Db[x[h]], cb)) {
+                            atomicOr(&nxt[x[h] >> 5], 1u << (x[h] & 31));
+                            any = true;
+                        }
                     }
                 }
+                cnt = 0;
+            };
+            for (int32_t c = wave; c < nchunk; c += LDS_WAVES) {
+                const int32_t v = c * WAVE + lane;
+                const bool act = v < nc && ((cur[v >> 5] >> (v & 31)) & 1u);
+                const uint64_t m = __ballot(act);
+                if (!m) continue;
+                if ((lane & 31) == 0 && v < nc) cur[v >> 5] = 0;   // consumed (one wave per word)
+                if (cnt + __popcll(m) > WAVE) flush();
+                if (act) wl[cnt + __popcll(m & ((1ull << lane) - 1ull))] = v;
+                cnt += __popcll(m);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
-            __syncthreads();
-            for (int32_t w = tid; w < nw; w += LDS_T) cur[w] = 0;
+            if (cnt) flush();
+            ++nround;
             if (!__syncthreads_or(any)) break;
             uint32_t* tmp = cur;
             cur = nxt;
             nxt = tmp;
         }
-        // 2. canonical parents (the source and a pendant seed keep theirs)
-        for (int32_t v = tid; v < nc; v += LDS_T) {
-            if (v == sc || P[v] == -2) continue;
+        LDS_PHASE(1)
+        // 2. canonical parents: X[v] = in-CSR entry, -1 none (source), -2 pendant seed.
+        // One flat pass over the in-CSR registers every valid candidate
+        // (fl(d[u] + w) == d[v] > d[u]); a vertex with exactly one takes it, a
+        // vertex with several (exact ties) rescans its in-list for argmin (d[u], u).
+        for (int32_t v = tid; v < nc; v += LDS_T) X[v] = (v == seed) ? (sc >= 0 ? -1 : -2) : -1;
+        for (int32_t w = tid; w < nw; w += LDS_T) {
+            F0[w] = 0;   // has a candidate
+            F1[w] = 0;   // has several
+        }
+        __syncthreads();
+        {
+            const int32_t m_rel = G.iptr[nc];
+            constexpr int U = 4;
+            for (int32_t e0 = tid; e0 < m_rel; e0 += U * LDS_T) {
+                int32_t u[U], v[U];
+                double w[U];
+#pragma unroll
+                for (int q = 0; q < U; ++q) {
+                    const int32_t e = e0 + q * LDS_T;
+                    u[q] = -1;
+                    if (e < m_rel) {
+                        u[q] = G.icol[e];
+                        v[q] = G.irow[e];
+                        w[q] = G.iw[e];
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < U; ++q) {
+                    if (u[q] < 0 || v[q] == seed) continue;
+                    const double du = D[u[q]], dv = D[v[q]];
+                    const double alt = du + w[q];
+                    if (du < INF && alt == dv && alt > du) {
+                        const uint32_t bit = 1u << (v[q] & 31);
+                        if (atomicOr(&F0[v[q] >> 5], bit) & bit) atomicOr(&F1[v[q] >> 5], bit);
+                        else X[v[q]] = e0 + q * LDS_T;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        for (int32_t v = tid; v < nc; v += LDS_T) {   // exact ties: canonical argmin (d[u], u)
+            if (!((F1[v >> 5] >> (v & 31)) & 1u)) continue;
             const double dv = D[v];
-            if (Db[v] == INF_BITS) continue;
             double bdu = INF;
             int32_t bu = -1, bk = -1;
             for (int32_t k = G.iptr[v]; k < G.iptr[v + 1]; ++k) {
@@ -931,31 +1104,136 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                     bk = k;
                 }
             }
-            P[v] = bk;
+            X[v] = bk;
         }
         __syncthreads();
-        // 3a. hops by level sweeps over the parent tree
-        for (int32_t lev = (sc >= 0 ? 1 : 2);; ++lev) {
-            bool any = false;
-            for (int32_t v = tid; v < nc; v += LDS_T) {
-                const int32_t k = P[v];
-                if (k < 0 || H[v] != 0xFFFF) continue;
-                if (H[par_vertex(G, k)] == lev - 1) {
-                    H[v] = (uint16_t)lev;
-                    any = true;
-                }
-            }
-            if (!__syncthreads_or(any)) break;
-        }
-        // 4a. latency (+ hops) of every target; slow path re-folds along the tree
-        const int32_t sb_local = slot / WAVE - blk0, lane = slot % WAVE;
-        const double fs = G.vfac[s];
+        LDS_PHASE(2)
+        // 3. latencies (distances are final); unreachable targets complete here
+        const int32_t sb_local = slot / WAVE - blk0, lane_s = slot % WAVE;
         for (int32_t j = tid; j < tb.A; j += LDS_T) {
-            const int32_t t = slot_vertex[j];
-            const size_t o = tidx(sb_local, tb.A, j, lane);
-            double Lt = -1.0, R = -1.0;
-            int32_t N = -1, Hh = 0;
+            const SlotInfo si = slots[j];
+            if (si.t == s) continue;
+            const size_t o = tidx(sb_local, tb.A, j, lane_s);
+            if (Db[si.c] == INF_BITS) {
+                tb.lat[o] = -1.0;
+                tb.rel[o] = -1.0;
+                tb.next[o] = -1;
+                tb.hops[o] = 0;
+                if (tb.prev) tb.prev[o] = -1;
+            } else if (!md.multi_rep) {
+                double l = si.kt >= 0 ? D[si.c] + si.pw : D[si.c];
+                if (l == 0) l = 1;   // shd-topology.c:1833-1837
+                tb.lat[o] = l;
+            }
+        }
+        __syncthreads();
+        LDS_PHASE(3)
+        // 4a. child lists of the parent tree: coff[u] = first child slot of u
+        for (int32_t v = tid; v < nc; v += LDS_T) {
+            coff[v] = 0;
+            H[v] = 0xFFFF;
+        }
+        __syncthreads();
+        for (int32_t v = tid; v < nc; v += LDS_T) {
+            const int32_t k = X[v];
+            const int32_t p = k >= 0 ? par_vertex(G, k) : -1;
+            pvt[v] = p;
+            if (p >= 0) atomicAdd(&coff[p], 1);
+        }
+        __syncthreads();
+        {   // inclusive scan of the child counts (thread = contiguous segment)
+            const int32_t per = (nc + LDS_T - 1) / LDS_T;
+            const int32_t b0 = min(nc, tid * per), b1 = min(nc, b0 + per);
+            int32_t sum = 0;
+            for (int32_t i = b0; i < b1; ++i) sum += coff[i];
+            int32_t incl = sum;
+#pragma unroll
+            for (int d = 1; d < WAVE; d <<= 1) {
+                const int32_t y = __shfl_up(incl, d);
+                if (lane >= d) incl += y;
+            }
+            if (lane == WAVE - 1) s_wsum[wave] = incl;
+            __syncthreads();
+            int32_t wbase = 0;
+            for (int32_t q = 0; q < wave; ++q) wbase += s_wsum[q];
+            int32_t run = wbase + incl - sum;
+            for (int32_t i = b0; i < b1; ++i) {
+                run += coff[i];
+                coff[i] = run;
+            }
+            if (tid == LDS_T - 1) s_total = run;
+        }
+        __syncthreads();
+        for (int32_t v = tid; v < nc; v += LDS_T) {
+            const int32_t p = pvt[v];
+            if (p >= 0) child[atomicSub(&coff[p], 1) - 1] = v;
+        }
+        if (tid == 0) {
+            const double fs = G.vfac[s];
+            const double r0 = has_attr(fs) ? 1.0 * fs : 1.0;   // shd-topology.c:1428-1430
+            TreeItem it;
+            it.v = seed;
+            it.f = sc >= 0 ? -1 : G.corev[seed];
+            it.r = sc >= 0 ? r0 : r0 * G.fia[G.fiptr[s]];
+            Q[0] = it;
+            Rg[seed] = it.r;
+            Fg[seed] = it.f;
+            H[seed] = sc >= 0 ? 0 : 1;
+            s_tail = 1;
+        }
+        __syncthreads();
+        LDS_PHASE(4)
+        // 4b. top-down over the tree, one hop level per step
+        {
+            const int32_t total = s_total;
+            int32_t lb = 0, le = 1;
+            uint16_t hl = sc >= 0 ? 1 : 2;   // hop count of the next level
+            while (lb < le) {
+                for (int32_t i0 = lb + wave * WAVE; i0 < le; i0 += LDS_T) {
+                    const int32_t i = i0 + lane;
+                    int32_t u = -1, fu = -1, cs = 0, cn = 0;
+                    double ru = 0.0;
+                    if (i < le) {
+                        const TreeItem it = Q[i];
+                        u = it.v;
+                        fu = it.f;
+                        ru = it.r;
+                        cs = coff[u];
+                        cn = (u + 1 < nc ? coff[u + 1] : total) - cs;
+                    }
+                    wave_expand(lane, cn, [&](bool ok, int32_t o, int32_t off, int32_t, int32_t, int32_t) {
+                        const int32_t uo = __shfl(u, o), fo = __shfl(fu, o), co = __shfl(cs, o);
+                        const double ro = __shfl(ru, o);
+                        TreeItem it;
+                        if (ok) {
+                            it.v = child[co + off];
+                            it.r = ro * G.ia[X[it.v]];
+                            it.f = (uo == sc) ? G.corev[it.v] : fo;
+                            H[it.v] = hl;
+                            Rg[it.v] = it.r;
+                            Fg[it.v] = it.f;
+                        }
+                        const int32_t pos = wave_append(ok, lane, &s_tail);
+                        if (ok) Q[pos] = it;
+                    });
+                }
+                ++nlev;
+                __syncthreads();
+                lb = le;
+                le = s_tail;
+                ++hl;
+                __syncthreads();
+            }
+        }
+        LDS_PHASE(5)
+        // 5. reliability, next hop, hops (+ latency re-fold for multigraphs)
+        for (int32_t j = tid; j < tb.A; j += LDS_T) {
+            const SlotInfo si = slots[j];
+            const int32_t t = si.t;
+            const size_t o = tidx(sb_local, tb.A, j, lane_s);
             if (t == s) {
+                double Lt = -1.0, R = -1.0;
+                int32_t N = -1, Hh = 0;
                 self_entry(G, md, s, Lt, R, N, Hh);
                 tb.lat[o] = Lt;
                 tb.rel[o] = R;
@@ -964,70 +1242,16 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                 if (tb.prev) tb.prev[o] = (Hh == 2) ? N : (Hh > 0 ? s : -1);
                 continue;
             }
-            const int32_t tc = G.core_id[t];
-            const int32_t c = tc >= 0 ? tc : G.anchor_core[t];
-            const int32_t kt = tc >= 0 ? -1 : G.fiptr[t];
-            if (Db[c] != INF_BITS) {
-                Hh = H[c] + (kt >= 0 ? 1 : 0);
-                const double ft = G.vfac[t];
-                const bool fast = (!has_attr(ft) || ft == 1.0) && !md.multi_rep;
-                if (fast) {
-                    Lt = kt >= 0 ? D[c] + G.fiw[kt] : D[c];
-                } else {   // path-order re-fold (vertex loss on t / multigraph get_eid latencies)
-                    double l = 0.0;
-                    for (int32_t i = 1; i <= Hh; ++i) {
-                        int32_t back = Hh - i;
-                        double ew;
-                        if (kt >= 0 && back == 0) {
-                            ew = G.fiwrep[kt];
-                        } else {
-                            int32_t x = c;
-                            if (kt >= 0) back -= 1;
-                            for (int32_t q = 0; q < back; ++q) x = par_vertex(G, P[x]);
-                            ew = P[x] >= 0 ? G.iwrep[P[x]] : G.fiwrep[G.fiptr[s]];
-                        }
-                        l += ew;
-                    }
-                    Lt = l;
-                }
-                if (Lt == 0) Lt = 1;   // shd-topology.c:1833-1837
-                if (tb.prev) tb.prev[o] = kt >= 0 ? G.corev[c] : (P[c] >= 0 ? G.corev[par_vertex(G, P[c])] : s);
-            }
-            tb.lat[o] = Lt;
-            tb.hops[o] = (uint16_t)Hh;
-        }
-        __syncthreads();
-        // 3b. reliability fold by hop level, in D's space (D is no longer needed)
-        double* Rr = D;
-        const double r0 = has_attr(fs) ? 1.0 * fs : 1.0;   // shd-topology.c:1428-1430
-        for (int32_t v = tid; v < nc; v += LDS_T) {
-            if (v == sc) Rr[v] = r0;
-            else if (P[v] == -2) Rr[v] = r0 * G.fia[G.fiptr[s]];
-        }
-        __syncthreads();
-        for (int32_t lev = (sc >= 0 ? 1 : 2);; ++lev) {
-            bool any = false;
-            for (int32_t v = tid; v < nc; v += LDS_T) {
-                if (H[v] != lev || P[v] < 0) continue;
-                Rr[v] = Rr[par_vertex(G, P[v])] * G.ia[P[v]];
-                any = true;
-            }
-            if (!__syncthreads_or(any)) break;
-        }
-        for (int32_t j = tid; j < tb.A; j += LDS_T) {
-            const int32_t t = slot_vertex[j];
-            if (t == s) continue;
-            const int32_t tc = G.core_id[t];
-            const int32_t c = tc >= 0 ? tc : G.anchor_core[t];
-            const int32_t kt = tc >= 0 ? -1 : G.fiptr[t];
-            if (H[c] == 0xFFFF) continue;   // unreachable (lat already -1)
-            const size_t o = tidx(sb_local, tb.A, j, lane);
+            const int32_t c = si.c, kt = si.kt;
+            const uint16_t hc = H[c];
+            if (hc == 0xFFFF) continue;   // unreachable: written in pass 3
+            const int32_t Hh = hc + (kt >= 0 ? 1 : 0);
             const double ft = G.vfac[t];
             double R;
             if (!has_attr(ft) || ft == 1.0) {
-                R = kt >= 0 ? Rr[c] * G.fia[kt] : Rr[c];
+                R = Rg[c] * si.pa;   // pa = 1.0 for relaxation vertices (exact)
             } else {   // ((1 * fs) * ft) * a1 * a2 ... : the target factor comes second
-                const int32_t Hh = H[c] + (kt >= 0 ? 1 : 0);
+                const double fs = G.vfac[s];
                 double r = 1.0;
                 if (has_attr(fs)) r *= fs;
                 r *= ft;
@@ -1035,52 +1259,49 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                     int32_t back = Hh - i;
                     double ea;
                     if (kt >= 0 && back == 0) {
-                        ea = G.fia[kt];
+                        ea = si.pa;
                     } else {
                         int32_t x = c;
                         if (kt >= 0) back -= 1;
-                        for (int32_t q = 0; q < back; ++q) x = par_vertex(G, P[x]);
-                        ea = P[x] >= 0 ? G.ia[P[x]] : G.fia[G.fiptr[s]];
+                        for (int32_t q = 0; q < back; ++q) x = par_vertex(G, X[x]);
+                        ea = X[x] >= 0 ? G.ia[X[x]] : G.fia[G.fiptr[s]];
                     }
                     r *= ea;
                 }
                 R = r;
             }
+            if (md.multi_rep) {   // path-order re-fold of the get_eid latencies
+                double l = 0.0;
+                for (int32_t i = 1; i <= Hh; ++i) {
+                    int32_t back = Hh - i;
+                    double ew;
+                    if (kt >= 0 && back == 0) {
+                        ew = G.fiwrep[kt];
+                    } else {
+                        int32_t x = c;
+                        if (kt >= 0) back -= 1;
+                        for (int32_t q = 0; q < back; ++q) x = par_vertex(G, X[x]);
+                        ew = X[x] >= 0 ? G.iwrep[X[x]] : G.fiwrep[G.fiptr[s]];
+                    }
+                    l += ew;
+                }
+                if (l == 0) l = 1;
+                tb.lat[o] = l;
+            }
             tb.rel[o] = R;
+            tb.next[o] = kt >= 0 && hc == 0 ? t : Fg[c];
+            tb.hops[o] = (uint16_t)Hh;
+            if (tb.prev) tb.prev[o] = kt >= 0 ? G.corev[c] : (X[c] >= 0 ? G.corev[par_vertex(G, X[c])] : s);
         }
         __syncthreads();
-        // 3c. first hop by hop level (original ids), in the same space
-        int32_t* Fh = reinterpret_cast<int32_t*>(D);
-        for (int32_t v = tid; v < nc; v += LDS_T) {
-            if (P[v] == -2) Fh[v] = G.corev[v];
+        LDS_PHASE(6)
+        if (dbg && tid == 0) {
+            atomicAdd(&dbg[8], nround);
+            atomicAdd(&dbg[9], nlev);
+            atomicAdd(&dbg[10], 1ull);
         }
-        __syncthreads();
-        for (int32_t lev = (sc >= 0 ? 1 : 2);; ++lev) {
-            bool any = false;
-            for (int32_t v = tid; v < nc; v += LDS_T) {
-                if (H[v] != lev || P[v] < 0) continue;
-                const int32_t u = par_vertex(G, P[v]);
-                Fh[v] = (u == sc) ? G.corev[v] : Fh[u];
-                any = true;
-            }
-            if (!__syncthreads_or(any)) break;
-        }
-        for (int32_t j = tid; j < tb.A; j += LDS_T) {
-            const int32_t t = slot_vertex[j];
-            if (t == s) continue;
-            const int32_t tc = G.core_id[t];
-            const int32_t c = tc >= 0 ? tc : G.anchor_core[t];
-            const size_t o = tidx(sb_local, tb.A, j, lane);
-            int32_t N = -1;
-            if (H[c] != 0xFFFF) N = tc >= 0 ? Fh[c] : (H[c] == 0 ? t : Fh[c]);
-            tb.next[o] = N;
-            if (N < 0) {
-                tb.rel[o] = -1.0;
-                if (tb.prev) tb.prev[o] = -1;
-            }
-        }
-        __syncthreads();
     }
+#undef LDS_PHASE
 }
 
 // Owner replay (compat with the reference's first-writer-wins path cache,
@@ -1195,12 +1416,16 @@ struct spe_table {
     int32_t engine = SPE_ENGINE_BATCH;   // resolved engine
     int32_t infl = 8;              // neighbour rows in flight per subgroup (4 or 8)
     bool trace = getenv("SPE_TRACE") != nullptr;   // diagnostic: per-launch times to stderr
+    unsigned long long* d_lds_dbg = nullptr;       // diagnostic (SPE_LDS_DEBUG): LDS engine phase clocks
     int32_t occ = 0;               // diagnostic: forced waves/SIMD of k_relax (0 = compiler's choice)
     RowMode md{};
     bool ext = false;
     bool built = false;
     Table tb{};
     int32_t* d_slot_vertex = nullptr;
+    SlotInfo* d_slots = nullptr;   // LDS engine: per-target constants
+    LdsScratch lsc{};              // LDS engine: per-workgroup tree scratch
+    int32_t lds_grid = 0;          // LDS engine: workgroups per launch (scratch is sized for it)
     int32_t* d_rank = nullptr;     // owner replay: position of each slot in the source-run order
     int32_t* d_vertex_slot = nullptr;
     std::vector<int32_t> attached;
@@ -1323,6 +1548,16 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
     } while (0)
     UP(iptr, h.iptr);
     UP(icol, h.icol);
+    {
+        std::vector<int32_t> irow(h.icol.size());
+        for (int32_t v = 0; v < h.nc; ++v)
+            for (int32_t k = h.iptr[v]; k < h.iptr[v + 1]; ++k) irow[k] = v;
+        r = dev_upload(g->allocs, irow, &d.irow);
+        if (r) {
+            spe_graph_free(g);
+            return r;
+        }
+    }
     UP(iw, h.iw);
     UP(ia, h.ia);
     UP(iwrep, h.iwrep);
@@ -1332,12 +1567,14 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
         UP(ocol, h.ocol);
         UP(owrep, h.owrep);
         UP(oarep, h.oarep);
+        UP(ow, h.ow);
         d.undirected = 0;
     } else {
         d.optr = d.iptr;
         d.ocol = d.icol;
         d.owrep = d.iwrep;
         d.oarep = d.ia;
+        d.ow = d.iw;
         d.undirected = 1;
     }
     UP(vfac, h.vfac);
@@ -1562,6 +1799,39 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     t->d_slot_vertex = const_cast<int32_t*>(tmp);
     TRY(dev_upload(t->allocs, vslot, &tmp));
     t->d_vertex_slot = const_cast<int32_t*>(tmp);
+    if (!t->md.complete && t->engine == SPE_ENGINE_LDS) {
+        const spe::HostGraph& h = g->hg;
+        std::vector<SlotInfo> si(n_attached);
+        for (int32_t j = 0; j < n_attached; ++j) {
+            const int32_t v = attached[j];
+            SlotInfo& x = si[j];
+            x.t = v;
+            x.pad = 0;
+            if (h.core_id[v] >= 0) {
+                x.c = h.core_id[v];
+                x.kt = -1;
+                x.pw = 0.0;
+                x.pa = 1.0;
+            } else {
+                x.c = h.anchor_core[v];
+                x.kt = h.fiptr[v];
+                x.pw = h.fiw[x.kt];
+                x.pa = h.fia[x.kt];
+            }
+        }
+        const SlotInfo* tsi = nullptr;
+        TRY(dev_upload(t->allocs, si, &tsi));
+        t->d_slots = const_cast<SlotInfo*>(tsi);
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device);
+        const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, LDS_MAX_BYTES / lds_bytes(h.nc)));
+        t->lds_grid = cus * per_cu;
+        const size_t per = (size_t)t->lds_grid * std::max(1, h.nc);
+        TRY(dev_alloc(t->allocs, &t->lsc.child, per));
+        TRY(dev_alloc(t->allocs, &t->lsc.q, per));
+        TRY(dev_alloc(t->allocs, &t->lsc.r, per));
+        TRY(dev_alloc(t->allocs, &t->lsc.f, per));
+    }
     const size_t G = (size_t)t->groups;
     const size_t GL = G * (WAVE / t->lanes);   // lane groups per batch
     if (!t->md.complete && t->engine == SPE_ENGINE_BATCH) {
@@ -1776,13 +2046,24 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
                 LaunchTimer lt(t, s, SPE_K_LDS);
                 const int32_t s0 = b * WAVE, s1 = std::min(t->A, (b + groups) * WAVE);
                 const size_t bytes = lds_bytes(g->hg.nc);
-                int cus = 256;
-                (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device);
-                const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, LDS_MAX_BYTES / bytes));
-                int grid = std::min(s1 - s0, cus * per_cu);
+                int grid = std::min(s1 - s0, t->lds_grid);
                 if (grid >= 8) grid -= grid % 8;   // whole XCD rounds (see k_sssp_lds's slot order)
-                k_sssp_lds<<<std::max(1, grid), LDS_T, bytes, s>>>(s0, s1, t->d_slot_vertex, t->blk0, g->dev, t->md,
-                                                                   t->tb);
+                if (getenv("SPE_LDS_DEBUG") && !t->d_lds_dbg) {
+                    if (int r = dev_alloc(t->allocs, &t->d_lds_dbg, 16)) return r;
+                    HIP_TRY(hipMemset(t->d_lds_dbg, 0, 16 * sizeof(unsigned long long)));
+                }
+                k_sssp_lds<<<std::max(1, grid), LDS_T, bytes, s>>>(s0, s1, t->d_slots, t->blk0, g->dev, t->md, t->tb,
+                                                                   t->lsc, t->d_lds_dbg);
+                if (t->d_lds_dbg) {
+                    unsigned long long h[16];
+                    HIP_TRY(hipStreamSynchronize(s));
+                    HIP_TRY(hipMemcpy(h, t->d_lds_dbg, sizeof(h), hipMemcpyDeviceToHost));
+                    const double nsrc = (double)std::max(1ull, h[10]);
+                    fprintf(stderr, "spe-lds sources %llu rounds/src %.1f levels/src %.1f us/src: init %.1f push %.1f "
+                            "parent %.1f lat %.1f tree-build %.1f tree-pass %.1f rows %.1f\n", h[10], h[8] / nsrc, h[9] / nsrc,
+                            h[0] / nsrc / 100.0, h[1] / nsrc / 100.0, h[2] / nsrc / 100.0, h[3] / nsrc / 100.0,
+                            h[4] / nsrc / 100.0, h[5] / nsrc / 100.0, h[6] / nsrc / 100.0);
+                }
             }
             if (t->md.prefer) {
                 LaunchTimer lt(t, s, SPE_K_DIRECT);

@@ -140,11 +140,13 @@ int prepare_graph(const spe_graph_desc* d, HostGraph* hg, std::string* err) {
         hg->ocol.resize(idx.size());
         hg->orev.resize(idx.size());
         hg->owrep.resize(idx.size());
+        hg->ow.resize(idx.size());
         hg->oarep.resize(idx.size());
         for (size_t i = 0; i < idx.size(); ++i) {
             hg->ocol[i] = to_of[idx[i]];
             hg->orev[i] = (int32_t)idx[i];
             hg->owrep[i] = hg->iwrep[idx[i]];
+            hg->ow[i] = hg->iw[idx[i]];
             hg->oarep[i] = hg->ia[idx[i]];
             hg->optr[hg->icol[idx[i]] + 1]++;
         }

@@ -40,7 +40,7 @@ struct HostGraph {
     // out-CSR (directed only; undirected graphs reuse the in-CSR)
     std::vector<int32_t> optr, ocol;
     std::vector<int32_t> orev;     // out entry -> in-CSR index of the same (merged) edge
-    std::vector<double> owrep, oarep;
+    std::vector<double> owrep, oarep, ow;
     // per vertex
     std::vector<double> vfac;      // 1 - vertex loss, NaN when absent
     std::vector<int64_t> loop_eid;
