@@ -842,7 +842,8 @@ __global__ __launch_bounds__(BLOCK) void k_direct_overlay(int32_t groups, int32_
 constexpr int LDS_T = 1024;                 // threads per workgroup (16 waves)
 constexpr int LDS_WAVES = LDS_T / WAVE;
 constexpr int LDS_MAX_BYTES = 160 * 1024 - 1024;   // dynamic share; the rest covers static __shared__
-constexpr int LDS_CAND_BYTES = LDS_WAVES * WAVE * 16;   // per-wave argmin scratch of the parent pass
+constexpr int LDS_WL = 256;                 // per-wave marked-vertex list of the push pass
+constexpr int LDS_CAND_BYTES = LDS_WAVES * (LDS_WL * 4 + 2 * WAVE);   // push lists + owner maps (H space)
 
 __host__ __device__ constexpr size_t lds_align(size_t b) { return (b + 15) & ~(size_t)15; }
 // D f64 | X i32 (out-row starts, then parent entry) | H u16 / argmin scratch | 2 bitsets
@@ -872,6 +873,7 @@ struct alignas(16) TreeItem {
 };
 struct LdsScratch {
     int32_t* child;     // [grid][nc]
+    double* cia;        // [grid][nc] 1 - p of each child's parent edge, aligned with child
     TreeItem* q;        // [grid][nc] vertices in hop-level order
     double* r;          // [grid][nc]
     int32_t* f;         // [grid][nc]
@@ -940,6 +942,7 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
     const int32_t gx = gridDim.x;
     const int32_t bx = (gx % 8 == 0) ? (blockIdx.x % 8) * (gx / 8) + blockIdx.x / 8 : blockIdx.x;
     int32_t* child = sc_.child + (size_t)blockIdx.x * nc;
+    double* cia = sc_.cia + (size_t)blockIdx.x * nc;
     TreeItem* Q = sc_.q + (size_t)blockIdx.x * nc;
     double* Rg = sc_.r + (size_t)blockIdx.x * nc;
     int32_t* Fg = sc_.f + (size_t)blockIdx.x * nc;
@@ -970,17 +973,22 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
         }
         __syncthreads();
         LDS_PHASE(0)
-        // 1. push relaxation to the fixpoint.  Each wave collects the marked
-        // vertices of its chunks into a 64-entry list, then spreads their
-        // out-edges over its lanes two windows (128 edges) per global round trip.
+        // 1. push relaxation to the fixpoint.  Each wave reads 64 bitset words at
+        // once (words wave, wave+16, ...), lists their marked vertices (up to
+        // 256), then spreads the listed vertices' out-edges over its lanes, two
+        // 64-edge windows per global round trip.
         uint32_t* cur = F0;
         uint32_t* nxt = F1;
-        int32_t* wl = reinterpret_cast<int32_t*>(hs) + wave * WAVE;   // argmin scratch is idle here
+        int32_t* wl = reinterpret_cast<int32_t*>(hs) + wave * LDS_WL;   // H space is idle here
+        uint8_t* om = hs + LDS_WAVES * LDS_WL * 4 + wave * 2 * WAVE;
         for (;;) {
             bool any = false;
             int32_t cnt = 0;   // wave-uniform list length
+            unsigned long long tfl = 0;
             auto flush = [&]() {
-                const int32_t v = lane < cnt ? wl[lane] : -1;
+                const unsigned long long tf0 = (dbg && tid == 0) ? wall_clock64() : 0;
+                for (int32_t lb = 0; lb < cnt; lb += WAVE) {
+                const int32_t v = lb + lane < cnt ? wl[lb + lane] : -1;
                 int32_t k0 = 0, deg = 0;
                 double dv = 0.0;
                 if (v >= 0) {
@@ -1000,15 +1008,16 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                     int32_t x[2];
                     double cand[2];
                     bool ok[2];
+                    // owner map of this 128-edge window: each lane stamps its own edges
+                    for (int32_t i = max(excl, base), ie = min(incl, base + 2 * WAVE); i < ie; ++i)
+                        om[i - base] = (uint8_t)lane;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const int32_t e = base + h * WAVE + lane;
-                        int32_t o = 0;
-#pragma unroll
-                        for (int step = WAVE / 2; step; step >>= 1) {
-                            const int32_t y = __shfl(incl, o + step - 1);
-                            if (y <= e) o += step;
-                        }
+                        const int32_t o = e < total ? om[e - base] : 0;
                         const int32_t k = __shfl(k0, o) + e - __shfl(excl, o);
                         const double du = __shfl(dv, o);
                         ok[h] = e < total;
@@ -1024,25 +1033,54 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                             any = true;
                         }
                     }
+                    __builtin_amdgcn_wave_barrier();   // owner map reads done before the next stamps
+                }
                 }
                 cnt = 0;
+                if (dbg && tid == 0) tfl += wall_clock64() - tf0;
             };
-            for (int32_t c = wave; c < nchunk; c += LDS_WAVES) {
-                const int32_t v = c * WAVE + lane;
-                const bool act = v < nc && ((cur[v >> 5] >> (v & 31)) & 1u);
-                const uint64_t m = __ballot(act);
-                if (!m) continue;
-                if ((lane & 31) == 0 && v < nc) cur[v >> 5] = 0;   // consumed (one wave per word)
-                if (cnt + __popcll(m) > WAVE) flush();
-                if (act) wl[cnt + __popcll(m & ((1ull << lane) - 1ull))] = v;
-                cnt += __popcll(m);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int32_t w0 = wave; w0 < nw; w0 += LDS_WAVES * WAVE) {
+                const int32_t wi = w0 + lane * LDS_WAVES;
+                uint32_t W = wi < nw ? cur[wi] : 0u;
+                uint64_t pend = __ballot(W != 0);
+                if (!pend) continue;
+                if (W) cur[wi] = 0;   // consumed (each word belongs to one wave)
+                while (pend) {
+                    const bool mine = (pend >> lane) & 1ull;
+                    const int32_t c = mine ? __popc(W) : 0;
+                    int32_t incl = c;
+#pragma unroll
+                    for (int d = 1; d < WAVE; d <<= 1) {
+                        const int32_t y = __shfl_up(incl, d);
+                        if (lane >= d) incl += y;
+                    }
+                    const bool fit = mine && incl <= LDS_WL - cnt;   // a prefix of the pending lanes
+                    const uint64_t fm = __ballot(fit);
+                    if (!fm) {   // list full: process it, then retry
+                        flush();
+                        continue;
+                    }
+                    if (fit) {
+                        int32_t pos = cnt + incl - c;
+                        for (uint32_t x = W; x; x &= x - 1) wl[pos++] = wi * 32 + __builtin_ctz(x);
+                    }
+                    cnt += __shfl(incl, 63 - __builtin_clzll(fm));
+                    pend &= ~fm;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (pend) flush();
+                }
             }
             if (cnt) flush();
             ++nround;
-            if (!__syncthreads_or(any)) break;
+            const unsigned long long tb0 = (dbg && tid == 0) ? wall_clock64() : 0;
+            const bool more = __syncthreads_or(any);
+            if (dbg && tid == 0) {
+                atomicAdd(&dbg[11], tfl);
+                atomicAdd(&dbg[12], wall_clock64() - tb0);
+            }
+            if (!more) break;
             uint32_t* tmp = cur;
             cur = nxt;
             nxt = tmp;
@@ -1134,11 +1172,21 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
             H[v] = 0xFFFF;
         }
         __syncthreads();
-        for (int32_t v = tid; v < nc; v += LDS_T) {
-            const int32_t k = X[v];
-            const int32_t p = k >= 0 ? par_vertex(G, k) : -1;
-            pvt[v] = p;
-            if (p >= 0) atomicAdd(&coff[p], 1);
+        for (int32_t v0 = tid; v0 < nc; v0 += 4 * LDS_T) {   // 4 vertices' loads in flight
+            int32_t p[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int32_t v = v0 + q * LDS_T;
+                const int32_t k = v < nc ? X[v] : -1;
+                p[q] = k >= 0 ? par_vertex(G, k) : -1;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int32_t v = v0 + q * LDS_T;
+                if (v >= nc) continue;
+                pvt[v] = p[q];
+                if (p[q] >= 0) atomicAdd(&coff[p[q]], 1);
+            }
         }
         __syncthreads();
         {   // inclusive scan of the child counts (thread = contiguous segment)
@@ -1164,9 +1212,22 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
             if (tid == LDS_T - 1) s_total = run;
         }
         __syncthreads();
-        for (int32_t v = tid; v < nc; v += LDS_T) {
-            const int32_t p = pvt[v];
-            if (p >= 0) child[atomicSub(&coff[p], 1) - 1] = v;
+        for (int32_t v0 = tid; v0 < nc; v0 += 4 * LDS_T) {
+            int32_t p[4];
+            double a[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int32_t v = v0 + q * LDS_T;
+                p[q] = v < nc ? pvt[v] : -1;
+                a[q] = p[q] >= 0 ? G.ia[X[v]] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (p[q] < 0) continue;
+                const int32_t pos = atomicSub(&coff[p[q]], 1) - 1;
+                child[pos] = v0 + q * LDS_T;
+                cia[pos] = a[q];
+            }
         }
         if (tid == 0) {
             const double fs = G.vfac[s];
@@ -1207,7 +1268,7 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                         TreeItem it;
                         if (ok) {
                             it.v = child[co + off];
-                            it.r = ro * G.ia[X[it.v]];
+                            it.r = ro * cia[co + off];
                             it.f = (uo == sc) ? G.corev[it.v] : fo;
                             H[it.v] = hl;
                             Rg[it.v] = it.r;
@@ -1828,6 +1889,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         t->lds_grid = cus * per_cu;
         const size_t per = (size_t)t->lds_grid * std::max(1, h.nc);
         TRY(dev_alloc(t->allocs, &t->lsc.child, per));
+        TRY(dev_alloc(t->allocs, &t->lsc.cia, per));
         TRY(dev_alloc(t->allocs, &t->lsc.q, per));
         TRY(dev_alloc(t->allocs, &t->lsc.r, per));
         TRY(dev_alloc(t->allocs, &t->lsc.f, per));
@@ -2060,9 +2122,10 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
                     HIP_TRY(hipMemcpy(h, t->d_lds_dbg, sizeof(h), hipMemcpyDeviceToHost));
                     const double nsrc = (double)std::max(1ull, h[10]);
                     fprintf(stderr, "spe-lds sources %llu rounds/src %.1f levels/src %.1f us/src: init %.1f push %.1f "
-                            "parent %.1f lat %.1f tree-build %.1f tree-pass %.1f rows %.1f\n", h[10], h[8] / nsrc, h[9] / nsrc,
+                            "parent %.1f lat %.1f tree-build %.1f tree-pass %.1f rows %.1f | push: wave0 flush %.1f barrier %.1f\n", h[10], h[8] / nsrc, h[9] / nsrc,
                             h[0] / nsrc / 100.0, h[1] / nsrc / 100.0, h[2] / nsrc / 100.0, h[3] / nsrc / 100.0,
-                            h[4] / nsrc / 100.0, h[5] / nsrc / 100.0, h[6] / nsrc / 100.0);
+                            h[4] / nsrc / 100.0, h[5] / nsrc / 100.0, h[6] / nsrc / 100.0, h[11] / nsrc / 100.0,
+                            h[12] / nsrc / 100.0);
                 }
             }
             if (t->md.prefer) {
