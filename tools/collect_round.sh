@@ -1,0 +1,12 @@
+# copy the judged artefacts of a tools/gpu_round.sh run into profiles/
+set -e
+R=${ROUND:-r01}
+O=gpurun_out/$R
+for C in c3 c2 c5; do
+  cp $O/bench_$C.log profiles/${R}_bench_$C.log
+  f=$(find $O/kt_$C -name '*kernel_stats.csv' | head -1)
+  [ -n "$f" ] && cp "$f" profiles/${R}_rocprof_kernel_stats_$C.csv
+done
+cp $O/pytest_gpu.log profiles/${R}_pytest_gpu.log
+cp $O/smoke.log profiles/${R}_smoke.log
+ls -la profiles
