@@ -147,7 +147,7 @@ def bench_full_table(args, rank, world, local, dist):
     """Whole path-table precompute (BASELINE north star: C4 on 8 GPUs in < 10 s).
     Rank r owns the contiguous source-block range r of `shares` (= world, or more to
     emulate one rank of a larger job on fewer GPUs); with --gather and world > 1 the
-    latency and reliability fields are then all-gathered over RCCL into a full
+    latency/reliability records are then all-gathered over RCCL into a full
     replicated table on every GPU (one contiguous SB64 span per rank)."""
     import torch
     from shadow_amd import spe
@@ -162,7 +162,7 @@ def bench_full_table(args, rank, world, local, dist):
     b0, b1 = min(nblk, share * cb), min(nblk, (share + 1) * cb)
     elems = cb * A * 64
     dev = torch.device("cuda", local)
-    bufs = [torch.empty(elems, dtype=torch.float64, device=dev), torch.empty(elems, dtype=torch.float64, device=dev),
+    bufs = [torch.empty((elems, 2), dtype=torch.float64, device=dev),   # {latency, reliability}
             torch.empty(elems, dtype=torch.int32, device=dev), torch.empty(elems, dtype=torch.int16, device=dev)]
     t = None
     if b1 > b0:   # (a rank past the last block owns nothing but still joins the gather)
@@ -182,13 +182,11 @@ def bench_full_table(args, rank, world, local, dist):
     t_all = time.perf_counter() - t0
     gather = None
     if args.gather and dist is not None:
-        full_lat = torch.empty(world * elems, dtype=torch.float64, device=dev)
-        full_rel = torch.empty(world * elems, dtype=torch.float64, device=dev)
+        full_lr = torch.empty((world * elems, 2), dtype=torch.float64, device=dev)
         torch.cuda.synchronize(dev)
         dist.barrier()
         tg = time.perf_counter()
-        dist.all_gather_into_tensor(full_lat, bufs[0])
-        dist.all_gather_into_tensor(full_rel, bufs[1])
+        dist.all_gather_into_tensor(full_lr, bufs[0])
         torch.cuda.synchronize(dev)
         dist.barrier()
         t_gather = time.perf_counter() - tg

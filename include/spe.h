@@ -97,10 +97,9 @@ typedef struct spe_table_opts {
     int32_t groups_per_launch;      /* 64-source groups relaxed together; 0 = auto */
     int32_t block_begin;            /* first 64-row source block owned by this table */
     int32_t block_end;              /* one past the last; 0,0 = all blocks */
-    /* optional caller-owned device storage for the owned blocks (all four or none),
+    /* optional caller-owned device storage for the owned blocks (all three or none),
      * each sized (block_end-block_begin) * n_attached * 64 elements */
-    void* ext_latency;              /* double   */
-    void* ext_reliability;          /* double   */
+    void* ext_latrel;               /* double[2] {latency, reliability} */
     void* ext_next_hop;             /* int32_t  */
     void* ext_hops;                 /* uint16_t */
     int32_t ext_filled;             /* 1: the external storage already holds the rows (e.g. an
@@ -121,14 +120,15 @@ typedef struct spe_table_opts {
 /* Where a table keeps its rows.  Element (s_slot, t_slot) of a field lives at
  *   ((s_slot / 64 - block_begin) * n_attached + t_slot) * 64 + s_slot % 64
  * ("SB64": 64 source rows interleaved per target, so one source block is one
- * contiguous span and a 64-source batch writes whole 512-byte segments). */
+ * contiguous span and a 64-source batch writes whole segments).  Latency and
+ * reliability share one 16-byte record (the per-packet lookup reads both:
+ * one HBM line per query instead of two). */
 typedef struct spe_table_layout {
     int32_t n_attached;
     int32_t block_begin;
     int32_t block_end;
     int64_t elems;                  /* per field */
-    void* latency;                  /* device pointers */
-    void* reliability;
+    void* latrel;                   /* device pointers: double[2] {latency, reliability} */
     void* next_hop;
     void* hops;
 } spe_table_layout;

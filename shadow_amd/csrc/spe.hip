@@ -132,8 +132,7 @@ struct State {
 };
 
 struct Table {
-    double* lat;
-    double* rel;
+    double2* lr;      // {latency, reliability}: one 16-B record, so a lookup is one HBM line
     int32_t* next;
     uint16_t* hops;
     int32_t A;
@@ -755,8 +754,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
             }
         }
         const size_t o = tidx(sb0 + b, tb.A, jt, lane);
-        tb.lat[o] = Lt;
-        tb.rel[o] = R;
+        tb.lr[o] = make_double2(Lt, R);
         tb.next[o] = N;
         tb.hops[o] = (uint16_t)(H > 65535 ? 65535 : H);
         if (tb.prev) tb.prev[o] = PV;
@@ -783,8 +781,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_direct(int32_t groups, int32_t s
             else direct_entry(G, s, t, L, R, N, H);
         }
         const size_t o = tidx(sb0 + g, tb.A, j, lane);
-        tb.lat[o] = L;
-        tb.rel[o] = R;
+        tb.lr[o] = make_double2(L, R);
         tb.next[o] = N;
         tb.hops[o] = (uint16_t)H;
         if (tb.prev) tb.prev[o] = (H == 2) ? N : (H > 0 ? s : -1);
@@ -812,8 +809,7 @@ __global__ __launch_bounds__(BLOCK) void k_direct_overlay(int32_t groups, int32_
         if (has_attr(ft)) r *= ft;
         r *= G.darep[k];
         const size_t o = tidx(sb0 + g, tb.A, j, lane);
-        tb.lat[o] = 0.0 + G.dwrep[k];
-        tb.rel[o] = r;
+        tb.lr[o] = make_double2(0.0 + G.dwrep[k], r);
         tb.next[o] = t;
         tb.hops[o] = 1;
         if (tb.prev) tb.prev[o] = s;
@@ -1153,15 +1149,14 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
             if (si.t == s) continue;
             const size_t o = tidx(sb_local, tb.A, j, lane_s);
             if (Db[si.c] == INF_BITS) {
-                tb.lat[o] = -1.0;
-                tb.rel[o] = -1.0;
+                tb.lr[o] = make_double2(-1.0, -1.0);
                 tb.next[o] = -1;
                 tb.hops[o] = 0;
                 if (tb.prev) tb.prev[o] = -1;
             } else if (!md.multi_rep) {
                 double l = si.kt >= 0 ? D[si.c] + si.pw : D[si.c];
                 if (l == 0) l = 1;   // shd-topology.c:1833-1837
-                tb.lat[o] = l;
+                tb.lr[o].x = l;
             }
         }
         __syncthreads();
@@ -1296,8 +1291,7 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                 double Lt = -1.0, R = -1.0;
                 int32_t N = -1, Hh = 0;
                 self_entry(G, md, s, Lt, R, N, Hh);
-                tb.lat[o] = Lt;
-                tb.rel[o] = R;
+                tb.lr[o] = make_double2(Lt, R);
                 tb.next[o] = N;
                 tb.hops[o] = (uint16_t)Hh;
                 if (tb.prev) tb.prev[o] = (Hh == 2) ? N : (Hh > 0 ? s : -1);
@@ -1347,9 +1341,9 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                     l += ew;
                 }
                 if (l == 0) l = 1;
-                tb.lat[o] = l;
+                tb.lr[o].x = l;
             }
-            tb.rel[o] = R;
+            tb.lr[o].y = R;
             tb.next[o] = kt >= 0 && hc == 0 ? t : Fg[c];
             tb.hops[o] = (uint16_t)Hh;
             if (tb.prev) tb.prev[o] = kt >= 0 ? G.corev[c] : (X[c] >= 0 ? G.corev[par_vertex(G, X[c])] : s);
@@ -1404,21 +1398,20 @@ __global__ __launch_bounds__(BLOCK) void k_owner_replay(int32_t A, const int32_t
         const bool i_first = rank[i] < rank[j];
         const size_t of = i_first ? oij : oji, oo = i_first ? oji : oij;
         const bool dfo = i_first ? dij : dji, dof = i_first ? dji : dij;
-        const double lf = tb.lat[of], lo_ = tb.lat[oo];
+        const double2 ef = tb.lr[of], eo = tb.lr[oo];
+        const double lf = ef.x, lo_ = eo.x;
         const bool sf = !dfo && lf > -1.0;                 // first runner stored (f, o)
         const bool so = !dof && lo_ > -1.0 && !sf;         // second stored (o, f)
-        const double rf = tb.rel[of], ro = tb.rel[oo];
+        const double rf = ef.y, ro = eo.y;
         const uint16_t hf = tb.hops[of], ho = tb.hops[oo];
         const int32_t pf = tb.prev[of], po = tb.prev[oo];
         if (!dfo && !sf) {   // (f, o) answers the reverse path or fails
-            tb.lat[of] = so ? lo_ : -1.0;
-            tb.rel[of] = so ? ro : -1.0;
+            tb.lr[of] = make_double2(so ? lo_ : -1.0, so ? ro : -1.0);
             tb.hops[of] = so ? ho : 0;
             tb.next[of] = (so && !md.directed) ? po : -1;
         }
         if (!dof && !so) {   // (o, f)
-            tb.lat[oo] = sf ? lf : -1.0;
-            tb.rel[oo] = sf ? rf : -1.0;
+            tb.lr[oo] = make_double2(sf ? lf : -1.0, sf ? rf : -1.0);
             tb.hops[oo] = sf ? hf : 0;
             tb.next[oo] = (sf && !md.directed) ? pf : -1;
         }
@@ -1434,8 +1427,9 @@ __global__ __launch_bounds__(BLOCK) void k_lookup(const int2* __restrict__ pairs
         double L = -1.0, R = -1.0;
         if (p.x >= 0 && p.y >= 0 && p.y < tb.A && sb >= blk0 && sb < blk1) {
             const size_t o = tidx(sb - blk0, tb.A, p.y, p.x & (WAVE - 1));
-            L = tb.lat[o];
-            R = tb.rel[o];
+            const double2 e = tb.lr[o];
+            L = e.x;
+            R = e.y;
         }
         lat[i] = L;
         rel[i] = R;
@@ -1443,11 +1437,11 @@ __global__ __launch_bounds__(BLOCK) void k_lookup(const int2* __restrict__ pairs
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_min_latency(const double* __restrict__ lat, int64_t elems,
+__global__ __launch_bounds__(BLOCK) void k_min_latency(const double2* __restrict__ lr, int64_t elems,
                                                        unsigned long long* out) {
     double m = INF;
     for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < elems; i += (int64_t)gridDim.x * BLOCK) {
-        const double l = lat[i];
+        const double l = lr[i].x;
         if (l > -1.0 && l < m) m = l;
     }
     for (int off = 32; off > 0; off >>= 1) m = fmin(m, __shfl_xor(m, off));
@@ -1826,20 +1820,18 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
             return r;           \
         }                       \
     } while (0)
-    if (o.ext_latency || o.ext_reliability || o.ext_next_hop || o.ext_hops) {
-        if (!(o.ext_latency && o.ext_reliability && o.ext_next_hop && o.ext_hops)) {
+    if (o.ext_latrel || o.ext_next_hop || o.ext_hops) {
+        if (!(o.ext_latrel && o.ext_next_hop && o.ext_hops)) {
             delete t;
-            return fail(SPE_EINVAL, "external storage needs all four fields");
+            return fail(SPE_EINVAL, "external storage needs all three fields");
         }
         t->ext = true;
         t->built = o.ext_filled != 0;
-        t->tb.lat = (double*)o.ext_latency;
-        t->tb.rel = (double*)o.ext_reliability;
+        t->tb.lr = (double2*)o.ext_latrel;
         t->tb.next = (int32_t*)o.ext_next_hop;
         t->tb.hops = (uint16_t*)o.ext_hops;
     } else {
-        TRY(dev_alloc(t->allocs, &t->tb.lat, elems));
-        TRY(dev_alloc(t->allocs, &t->tb.rel, elems));
+        TRY(dev_alloc(t->allocs, &t->tb.lr, elems));
         TRY(dev_alloc(t->allocs, &t->tb.next, elems));
         TRY(dev_alloc(t->allocs, &t->tb.hops, elems));
     }
@@ -2186,8 +2178,7 @@ int spe_table_layout_get(const spe_table* t, spe_table_layout* out) {
     out->block_begin = t->blk0;
     out->block_end = t->blk1;
     out->elems = (int64_t)(t->blk1 - t->blk0) * t->A * WAVE;
-    out->latency = t->tb.lat;
-    out->reliability = t->tb.rel;
+    out->latrel = t->tb.lr;
     out->next_hop = t->tb.next;
     out->hops = t->tb.hops;
     return SPE_OK;
@@ -2202,8 +2193,10 @@ int spe_table_get(const spe_table* t, int32_t s_slot, int32_t t_slot, spe_entry*
     HIP_TRY(hipSetDevice(t->g->device));
     const size_t o = ((size_t)(sb - t->blk0) * t->A + t_slot) * WAVE + (s_slot % WAVE);
     uint16_t h = 0;
-    HIP_TRY(hipMemcpy(&out->latency, t->tb.lat + o, sizeof(double), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(&out->reliability, t->tb.rel + o, sizeof(double), hipMemcpyDeviceToHost));
+    double2 e;
+    HIP_TRY(hipMemcpy(&e, t->tb.lr + o, sizeof(double2), hipMemcpyDeviceToHost));
+    out->latency = e.x;
+    out->reliability = e.y;
     HIP_TRY(hipMemcpy(&out->next_hop, t->tb.next + o, sizeof(int32_t), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&h, t->tb.hops + o, sizeof(uint16_t), hipMemcpyDeviceToHost));
     out->hops = h;
@@ -2220,13 +2213,13 @@ int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, d
     const int32_t A = t->A;
     const int32_t b0 = row_begin / WAVE, b1 = (row_end + WAVE - 1) / WAVE;
     const size_t blk_elems = (size_t)A * WAVE;
-    std::vector<double> bl(blk_elems), br(blk_elems);
+    std::vector<double2> blr(blk_elems);
     std::vector<int32_t> bn(blk_elems);
     std::vector<uint16_t> bh(blk_elems);
     for (int32_t b = b0; b < b1; ++b) {
         const size_t off = (size_t)(b - t->blk0) * blk_elems;
-        if (latency) HIP_TRY(hipMemcpy(bl.data(), t->tb.lat + off, blk_elems * 8, hipMemcpyDeviceToHost));
-        if (reliability) HIP_TRY(hipMemcpy(br.data(), t->tb.rel + off, blk_elems * 8, hipMemcpyDeviceToHost));
+        if (latency || reliability)
+            HIP_TRY(hipMemcpy(blr.data(), t->tb.lr + off, blk_elems * 16, hipMemcpyDeviceToHost));
         if (next_hop) HIP_TRY(hipMemcpy(bn.data(), t->tb.next + off, blk_elems * 4, hipMemcpyDeviceToHost));
         if (hops) HIP_TRY(hipMemcpy(bh.data(), t->tb.hops + off, blk_elems * 2, hipMemcpyDeviceToHost));
         for (int32_t l = 0; l < WAVE; ++l) {
@@ -2235,8 +2228,8 @@ int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, d
             const size_t ro = (size_t)(row - row_begin) * A;
             for (int32_t j = 0; j < A; ++j) {
                 const size_t src = (size_t)j * WAVE + l;
-                if (latency) latency[ro + j] = bl[src];
-                if (reliability) reliability[ro + j] = br[src];
+                if (latency) latency[ro + j] = blr[src].x;
+                if (reliability) reliability[ro + j] = blr[src].y;
                 if (next_hop) next_hop[ro + j] = bn[src];
                 if (hops) hops[ro + j] = bh[src];
             }
@@ -2266,7 +2259,7 @@ int spe_table_min_latency(const spe_table* t, double* out) {
     const unsigned long long init = 0x7FF0000000000000ull;  // +inf
     HIP_TRY(hipMemcpyAsync(t->d_min, &init, sizeof(init), hipMemcpyHostToDevice, t->stream));
     const int64_t elems = (int64_t)(t->blk1 - t->blk0) * t->A * WAVE;
-    k_min_latency<<<grid_for(elems, BLOCK, 4096), BLOCK, 0, t->stream>>>(t->tb.lat, elems, t->d_min);
+    k_min_latency<<<grid_for(elems, BLOCK, 4096), BLOCK, 0, t->stream>>>(t->tb.lr, elems, t->d_min);
     HIP_TRY(hipGetLastError());
     unsigned long long bits = 0;
     HIP_TRY(hipMemcpyAsync(&bits, t->d_min, sizeof(bits), hipMemcpyDeviceToHost, t->stream));

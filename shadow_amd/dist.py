@@ -15,7 +15,9 @@ from typing import Dict, Tuple
 import numpy as np
 
 WAVE = 64
-FIELDS = (("lat", np.float64), ("rel", np.float64), ("next", np.int32), ("hops", np.uint16))
+# table fields as stored on the device (include/spe.h spe_table_layout):
+# "lr" = {latency, reliability} f64 pairs, then next hop and hop count
+FIELDS = (("lr", np.float64, 2), ("next", np.int32, 1), ("hops", np.uint16, 1))
 
 
 def nblocks(n_attached: int) -> int:
@@ -42,30 +44,30 @@ def sb64_index(s_slot, t_slot, n_attached: int, block_begin: int = 0):
 
 
 def rows_to_sb64(rows: Dict[str, np.ndarray], row_begin: int, n_attached: int, nblk: int) -> Dict[str, np.ndarray]:
-    """Host rows (row-major [rows][A]) -> SB64 fields covering `nblk` blocks starting at
-    block row_begin // 64; missing rows are unroutable (-1 / -1 / -1 / 0)."""
+    """Host rows (row-major [rows][A]: lat, rel, next, hops) -> SB64 fields covering
+    `nblk` blocks starting at block row_begin // 64; missing rows are unroutable
+    (-1 / -1 / -1 / 0)."""
     assert row_begin % WAVE == 0
     b0 = row_begin // WAVE
-    out = {}
-    fill = {"lat": -1.0, "rel": -1.0, "next": -1, "hops": 0}
-    for name, dt in FIELDS:
-        f = np.full(nblk * n_attached * WAVE, fill[name], dtype=dt)
-        src = rows[name]
-        for r in range(src.shape[0]):
-            s = row_begin + r
-            idx = sb64_index(s, np.arange(n_attached), n_attached, b0)
-            f[idx] = src[r].astype(dt)
-        out[name] = f
-    return out
+    elems = nblk * n_attached * WAVE
+    lr = np.full((elems, 2), -1.0, dtype=np.float64)
+    nxt = np.full(elems, -1, dtype=np.int32)
+    hops = np.zeros(elems, dtype=np.uint16)
+    for r in range(rows["lat"].shape[0]):
+        idx = sb64_index(row_begin + r, np.arange(n_attached), n_attached, b0)
+        lr[idx, 0] = rows["lat"][r]
+        lr[idx, 1] = rows["rel"][r]
+        nxt[idx] = rows["next"][r]
+        hops[idx] = rows["hops"][r].astype(np.uint16)
+    return {"lr": lr, "next": nxt, "hops": hops}
 
 
 def sb64_to_rows(fields: Dict[str, np.ndarray], n_attached: int, row_begin: int, row_end: int) -> Dict[str, np.ndarray]:
-    out = {}
     t = np.arange(n_attached)
-    for name, _ in FIELDS:
-        f = fields[name]
-        out[name] = np.stack([f[sb64_index(s, t, n_attached)] for s in range(row_begin, row_end)])
-    return out
+    idx = [sb64_index(s, t, n_attached) for s in range(row_begin, row_end)]
+    lr = np.asarray(fields["lr"]).reshape(-1, 2)
+    return {"lat": np.stack([lr[i, 0] for i in idx]), "rel": np.stack([lr[i, 1] for i in idx]),
+            "next": np.stack([fields["next"][i] for i in idx]), "hops": np.stack([fields["hops"][i] for i in idx])}
 
 
 def allgather_table(shard: Dict, world: int, dist):
@@ -74,9 +76,9 @@ def allgather_table(shard: Dict, world: int, dist):
     import torch
     full = {}
     gloo = dist.get_backend() == "gloo"
-    for name, _ in FIELDS:
+    for name, _, _ in FIELDS:
         x = shard[name]
-        xb = x.view(torch.uint8)   # move raw bytes: not every backend takes uint16
+        xb = x.contiguous().view(-1).view(torch.uint8)   # raw bytes: not every backend takes uint16
         out = torch.empty(xb.numel() * world, dtype=torch.uint8, device=x.device)
         if gloo:
             parts = list(out.chunk(world))
@@ -84,5 +86,5 @@ def allgather_table(shard: Dict, world: int, dist):
             out = torch.cat(parts)
         else:
             dist.all_gather_into_tensor(out, xb)
-        full[name] = out.view(x.dtype)
+        full[name] = out.view(x.dtype).reshape((-1,) + tuple(x.shape[1:]))
     return full

@@ -45,14 +45,14 @@ class GraphInfo(C.Structure):
 class TableOpts(C.Structure):
     _fields_ = [("self_mode", C.c_int32), ("force_sssp", C.c_int32), ("groups_per_launch", C.c_int32),
                 ("block_begin", C.c_int32), ("block_end", C.c_int32),
-                ("ext_latency", C.c_void_p), ("ext_reliability", C.c_void_p),
+                ("ext_latrel", C.c_void_p),
                 ("ext_next_hop", C.c_void_p), ("ext_hops", C.c_void_p), ("ext_filled", C.c_int32),
                 ("owner_rank", C.c_void_p), ("engine", C.c_int32), ("lanes_per_group", C.c_int32)]
 
 
 class TableLayout(C.Structure):
     _fields_ = [("n_attached", C.c_int32), ("block_begin", C.c_int32), ("block_end", C.c_int32),
-                ("elems", C.c_int64), ("latency", C.c_void_p), ("reliability", C.c_void_p),
+                ("elems", C.c_int64), ("latrel", C.c_void_p),
                 ("next_hop", C.c_void_p), ("hops", C.c_void_p)]
 
 
@@ -187,8 +187,8 @@ class PathTable:
             o.owner_rank = self._rank.ctypes.data
         if blocks is not None:
             o.block_begin, o.block_end = int(blocks[0]), int(blocks[1])
-        if ext is not None:  # four device pointers (ints)
-            o.ext_latency, o.ext_reliability, o.ext_next_hop, o.ext_hops = [int(x) for x in ext]
+        if ext is not None:  # three device pointers (ints): latrel (2 x f64), next_hop (i32), hops (u16)
+            o.ext_latrel, o.ext_next_hop, o.ext_hops = [int(x) for x in ext]
             o.ext_filled = int(bool(ext_filled))
         h = C.c_void_p()
         _check(lib().spe_table_create(graph.h, _p(self.attached), self.A, C.byref(o), C.byref(h)),

@@ -32,7 +32,8 @@ def test_sb64_roundtrip_matches_layout():
         np.testing.assert_array_equal(back[k], r[k])
     # element (s, t) is where include/spe.h says it is
     s, t = 77, 12
-    assert f["lat"][((s // 64) * top.n + t) * 64 + s % 64] == r["lat"][s, t]
+    e = ((s // 64) * top.n + t) * 64 + s % 64
+    assert f["lr"][e, 0] == r["lat"][s, t] and f["lr"][e, 1] == r["rel"][s, t] and f["next"][e] == r["next"][s, t]
 
 
 def sys_path_oracle():

@@ -219,8 +219,7 @@ def test_external_storage_and_prefilled_table(spe):
     top = graphs.gen_random_small(200, 600, 47)
     A = np.arange(top.n, dtype=np.int32)
     elems = math.ceil(top.n / 64) * top.n * 64
-    bufs = [torch.empty(elems, dtype=torch.float64, device="cuda"),
-            torch.empty(elems, dtype=torch.float64, device="cuda"),
+    bufs = [torch.empty((elems, 2), dtype=torch.float64, device="cuda"),   # {latency, reliability}
             torch.empty(elems, dtype=torch.int32, device="cuda"),
             torch.empty(elems, dtype=torch.int16, device="cuda")]
     g = spe.Graph(top)
@@ -234,4 +233,6 @@ def test_external_storage_and_prefilled_table(spe):
         np.testing.assert_array_equal(out2[k], out[k])
     # the SB64 layout the header documents
     s, tt = 77, 12
-    assert bufs[0][((s // 64) * top.n + tt) * 64 + s % 64].item() == out["lat"][s, tt]
+    e = ((s // 64) * top.n + tt) * 64 + s % 64
+    assert bufs[0][e, 0].item() == out["lat"][s, tt] and bufs[0][e, 1].item() == out["rel"][s, tt]
+    assert bufs[1][e].item() == out["next"][s, tt]
