@@ -15,7 +15,9 @@ root, out = sys.argv[1], sys.argv[2]
 acc = collections.defaultdict(lambda: {"fetch_kb": 0.0, "write_kb": 0.0, "dispatches": set()})
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+        # "void (anonymous namespace)::k_relax<64, 8, 1>(...)" -> "k_relax"
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
+        k = k[5:] if k.startswith("void ") else k
         if r["Counter_Name"] == "FETCH_SIZE":
             acc[k]["fetch_kb"] += float(r["Counter_Value"])
             acc[k]["dispatches"].add((f, r["Dispatch_Id"]))
