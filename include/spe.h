@@ -188,6 +188,16 @@ int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, d
 int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, double* d_latency,
                      double* d_reliability, uint8_t* d_ok, void* stream);
 /* Minimum latency over every owned routable entry (minimumPathLatency). */
+/* On-disk path-table cache (the reference recomputes its paths
+ * every run).  The key hashes everything that determines the rows: the graph
+ * description, the attached set, self_mode, force_sssp, owner_rank and the block
+ * range.  spe_table_save writes the owned rows of a built table (atomically:
+ * "<path>.tmp" then rename); spe_table_load fills a created table from a file
+ * saved under the same key and marks it built, or returns SPE_EINVAL (other key,
+ * not a cache file, truncated) and leaves it unbuilt. */
+int spe_table_key(const spe_table* t, uint64_t* key);
+int spe_table_save(const spe_table* t, const char* path);
+int spe_table_load(spe_table* t, const char* path);
 int spe_table_min_latency(const spe_table* t, double* out);
 void spe_table_free(spe_table* t);
 

@@ -24,8 +24,12 @@
 //                  targets with vertex loss or multigraph get_eid latencies)
 //   k_rows_direct  complete graphs: every pair is the direct edge
 //   k_direct_overlay  preferdirectpaths: adjacent pairs get the direct edge
+//   k_sssp_lds     small graphs (<= ~11k relaxation vertices): one workgroup per
+//                  source row, relaxation state in LDS, rows written directly
+//   k_owner_replay compat: the reference's first-writer-wins path cache
 //   k_lookup       batched per-packet (s, t) -> (latency, reliability, ok)
 //   k_min_latency  minimumPathLatency reduction
+// plus the host side: graph upload, table build loop, on-disk table cache.
 //
 // Bit-exactness: every distance is the least fixpoint of
 // d[v] = min_u fl(d[u] + w), which igraph's Dijkstra also computes (IEEE
@@ -55,6 +59,20 @@ int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+
+// FNV-1a 64 over raw bytes (table cache keys)
+struct Fnv {
+    uint64_t h = 1469598103934665603ull;
+    void add(const void* p, size_t n) {
+        const unsigned char* b = static_cast<const unsigned char*>(p);
+        for (size_t i = 0; i < n; ++i) {
+            h ^= b[i];
+            h *= 1099511628211ull;
+        }
+    }
+    template <typename T>
+    void val(const T& x) { add(&x, sizeof(x)); }
+};
 
 #define HIP_TRY(expr)                                                                      \
     do {                                                                                   \
@@ -929,7 +947,6 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
     int32_t* pvt = coff + nc;
     __shared__ int32_t s_tail, s_total, s_wsum[LDS_WAVES];
     const int32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
-    const int32_t nchunk = (nc + WAVE - 1) / WAVE;
     const unsigned long long INF_BITS = 0x7FF0000000000000ull;
     const int32_t oend = G.optr[nc];
     // Workgroups are dealt round-robin over the 8 XCDs; give the workgroups of
@@ -1455,6 +1472,7 @@ __global__ __launch_bounds__(BLOCK) void k_min_latency(const double2* __restrict
 
 struct spe_graph {
     spe::HostGraph hg;
+    uint64_t key = 0;              // hash of the graph description (table cache key)
     int32_t device = 0;
     DevGraph dev{};
     HeavyPlan hp{};
@@ -1464,6 +1482,7 @@ struct spe_graph {
 
 struct spe_table {
     spe_graph* g = nullptr;
+    uint64_t key = 0;              // on-disk cache key (spe_table_key)
     int32_t A = 0;
     int32_t blk0 = 0, blk1 = 0;
     int32_t groups = 8;            // 64-source blocks per batch
@@ -1585,6 +1604,22 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
         return r;
     }
     g->device = device;
+    {   // everything in the description that can change a row
+        Fnv f;
+        f.val(desc->n_vertices);
+        f.val(desc->n_edges);
+        const size_t m = (size_t)desc->n_edges;
+        f.add(desc->edge_source, m * sizeof(int32_t));
+        f.add(desc->edge_target, m * sizeof(int32_t));
+        f.add(desc->edge_latency, m * sizeof(double));
+        f.add(desc->edge_packetloss, m * sizeof(double));
+        const int32_t has_v = desc->vertex_packetloss != nullptr;
+        f.val(has_v);
+        if (has_v) f.add(desc->vertex_packetloss, (size_t)desc->n_vertices * sizeof(double));
+        f.val(desc->directed);
+        f.val(desc->prefer_direct);
+        g->key = f.h;
+    }
     spe::prune_pendants(&g->hg, getenv("SPE_NO_PRUNE") == nullptr);
     const spe::HostGraph& h = g->hg;
     DevGraph& d = g->dev;
@@ -1759,6 +1794,23 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         t->blk1 = o.block_end;
     }
     const bool force = o.force_sssp != 0;
+    {   // table cache key: graph, attached set, and every option that changes a row
+        Fnv f;
+        const char fmt[] = "spe-table-v1 latrel+next+hops SB64";
+        f.add(fmt, sizeof(fmt));
+        f.val(g->key);
+        f.val(n_attached);
+        f.add(attached, (size_t)n_attached * sizeof(int32_t));
+        f.val(o.self_mode);
+        const int32_t fs = force;
+        f.val(fs);
+        f.val(t->blk0);
+        f.val(t->blk1);
+        const int32_t has_owner = o.owner_rank != nullptr;
+        f.val(has_owner);
+        if (has_owner) f.add(o.owner_rank, (size_t)n_attached * sizeof(int32_t));
+        t->key = f.h;
+    }
     t->md.complete = g->hg.complete && !force;
     t->md.prefer = g->hg.prefer_direct && !force;
     t->md.self_mode = o.self_mode;
@@ -2268,6 +2320,119 @@ int spe_table_min_latency(const spe_table* t, double* out) {
     std::memcpy(&v, &bits, sizeof(v));
     *out = (v == INF) ? 0.0 : v;   // reference's "0 = unset" sentinel, shd-topology.c:1360
     return SPE_OK;
+}
+
+// ---------------------------------------------------------------- table cache
+// File: 64-byte header, then the owned SB64 span of each field (latrel, next,
+// hops), raw.  Written to "<path>.tmp" and renamed, so a reader never sees a
+// partial file under the final name.
+namespace {
+struct CacheHeader {
+    char magic[8];        // "SPETAB01"
+    uint64_t key;
+    int32_t A, blk0, blk1, pad;
+    int64_t elems;
+    int64_t bytes;        // payload bytes after the header
+    char reserved[16];
+};
+static_assert(sizeof(CacheHeader) == 64, "cache header is 64 bytes");
+const char kMagic[8] = {'S', 'P', 'E', 'T', 'A', 'B', '0', '1'};
+constexpr size_t kChunk = 64u << 20;   // staging chunk
+
+struct Field {
+    void* dev;
+    size_t bytes;
+};
+
+void fields_of(const spe_table* t, Field f[3], int64_t* elems) {
+    const int64_t e = (int64_t)(t->blk1 - t->blk0) * t->A * WAVE;
+    *elems = e;
+    f[0] = {t->tb.lr, (size_t)e * sizeof(double2)};
+    f[1] = {t->tb.next, (size_t)e * sizeof(int32_t)};
+    f[2] = {t->tb.hops, (size_t)e * sizeof(uint16_t)};
+}
+}  // namespace
+
+int spe_table_key(const spe_table* t, uint64_t* key) {
+    if (!t || !key) return fail(SPE_EINVAL, "NULL argument");
+    *key = t->key;
+    return SPE_OK;
+}
+
+int spe_table_save(const spe_table* t, const char* path) {
+    if (!t || !path) return fail(SPE_EINVAL, "NULL argument");
+    if (!t->built) return fail(SPE_ESTATE, "table not built");
+    HIP_TRY(hipSetDevice(t->g->device));
+    HIP_TRY(hipStreamSynchronize(t->stream));
+    Field f[3];
+    int64_t elems = 0;
+    fields_of(t, f, &elems);
+    CacheHeader h{};
+    std::memcpy(h.magic, kMagic, 8);
+    h.key = t->key;
+    h.A = t->A;
+    h.blk0 = t->blk0;
+    h.blk1 = t->blk1;
+    h.elems = elems;
+    h.bytes = (int64_t)(f[0].bytes + f[1].bytes + f[2].bytes);
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE* fp = fopen(tmp.c_str(), "wb");
+    if (!fp) return fail(SPE_EINVAL, "cannot create " + tmp);
+    void* stage = nullptr;
+    if (hipHostMalloc(&stage, kChunk) != hipSuccess) {
+        fclose(fp);
+        remove(tmp.c_str());
+        return fail(SPE_ENOMEM, "cache staging buffer");
+    }
+    int rc = SPE_OK;
+    if (fwrite(&h, sizeof(h), 1, fp) != 1) rc = fail(SPE_EINVAL, "short write " + tmp);
+    for (int i = 0; i < 3 && rc == SPE_OK; ++i) {
+        for (size_t off = 0; off < f[i].bytes && rc == SPE_OK; off += kChunk) {
+            const size_t n = std::min(kChunk, f[i].bytes - off);
+            const hipError_t e = hipMemcpy(stage, (const char*)f[i].dev + off, n, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) rc = fail(SPE_EHIP, std::string("hipMemcpy D2H: ") + hipGetErrorString(e));
+            else if (fwrite(stage, 1, n, fp) != n) rc = fail(SPE_EINVAL, "short write " + tmp);
+        }
+    }
+    (void)hipHostFree(stage);
+    if (fclose(fp) != 0 && rc == SPE_OK) rc = fail(SPE_EINVAL, "close " + tmp);
+    if (rc == SPE_OK && rename(tmp.c_str(), path) != 0) rc = fail(SPE_EINVAL, std::string("rename to ") + path);
+    if (rc != SPE_OK) remove(tmp.c_str());
+    return rc;
+}
+
+int spe_table_load(spe_table* t, const char* path) {
+    if (!t || !path) return fail(SPE_EINVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(t->g->device));
+    FILE* fp = fopen(path, "rb");
+    if (!fp) return fail(SPE_EINVAL, std::string("no cache file ") + path);
+    Field f[3];
+    int64_t elems = 0;
+    fields_of(t, f, &elems);
+    CacheHeader h{};
+    int rc = SPE_OK;
+    if (fread(&h, sizeof(h), 1, fp) != 1 || std::memcmp(h.magic, kMagic, 8) != 0)
+        rc = fail(SPE_EINVAL, std::string("not a path-table cache: ") + path);
+    else if (h.key != t->key || h.A != t->A || h.blk0 != t->blk0 || h.blk1 != t->blk1 || h.elems != elems ||
+             h.bytes != (int64_t)(f[0].bytes + f[1].bytes + f[2].bytes))
+        rc = fail(SPE_EINVAL, std::string("cache file is for another graph / attached set / options: ") + path);
+    void* stage = nullptr;
+    if (rc == SPE_OK && hipHostMalloc(&stage, kChunk) != hipSuccess) rc = fail(SPE_ENOMEM, "cache staging buffer");
+    for (int i = 0; i < 3 && rc == SPE_OK; ++i) {
+        for (size_t off = 0; off < f[i].bytes && rc == SPE_OK; off += kChunk) {
+            const size_t n = std::min(kChunk, f[i].bytes - off);
+            if (fread(stage, 1, n, fp) != n) {
+                rc = fail(SPE_EINVAL, std::string("truncated cache file ") + path);
+                break;
+            }
+            const hipError_t e = hipMemcpy((char*)f[i].dev + off, stage, n, hipMemcpyHostToDevice);
+            if (e != hipSuccess) rc = fail(SPE_EHIP, std::string("hipMemcpy H2D: ") + hipGetErrorString(e));
+        }
+    }
+    if (stage) (void)hipHostFree(stage);
+    fclose(fp);
+    if (rc == SPE_OK) t->built = true;
+    return rc;
 }
 
 void spe_table_free(spe_table* t) {

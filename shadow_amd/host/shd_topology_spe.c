@@ -802,7 +802,23 @@ int32_t topology_seal(Topology* top) {
             memset(&o, 0, sizeof o);
             o.self_mode = SPE_SELF_ROW;
             rc = spe_table_create(top->graph, att, A, &o, &top->table);
-            if (rc == SPE_OK) rc = spe_table_build(top->table, NULL);
+            /* SHADOW_SPE_TABLE_CACHE=<dir>: reuse the rows of an earlier run on the
+             * same graph / hosts (keyed file), else build and save them */
+            const char* cdir = getenv("SHADOW_SPE_TABLE_CACHE");
+            char cpath[4096] = {0};
+            int loaded = 0;
+            if (rc == SPE_OK && cdir && *cdir) {
+                uint64_t key = 0;
+                spe_table_key(top->table, &key);
+                snprintf(cpath, sizeof cpath, "%s/spe-table-%016llx.bin", cdir, (unsigned long long)key);
+                loaded = spe_table_load(top->table, cpath) == SPE_OK;
+                tlog(top, LOG_MESSAGE, "path table cache %s: %s", loaded ? "hit" : "miss", cpath);
+            }
+            if (rc == SPE_OK && !loaded) {
+                rc = spe_table_build(top->table, NULL);
+                if (rc == SPE_OK && cpath[0] && spe_table_save(top->table, cpath) != SPE_OK)
+                    tlog(top, LOG_WARNING, "could not save the path table cache: %s", spe_last_error());
+            }
             if (rc == SPE_OK) {
                 free(top->lat);
                 free(top->rel);

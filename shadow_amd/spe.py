@@ -78,7 +78,7 @@ EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_
            "spe_table_create", "spe_table_build", "spe_table_build_blocks", "spe_table_profile_enable",
            "spe_table_profile_get", "spe_table_build_stats", "spe_table_layout_get",
            "spe_table_get", "spe_table_download", "spe_lookup_batch", "spe_table_min_latency",
-           "spe_table_free"]
+           "spe_table_key", "spe_table_save", "spe_table_load", "spe_table_free"]
 
 _lib = None
 
@@ -115,6 +115,9 @@ def lib():
         L.spe_table_download.argtypes = [P, C.c_int32, C.c_int32, P, P, P, P]
         L.spe_lookup_batch.argtypes = [P, P, C.c_int64, P, P, P, P]
         L.spe_table_min_latency.argtypes = [P, P]
+        L.spe_table_key.argtypes = [P, P]
+        L.spe_table_save.argtypes = [P, C.c_char_p]
+        L.spe_table_load.argtypes = [P, C.c_char_p]
         L.spe_table_free.argtypes = [P]
         L.spe_table_free.restype = None
         _lib = L
@@ -245,6 +248,17 @@ class PathTable:
         _check(lib().spe_lookup_batch(self.h, C.c_void_p(d_pairs), int(q), C.c_void_p(d_lat), C.c_void_p(d_rel),
                                       C.c_void_p(d_ok), C.c_void_p(stream) if stream else None),
                "spe_lookup_batch")
+
+    def key(self) -> int:
+        k = C.c_uint64(0)
+        _check(lib().spe_table_key(self.h, C.byref(k)), "spe_table_key")
+        return int(k.value)
+
+    def save(self, path: str):
+        _check(lib().spe_table_save(self.h, os.fsencode(path)), "spe_table_save")
+
+    def load(self, path: str):
+        _check(lib().spe_table_load(self.h, os.fsencode(path)), "spe_table_load")
 
     def min_latency(self) -> float:
         v = C.c_double(0)
