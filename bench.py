@@ -42,6 +42,14 @@ def workload(name: str):
         top = graphs.gen_tiered()
         att = graphs.tiered_attached(top)
         desc = "C4: tiered BA core 20k + 180k stubs, A=100000 stubs"
+    elif name == "c1":
+        # the reference's shipped topology (resource/topology.graphml.xml.xz, 183 vertices,
+        # complete => DIRECT regime), committed as data in tests/golden; every vertex attached
+        z = np.load(os.path.join(ROOT, "tests", "golden", "shipped_topology.npz"))
+        top = graphs.Topology(n=int(z["n"]), esrc=z["esrc"], edst=z["edst"], elat=z["elat"], eloss=z["eloss"],
+                              vloss=z["vloss"], directed=bool(z["directed"]), prefer_direct=bool(z["prefer_direct"]))
+        att = np.arange(top.n, dtype=np.int32)
+        desc = "C1: shipped resource/topology.graphml.xml.xz (183 V, complete: DIRECT), all 183 vertices attached"
     elif name == "c2":
         top = graphs.gen_rgg(10000, 2)
         att = np.arange(top.n, dtype=np.int32)
@@ -308,15 +316,19 @@ def main():
     roof = None
     extra = {}
     lds = kp is not None and kp["lds"]["launches"] > 0
+    direct = kp is not None and kp["direct"]["launches"] > 0 and kp["relax"]["launches"] == 0 and not lds
     if lds:   # one fused kernel: relaxation in LDS + row writes
         b_relax += b_rows
+    if direct:   # complete graph: every row is DIRECT, 38 B per pair
+        b_relax = 38.0 * A
     if kp is not None:
-        kname = "k_sssp_lds" if lds else "k_relax"
-        rl = kp["lds" if lds else "relax"]
+        kname = "k_sssp_lds" if lds else ("k_rows_direct" if direct else "k_relax")
+        rl = kp["lds" if lds else ("direct" if direct else "relax")]
         relax_s = rl["ms"] / 1e3
         ach = b_relax * done / relax_s / 1e9 if relax_s > 0 else 0.0
         traffic = pmc_traffic(args, kname)
-        roof = {"bound": "hbm", "kernel": kname + (" (SSSP + rows, LDS-resident state)" if lds else " (SSSP stage)"),
+        roof = {"bound": "hbm", "kernel": kname + (" (SSSP + rows, LDS-resident state)" if lds else
+                                                   (" (DIRECT rows)" if direct else " (SSSP stage)")),
                 "achieved": round(ach, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "launches": rl["launches"], "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
@@ -330,7 +342,7 @@ def main():
         extra["kernel_ms"] = {k: round(v["ms"], 3) for k, v in kp.items()}
         extra["kernel_launches"] = {k: v["launches"] for k, v in kp.items()}
         extra["pipeline_frac_of_hbm"] = round((b_relax + (0 if lds else b_rows)) * value / 1e9 / HBM_PEAK_GBS, 4)
-        extra["engine"] = "lds" if lds else "batch"
+        extra["engine"] = "lds" if lds else ("direct" if direct else "batch")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(top, att, args.cpu_seconds)

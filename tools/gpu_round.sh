@@ -22,6 +22,10 @@ timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d $O/kt_c3 -o run --output
 timeout -k 10 300 python -u bench.py --config c2 > $O/bench_c2.log 2>&1 || { tail -20 $O/bench_c2.log; exit 1; }
 tail -1 $O/bench_c2.log
 timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d $O/kt_c2 -o run --output-format csv -- python bench.py --config c2 --no-cpu-baseline > $O/kt_c2.log 2>&1
+timeout -k 10 200 python -u bench.py --config c1 > $O/bench_c1.log 2>&1 || { tail -20 $O/bench_c1.log; exit 1; }
+tail -1 $O/bench_c1.log
+timeout -k 10 300 python -u bench.py --config c4 --full-table --shares 8 --share-index 0 > $O/bench_c4.log 2>&1 || { tail -20 $O/bench_c4.log; exit 1; }
+tail -1 $O/bench_c4.log
 timeout -k 10 200 python -u bench.py --config c5 --steps 10 --warmup 2 > $O/bench_c5.log 2>&1 || { tail -20 $O/bench_c5.log; exit 1; }
 tail -1 $O/bench_c5.log
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $O/kt_c5 -o run --output-format csv -- python bench.py --config c5 --steps 4 --warmup 1 > $O/kt_c5.log 2>&1
