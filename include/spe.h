@@ -115,6 +115,12 @@ typedef struct spe_table_opts {
     int32_t engine;                 /* SPE_ENGINE_* */
     int32_t lanes_per_group;        /* sources sharing one relaxation frontier: 16, 32 or 64;
                                      * 0 = default (64: measured fastest on C3) */
+    int32_t want_aux;               /* 1: also fold the graph's auxiliary edge attribute
+                                     * (spe_graph_set_edge_aux) along every row's path, in path
+                                     * order from 0.0 -- the offline completion tool's jitter sum
+                                     * (compute-topology-paths.py:27-33).  SSSP rows on the batch
+                                     * engine only (force_sssp for complete / preferdirect graphs);
+                                     * (s,s) = 0, unroutable = -1. */
 } spe_table_opts;
 
 /* Where a table keeps its rows.  Element (s_slot, t_slot) of a field lives at
@@ -152,6 +158,11 @@ int spe_device_count(int32_t* out);
 
 int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out);
 int spe_graph_info_get(const spe_graph* g, spe_graph_info* out);
+/* Optional per-edge auxiliary attribute (e.g. GraphML "jitter"), edge_aux[e] for
+ * every edge e of the description; a merged vertex pair takes its get_eid edge's
+ * value.  Replaces nothing in shd-topology.c (which only validates jitter,
+ * :1090-1100); it serves the offline completion tool (compute-topology-paths.py). */
+int spe_graph_set_edge_aux(spe_graph* g, const double* edge_aux);
 void spe_graph_free(spe_graph* g);
 
 /* attached[i] = vertex of source/target slot i (unique vertices). */
@@ -181,6 +192,8 @@ int spe_table_get(const spe_table* t, int32_t s_slot, int32_t t_slot, spe_entry*
  * any output pointer may be NULL. */
 int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, double* latency,
                        double* reliability, int32_t* next_hop, int32_t* hops);
+/* Owned rows [row_begin,row_end) of the want_aux field, row-major, to host. */
+int spe_table_download_aux(const spe_table* t, int32_t row_begin, int32_t row_end, double* aux);
 /* Batched per-packet lookups against the HBM-resident table.  d_pairs holds q
  * (s_slot, t_slot) int32 pairs; outputs are device arrays of q elements.
  * ok = 1 when routable (topology_isRoutable).  Pairs whose source row is not

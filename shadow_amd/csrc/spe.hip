@@ -117,6 +117,9 @@ struct DevGraph {
     const double* fiw;
     const double* fia;
     const double* fiwrep;
+    // optional per-edge auxiliary attribute of the get_eid edge (spe_graph_set_edge_aux)
+    const double* iaux;          // [relaxation in-CSR entry]
+    const double* fiaux;         // [full in-CSR entry]
     const int32_t* dptr;         // DIRECT lookups: full out-CSR
     const int32_t* dcol;
     const double* dwrep;
@@ -155,6 +158,7 @@ struct Table {
     uint16_t* hops;
     int32_t A;
     int32_t* prev;    // owner-replay mode only: vertex before the target on the path
+    double* aux;      // want_aux only: path-order sum of the edges' auxiliary attribute
 };
 
 __device__ __forceinline__ bool has_attr(double x) { return !__builtin_isnan(x); }
@@ -678,6 +682,45 @@ __device__ __forceinline__ bool direct_entry(const DevGraph& G, int32_t s, int32
     return true;
 }
 
+// Path-order sum 0.0 + a_1 + a_2 + ... of the auxiliary edge attribute along the
+// row's path to core vertex c (then the pendant target edge kt, if any), as the
+// offline completion tool sums a path's jitters (compute-topology-paths.py:27-33).
+// The path is walked back from c through the parent edges; up to 64 core edges
+// are kept and folded forward, longer paths re-walk per edge (O(h^2)).
+template <int L>
+__device__ double aux_fold(const DevGraph& G, const State& st, int32_t g, int32_t n, int32_t j, int32_t s,
+                           int32_t c, int32_t kt) {
+    constexpr int KMAX = 64;
+    int32_t ks[KMAX];
+    int32_t nk = 0;
+    bool pend_src = false, overflow = false;
+    for (int32_t x = c;;) {
+        const int32_t k = st.P[sidx<L>(g, n, x, j)];
+        if (k == -1) break;             // x is the (core) source
+        if (k == -2) {                  // x is the anchor of a pruned source: s -> x
+            pend_src = true;
+            break;
+        }
+        if (nk < KMAX) ks[nk] = k;
+        else overflow = true;
+        ++nk;
+        x = G.icol[k];
+    }
+    double a = 0.0;
+    if (pend_src) a += G.fiaux[G.fiptr[s]];
+    if (!overflow) {
+        for (int32_t q = nk - 1; q >= 0; --q) a += G.iaux[ks[q]];
+    } else {
+        for (int32_t q = nk - 1; q >= 0; --q) {   // edge q (0 = the last one, into c)
+            int32_t x = c;
+            for (int32_t r = 0; r < q; ++r) x = G.icol[st.P[sidx<L>(g, n, x, j)]];
+            a += G.iaux[st.P[sidx<L>(g, n, x, j)]];
+        }
+    }
+    if (kt >= 0) a += G.fiaux[kt];
+    return a;
+}
+
 // State -> table rows.  One wave per (64-source block of the batch, target
 // slot): lane l = source b*64 + l, i.e. lane group b*(64/L) + l/L, lane l%L.
 template <int L>
@@ -694,12 +737,13 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
         const int32_t t = slot_vertex[jt];
         const int32_t g = b * (WAVE / L) + lane / L, j = lane % L;
         const int32_t s = srcv[b * WAVE + lane];
-        double Lt = -1.0, R = -1.0;
+        double Lt = -1.0, R = -1.0, AX = -1.0;
         int32_t N = -1, H = 0, PV = -1;
         if (s >= 0) {
             if (t == s) {
                 self_entry(G, md, s, Lt, R, N, H);
                 PV = (H == 2) ? N : (H > 0 ? s : -1);
+                AX = 0.0;
             } else {
                 // a pruned pendant target is one edge past its anchor: Dijkstra's
                 // d[t] = d[c] + w, parent c (its only candidate)
@@ -758,6 +802,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
                         R = r;
                     }
                     if (Lt == 0) Lt = 1;   // shd-topology.c:1833-1837
+                    if (tb.aux) AX = aux_fold<L>(G, st, g, n, j, s, c, kt);
                     N = rr.f;
                     H = rr.h;
                     if (tb.prev) {
@@ -776,6 +821,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
         tb.next[o] = N;
         tb.hops[o] = (uint16_t)(H > 65535 ? 65535 : H);
         if (tb.prev) tb.prev[o] = PV;
+        if (tb.aux) tb.aux[o] = AX;
     }
 }
 
@@ -1740,6 +1786,22 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
     return SPE_OK;
 }
 
+int spe_graph_set_edge_aux(spe_graph* g, const double* edge_aux) {
+    if (!g || (!edge_aux && g->hg.m > 0)) return fail(SPE_EINVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(g->device));
+    const spe::HostGraph& h = g->hg;
+    for (int64_t e = 0; e < h.m; ++e)
+        if (!std::isfinite(edge_aux[e])) return fail(SPE_EINVAL, "edge " + std::to_string(e) + " aux value is not finite");
+    std::vector<double> ia(h.ieid.size()), fa(h.fieid.size());
+    for (size_t k = 0; k < ia.size(); ++k) ia[k] = edge_aux[h.ieid[k]];
+    for (size_t k = 0; k < fa.size(); ++k) fa[k] = edge_aux[h.fieid[k]];
+    if (ia.empty()) ia.push_back(0.0);
+    if (fa.empty()) fa.push_back(0.0);
+    if (int r = dev_upload(g->allocs, ia, &g->dev.iaux)) return r;
+    if (int r = dev_upload(g->allocs, fa, &g->dev.fiaux)) return r;
+    return SPE_OK;
+}
+
 int spe_graph_info_get(const spe_graph* g, spe_graph_info* out) {
     if (!g || !out) return fail(SPE_EINVAL, "NULL argument");
     out->n_vertices = g->hg.n;
@@ -1808,11 +1870,29 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         f.val(t->blk1);
         const int32_t has_owner = o.owner_rank != nullptr;
         f.val(has_owner);
+        const int32_t aux = o.want_aux != 0;
+        f.val(aux);
         if (has_owner) f.add(o.owner_rank, (size_t)n_attached * sizeof(int32_t));
         t->key = f.h;
     }
     t->md.complete = g->hg.complete && !force;
     t->md.prefer = g->hg.prefer_direct && !force;
+    if (o.want_aux) {   // the aux fold walks the batch engine's parent edges: SSSP rows only
+        if (!g->dev.iaux) {
+            delete t;
+            return fail(SPE_ESTATE, "want_aux: no auxiliary edge attribute (spe_graph_set_edge_aux)");
+        }
+        if (t->md.complete || t->md.prefer || o.owner_rank) {
+            delete t;
+            return fail(SPE_EUNSUPPORTED, "want_aux needs SSSP rows (force_sssp on complete/preferdirect graphs, "
+                                          "no owner replay)");
+        }
+        if (o.engine == SPE_ENGINE_LDS) {
+            delete t;
+            return fail(SPE_EUNSUPPORTED, "want_aux runs on the batch engine");
+        }
+        o.engine = SPE_ENGINE_BATCH;
+    }
     t->md.self_mode = o.self_mode;
     t->md.multi_rep = g->hg.multi_rep;
     t->md.directed = g->hg.directed;
@@ -1836,7 +1916,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         const bool fits = lds_bytes(g->hg.nc) <= (size_t)LDS_MAX_BYTES;
         int32_t e = o.engine;
         bool from_env = false;
-        if (e == SPE_ENGINE_AUTO && getenv("SPE_ENGINE")) {   // test / diagnostic override
+        if (e == SPE_ENGINE_AUTO && !o.want_aux && getenv("SPE_ENGINE")) {   // test / diagnostic override
             e = atoi(getenv("SPE_ENGINE"));
             from_env = true;
         }
@@ -1898,6 +1978,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         t->d_rank = const_cast<int32_t*>(tmpr);
         TRY(dev_alloc(t->allocs, &t->tb.prev, elems));
     }
+    if (o.want_aux) TRY(dev_alloc(t->allocs, &t->tb.aux, elems));
     const std::vector<int32_t> sv(attached, attached + n_attached);
     const int32_t* tmp = nullptr;
     TRY(dev_upload(t->allocs, sv, &tmp));
@@ -2290,6 +2371,29 @@ int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, d
     return SPE_OK;
 }
 
+int spe_table_download_aux(const spe_table* t, int32_t row_begin, int32_t row_end, double* aux) {
+    if (!t || !aux) return fail(SPE_EINVAL, "NULL argument");
+    if (!t->tb.aux) return fail(SPE_ESTATE, "table was created without want_aux");
+    if (!t->built) return fail(SPE_ESTATE, "table not built");
+    if (row_begin < t->blk0 * WAVE || row_end > std::min(t->A, t->blk1 * WAVE) || row_begin > row_end)
+        return fail(SPE_EINVAL, "row range not owned by this table");
+    HIP_TRY(hipSetDevice(t->g->device));
+    const int32_t A = t->A;
+    const size_t blk_elems = (size_t)A * WAVE;
+    std::vector<double> ba(blk_elems);
+    for (int32_t b = row_begin / WAVE; b < (row_end + WAVE - 1) / WAVE; ++b) {
+        HIP_TRY(hipMemcpy(ba.data(), t->tb.aux + (size_t)(b - t->blk0) * blk_elems, blk_elems * 8,
+                          hipMemcpyDeviceToHost));
+        for (int32_t l = 0; l < WAVE; ++l) {
+            const int32_t row = b * WAVE + l;
+            if (row < row_begin || row >= row_end) continue;
+            double* o = aux + (size_t)(row - row_begin) * A;
+            for (int32_t j = 0; j < A; ++j) o[j] = ba[(size_t)j * WAVE + l];
+        }
+    }
+    return SPE_OK;
+}
+
 int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, double* d_latency,
                      double* d_reliability, uint8_t* d_ok, void* stream) {
     if (!t || (q > 0 && (!d_pairs || !d_latency || !d_reliability || !d_ok))) return fail(SPE_EINVAL, "bad arguments");
@@ -2360,6 +2464,7 @@ int spe_table_key(const spe_table* t, uint64_t* key) {
 }
 
 int spe_table_save(const spe_table* t, const char* path) {
+    if (t && t->tb.aux) return fail(SPE_EUNSUPPORTED, "the table cache does not hold want_aux rows");
     if (!t || !path) return fail(SPE_EINVAL, "NULL argument");
     if (!t->built) return fail(SPE_ESTATE, "table not built");
     HIP_TRY(hipSetDevice(t->g->device));
@@ -2402,6 +2507,7 @@ int spe_table_save(const spe_table* t, const char* path) {
 }
 
 int spe_table_load(spe_table* t, const char* path) {
+    if (t && t->tb.aux) return fail(SPE_EUNSUPPORTED, "the table cache does not hold want_aux rows");
     if (!t || !path) return fail(SPE_EINVAL, "NULL argument");
     HIP_TRY(hipSetDevice(t->g->device));
     FILE* fp = fopen(path, "rb");

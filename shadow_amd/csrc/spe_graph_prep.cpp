@@ -101,6 +101,7 @@ int prepare_graph(const spe_graph_desc* d, HostGraph* hg, std::string* err) {
     hg->iw.clear();
     hg->ia.clear();
     hg->iwrep.clear();
+    hg->ieid.clear();
     hg->multi_rep = false;
     for (size_t i = 0; i < ents.size();) {
         size_t j = i;
@@ -116,6 +117,7 @@ int prepare_graph(const spe_graph_desc* d, HostGraph* hg, std::string* err) {
         hg->iw.push_back(wrel);
         hg->ia.push_back(1.0 - d->edge_packetloss[rep]);
         hg->iwrep.push_back(wrep);
+        hg->ieid.push_back(rep);
         hg->iptr[ents[i].to + 1]++;
         i = j;
     }
@@ -225,6 +227,7 @@ void prune_pendants(HostGraph* hg, bool enable) {
     hg->fiw = hg->iw;
     hg->fia = hg->ia;
     hg->fiwrep = hg->iwrep;
+    hg->fieid = hg->ieid;
     hg->core_id.resize(n);
     hg->anchor_core.assign(n, -1);
     std::vector<uint8_t> pend(n, 0);
@@ -255,6 +258,7 @@ void prune_pendants(HostGraph* hg, bool enable) {
     // neighbour order is unchanged, so lists stay sorted by original = core id)
     std::vector<int32_t> iptr(1, 0), icol;
     std::vector<double> iw, ia, iwrep;
+    std::vector<int64_t> ieid;
     for (int32_t c = 0; c < hg->nc; ++c) {
         const int32_t v = hg->corev[c];
         for (int32_t k = hg->fiptr[v]; k < hg->fiptr[v + 1]; ++k) {
@@ -264,6 +268,7 @@ void prune_pendants(HostGraph* hg, bool enable) {
             iw.push_back(hg->fiw[k]);
             ia.push_back(hg->fia[k]);
             iwrep.push_back(hg->fiwrep[k]);
+            ieid.push_back(hg->fieid[k]);
         }
         iptr.push_back((int32_t)icol.size());
     }
@@ -272,6 +277,7 @@ void prune_pendants(HostGraph* hg, bool enable) {
     hg->iw.swap(iw);
     hg->ia.swap(ia);
     hg->iwrep.swap(iwrep);
+    hg->ieid.swap(ieid);
     hg->orev.resize(hg->icol.size());
     for (int32_t x = 0; x < hg->nc; ++x)
         for (int32_t k = hg->iptr[x]; k < hg->iptr[x + 1]; ++k) {

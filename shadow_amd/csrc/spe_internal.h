@@ -31,12 +31,14 @@ struct HostGraph {
     // full in-CSR (original ids): DIRECT lookups and the pendant edges
     std::vector<int32_t> fiptr, ficol;
     std::vector<double> fiw, fia, fiwrep;
+    std::vector<int64_t> fieid;        // get_eid edge id of each full in-CSR entry
 
     // relaxation in-CSR (relaxation ids): entries u -> v grouped by v, sorted by u
     std::vector<int32_t> iptr, icol;
     std::vector<double> iw;        // min latency over parallel u->v edges (what Dijkstra relaxes)
     std::vector<double> ia;        // 1 - loss of the get_eid edge
     std::vector<double> iwrep;     // latency of the get_eid edge
+    std::vector<int64_t> ieid;     // id of the get_eid edge (per-edge auxiliary attributes)
     // out-CSR (directed only; undirected graphs reuse the in-CSR)
     std::vector<int32_t> optr, ocol;
     std::vector<int32_t> orev;     // out entry -> in-CSR index of the same (merged) edge

@@ -43,6 +43,7 @@ class Topology:
     prefer_direct: bool = False
     vertex_ids: Optional[List[str]] = None
     vattrs: Dict[str, list] = field(default_factory=dict)
+    eattrs: Dict[str, np.ndarray] = field(default_factory=dict)   # optional f64 edge attrs (jitter)
     name: str = ""
 
     @property
@@ -163,8 +164,12 @@ def load_graphml(source: str, is_text: bool = False) -> Topology:
         kid, kdef = find_key("node", canon)
         if kid is not None:
             vattrs[canon] = [vd.get(kid, kdef) for vd in vdata]
+    eattrs = {}
+    jk, jdef = find_key("edge", "jitter")
+    if jk is not None:
+        eattrs["jitter"] = np.array([numeric(e[2].get(jk, jdef)) for e in edges], dtype=np.float64)
     top = Topology(n=n, esrc=esrc, edst=edst, elat=elat, eloss=eloss, vloss=vloss,
-                   directed=directed, prefer_direct=pref, vertex_ids=names, vattrs=vattrs)
+                   directed=directed, prefer_direct=pref, vertex_ids=names, vattrs=vattrs, eattrs=eattrs)
     return top
 
 
@@ -349,6 +354,55 @@ def write_graphml(top: Topology, path: str, ips=None, bandwidth: int = 10240) ->
         out.append(f'<edge source="v{int(top.esrc[e])}" target="v{int(top.edst[e])}">'
                    f'<data key="e0">{repr(float(top.elat[e]))}</data>'
                    f'<data key="e1">{repr(float(top.eloss[e]))}</data></edge>')
+    out.append("</graph></graphml>")
+    with open(path, "w") as f:
+        f.write("\n".join(out))
+
+
+_VATTR_TYPES = {"bandwidthdown": "int", "bandwidthup": "int", "asn": "int"}
+
+
+def write_graphml_attrs(top: Topology, path: str) -> None:
+    """GraphML of a topology with all its attributes: vertex ids from
+    ``vertex_ids`` (else "v{i}"), node packetloss + every ``vattrs`` entry, edge
+    latency / packetloss + every ``eattrs`` entry (the completion and collapse
+    tools' output, compute-topology-paths.py:173 / collapse-topology.py:55)."""
+    from xml.sax.saxutils import escape, quoteattr
+    keys = ['<key attr.name="packetloss" attr.type="double" for="node" id="n0"/>']
+    vk = {}
+    for i, name in enumerate(sorted(top.vattrs)):
+        vk[name] = f"n{i + 1}"
+        keys.append(f'<key attr.name="{name}" attr.type="{_VATTR_TYPES.get(name, "string")}" for="node" '
+                    f'id="{vk[name]}"/>')
+    keys += ['<key attr.name="latency" attr.type="double" for="edge" id="e0"/>',
+             '<key attr.name="packetloss" attr.type="double" for="edge" id="e1"/>']
+    ek = {}
+    for i, name in enumerate(sorted(top.eattrs)):
+        ek[name] = f"e{i + 2}"
+        keys.append(f'<key attr.name="{name}" attr.type="double" for="edge" id="{ek[name]}"/>')
+    if top.prefer_direct:
+        keys.append('<key attr.name="preferdirectpaths" attr.type="string" for="graph" id="g0"/>')
+    out = ['<?xml version="1.0" encoding="utf-8"?>', '<graphml xmlns="http://graphml.graphdrawing.org/xmlns">']
+    out += keys
+    out.append(f'<graph edgedefault="{"directed" if top.directed else "undirected"}">')
+    if top.prefer_direct:
+        out.append('<data key="g0">true</data>')
+    ids = top.vertex_ids if top.vertex_ids is not None else [f"v{v}" for v in range(top.n)]
+    for v in range(top.n):
+        d = []
+        if not math.isnan(top.vloss[v]):
+            d.append(f'<data key="n0">{repr(float(top.vloss[v]))}</data>')
+        for name, kid in vk.items():
+            x = top.vattrs[name][v]
+            if x is not None:
+                d.append(f'<data key="{kid}">{escape(str(x))}</data>')
+        out.append(f'<node id={quoteattr(str(ids[v]))}>{"".join(d)}</node>')
+    for e in range(top.m):
+        d = [f'<data key="e0">{repr(float(top.elat[e]))}</data>', f'<data key="e1">{repr(float(top.eloss[e]))}</data>']
+        for name, kid in ek.items():
+            d.append(f'<data key="{kid}">{repr(float(top.eattrs[name][e]))}</data>')
+        out.append(f'<edge source={quoteattr(str(ids[int(top.esrc[e])]))} '
+                   f'target={quoteattr(str(ids[int(top.edst[e])]))}>{"".join(d)}</edge>')
     out.append("</graph></graphml>")
     with open(path, "w") as f:
         f.write("\n".join(out))

@@ -47,7 +47,8 @@ class TableOpts(C.Structure):
                 ("block_begin", C.c_int32), ("block_end", C.c_int32),
                 ("ext_latrel", C.c_void_p),
                 ("ext_next_hop", C.c_void_p), ("ext_hops", C.c_void_p), ("ext_filled", C.c_int32),
-                ("owner_rank", C.c_void_p), ("engine", C.c_int32), ("lanes_per_group", C.c_int32)]
+                ("owner_rank", C.c_void_p), ("engine", C.c_int32), ("lanes_per_group", C.c_int32),
+                ("want_aux", C.c_int32)]
 
 
 class TableLayout(C.Structure):
@@ -78,7 +79,8 @@ EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_
            "spe_table_create", "spe_table_build", "spe_table_build_blocks", "spe_table_profile_enable",
            "spe_table_profile_get", "spe_table_build_stats", "spe_table_layout_get",
            "spe_table_get", "spe_table_download", "spe_lookup_batch", "spe_table_min_latency",
-           "spe_table_key", "spe_table_save", "spe_table_load", "spe_table_free"]
+           "spe_table_key", "spe_table_save", "spe_table_load", "spe_table_free",
+           "spe_graph_set_edge_aux", "spe_table_download_aux"]
 
 _lib = None
 
@@ -118,6 +120,8 @@ def lib():
         L.spe_table_key.argtypes = [P, P]
         L.spe_table_save.argtypes = [P, C.c_char_p]
         L.spe_table_load.argtypes = [P, C.c_char_p]
+        L.spe_graph_set_edge_aux.argtypes = [P, P]
+        L.spe_table_download_aux.argtypes = [P, C.c_int32, C.c_int32, P]
         L.spe_table_free.argtypes = [P]
         L.spe_table_free.restype = None
         _lib = L
@@ -155,6 +159,13 @@ class Graph:
         self.h = h
         self.device = device
 
+    def set_edge_aux(self, edge_aux) -> None:
+        """Per-edge auxiliary attribute (GraphML jitter) folded by want_aux tables."""
+        self._aux = np.ascontiguousarray(edge_aux, np.float64)
+        if self._aux.shape != (self.top.m,):
+            raise ValueError("edge_aux needs one value per edge")
+        _check(lib().spe_graph_set_edge_aux(self.h, _p(self._aux)), "spe_graph_set_edge_aux")
+
     def info(self) -> dict:
         i = GraphInfo()
         _check(lib().spe_graph_info_get(self.h, C.byref(i)), "spe_graph_info_get")
@@ -174,7 +185,7 @@ class PathTable:
 
     def __init__(self, graph: Graph, attached, self_mode: int = SPE_SELF_ROW, force_sssp: bool = False,
                  groups: int = 0, blocks=None, ext=None, ext_filled: bool = False, lanes: int = 0,
-                 owner_order=None, engine: int = 0):
+                 owner_order=None, engine: int = 0, want_aux: bool = False):
         self.graph = graph
         self.attached = np.ascontiguousarray(attached, np.int32)
         self.A = int(self.attached.shape[0])
@@ -184,6 +195,7 @@ class PathTable:
         o.groups_per_launch = int(groups)
         o.lanes_per_group = int(lanes)
         o.engine = int(engine)
+        o.want_aux = int(bool(want_aux))
         if owner_order is not None:   # source-run order (slots) -> rank of each slot
             self._rank = np.empty(self.A, np.int32)
             self._rank[np.asarray(owner_order, np.int64)] = np.arange(self.A, dtype=np.int32)
@@ -242,6 +254,12 @@ class PathTable:
         _check(lib().spe_table_download(self.h, int(row_begin), int(row_end), _p(out["lat"]), _p(out["rel"]),
                                         _p(out["next"]), _p(out["hops"])), "spe_table_download")
         out["ok"] = out["lat"] > -1.0
+        return out
+
+    def download_aux(self, row_begin: int = 0, row_end: Optional[int] = None) -> np.ndarray:
+        row_end = self.A if row_end is None else row_end
+        out = np.empty((row_end - row_begin, self.A), np.float64)
+        _check(lib().spe_table_download_aux(self.h, int(row_begin), int(row_end), _p(out)), "spe_table_download_aux")
         return out
 
     def lookup_batch(self, d_pairs: int, q: int, d_lat: int, d_rel: int, d_ok: int, stream: Optional[int] = None):

@@ -47,6 +47,14 @@ def main():
         sssp_canon_next=diag_cn["next"], sssp_canon_hops=diag_cn["hops"], sssp_canon_rel=diag_cn["rel"],
         sssp_double_ties=diag_ig["double_ties"],
     )
+    # --- completion tool (compute-topology-paths.py) on the shipped topology, every
+    # vertex a POI: networkx restatement (oracle/topology_tools.py) of its worker()
+    import topology_tools as tt
+    jit = top.eattrs["jitter"]
+    pois = np.arange(top.n, dtype=np.int32)
+    clat, cjit, chops = tt.all_rows(top, jit, pois)
+    np.savez_compressed(os.path.join(OUT, "completion_shipped.npz"), ejitter=jit, pois=pois,
+                        lat=clat, jitter=cjit, hops=chops)
     # --- K1/K2: the 1-vertex topologies embedded in the reference's configs
     kats = {}
     for name, rel in [("examples", "resource/examples/shadow.config.xml"),
