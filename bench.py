@@ -151,6 +151,47 @@ def bench_lookup(args):
     print(json.dumps(line), flush=True)
 
 
+def bench_complete(args):
+    """Offline topology completion (compute-topology-paths.py): all
+    ordered POI pairs of a 200k-vertex tiered topology (the C4 generator, edge
+    jitter U(0, 5)), POIs = the first --pois stub vertices (the reference samples
+    CLIENT_SAMPLE_SIZE = 10,000 clients).  Timed: complete_paths end to end (GPU
+    rows + the P x P host copy of latency / jitter / hops).  CPU leg: the
+    reference tool's per-source worker restated with networkx (its own
+    dependency), one core, bounded sample of sources."""
+    from shadow_amd import complete, graphs, spe
+    top = graphs.gen_tiered()
+    rng = np.random.default_rng(7)
+    jit = rng.uniform(0.0, 5.0, top.m)
+    pois = np.arange(20000, 20000 + args.pois, dtype=np.int32)
+    complete.complete_paths(top, pois[:256], jit)   # warm-up (code objects)
+    t0 = time.perf_counter()
+    r = complete.complete_paths(top, pois, jit)
+    el = time.perf_counter() - t0
+    assert not np.isnan(r["lat"]).any()
+    cpu = None
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import topology_tools as tt
+        G = tt.nx_graph(top, jit)
+        done, c0 = 0, time.perf_counter()
+        while time.perf_counter() - c0 < args.cpu_seconds and done < len(pois):
+            tt.source_rows(G, int(pois[done]), pois)
+            done += 1
+        cel = time.perf_counter() - c0
+        cpu = {"value": round(done / cel, 3), "unit": "POI sources/s", "cores": 1, "kind": "port",
+               "sample": f"{done} POI sources x {len(pois)} targets: networkx single_source_dijkstra_path + "
+                         f"per-target latency sum / jitter mean (compute-topology-paths.py:15-38), {cel:.1f} s"}
+    line = {"metric": "topology completion (compute-topology-paths.py): POI source rows/s", "value":
+            round(len(pois) / el, 1), "unit": "POI sources/s", "n_gpus": 1, "higher_is_better": True,
+            "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"tiered BA core 20k + 180k stubs (C4 graph), {len(pois)} POIs, jitter U(0,5)",
+                       "pairs": len(pois) ** 2},
+            "seconds": round(el, 3), "cpu_baseline": cpu,
+            "speedup_vs_cpu_1core": round(len(pois) / el / cpu["value"], 1) if cpu else None}
+    print(json.dumps(line), flush=True)
+
+
 def bench_full_table(args, rank, world, local, dist):
     """Whole path-table precompute (BASELINE north star: C4 on 8 GPUs in < 10 s).
     Rank r owns the contiguous source-block range r of `shares` (= world, or more to
@@ -234,6 +275,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--queries", type=int, default=100_000_000, help="c5: lookups per step")
+    ap.add_argument("--pois", type=int, default=10000, help="complete: POIs")
     ap.add_argument("--pmc-json", default=None, help="per-dispatch HBM bytes from tools/pmc_to_json.py")
     ap.add_argument("--full-table", action="store_true", help="time one whole path-table precompute")
     ap.add_argument("--gather", action="store_true", help="--full-table: RCCL all-gather of latency/reliability")
@@ -242,6 +284,8 @@ def main():
     args = ap.parse_args()
     if args.config == "c5":
         return bench_lookup(args)
+    if args.config == "complete":
+        return bench_complete(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
