@@ -1481,6 +1481,9 @@ __global__ __launch_bounds__(BLOCK) void k_owner_replay(int32_t A, const int32_t
     }
 }
 
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+
+template <int NT>
 __global__ __launch_bounds__(BLOCK) void k_lookup(const int2* __restrict__ pairs, int64_t q, int32_t blk0,
                                                   int32_t blk1, Table tb, double* __restrict__ lat,
                                                   double* __restrict__ rel, uint8_t* __restrict__ ok) {
@@ -1490,12 +1493,23 @@ __global__ __launch_bounds__(BLOCK) void k_lookup(const int2* __restrict__ pairs
         double L = -1.0, R = -1.0;
         if (p.x >= 0 && p.y >= 0 && p.y < tb.A && sb >= blk0 && sb < blk1) {
             const size_t o = tidx(sb - blk0, tb.A, p.y, p.x & (WAVE - 1));
-            const double2 e = tb.lr[o];
-            L = e.x;
-            R = e.y;
+            if constexpr (NT) {   // no L2 allocation for a record that is never re-read
+                const dvec2 e = __builtin_nontemporal_load(reinterpret_cast<const dvec2*>(tb.lr + o));
+                L = e.x;
+                R = e.y;
+            } else {
+                const double2 e = tb.lr[o];
+                L = e.x;
+                R = e.y;
+            }
         }
-        lat[i] = L;
-        rel[i] = R;
+        if constexpr (NT) {
+            __builtin_nontemporal_store(L, lat + i);
+            __builtin_nontemporal_store(R, rel + i);
+        } else {
+            lat[i] = L;
+            rel[i] = R;
+        }
         ok[i] = L > -1.0 ? 1 : 0;   // topology_isRoutable: getLatency > -1
     }
 }
@@ -2401,8 +2415,8 @@ int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, doub
     if (q == 0) return SPE_OK;
     HIP_TRY(hipSetDevice(t->g->device));
     hipStream_t s = stream ? (hipStream_t)stream : t->stream;
-    k_lookup<<<grid_for(q, BLOCK, 16384), BLOCK, 0, s>>>((const int2*)d_pairs, q, t->blk0, t->blk1, t->tb, d_latency,
-                                                        d_reliability, d_ok);
+    k_lookup<1><<<grid_for(q, BLOCK, 16384), BLOCK, 0, s>>>((const int2*)d_pairs, q, t->blk0, t->blk1, t->tb,
+                                                           d_latency, d_reliability, d_ok);
     HIP_TRY(hipGetLastError());
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return SPE_OK;
