@@ -247,6 +247,7 @@ struct Flags {
     uint8_t* in_cur;       // [group][in-CSR entry] changed in-neighbour (consumed)
     uint8_t* in_next;
     int32_t* any_changed;  // set when some vertex changed this round
+    const int32_t* prev_changed;   // the previous round's flag: 0 = converged, the round is a no-op
 };
 
 template <int L>
@@ -466,6 +467,7 @@ __device__ __forceinline__ uint32_t byte_mask(uint64_t w) {
 template <int L, int INFL, int OCC = 1>
 __global__ __launch_bounds__(BLOCK, OCC) void k_relax(int32_t total, int32_t n, const int32_t* __restrict__ srcv,
                                                  DevGraph G, State st, Flags fl) {
+    if (*fl.prev_changed == 0) return;   // converged: rounds are enqueued ahead of the host's check
     constexpr int V = Sub<L>::V;
     const int32_t lane = threadIdx.x & (WAVE - 1);
     const int32_t sub = lane / L, j = lane % L, base = sub * L;
@@ -526,6 +528,7 @@ struct Partial {                  // [group][segment][L]
 template <int L, int INFL = Sub<L>::INFL>
 __global__ __launch_bounds__(BLOCK) void k_heavy_partial(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
                                                          DevGraph G, State st, HeavyPlan hp, Partial pp, Flags fl) {
+    if (*fl.prev_changed == 0) return;
     constexpr int V = Sub<L>::V;
     const int32_t lane = threadIdx.x & (WAVE - 1);
     const int32_t sub = lane / L, j = lane % L, base = sub * L;
@@ -584,6 +587,7 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_partial(int32_t groups, int32_t
 template <int L>
 __global__ __launch_bounds__(BLOCK) void k_heavy_combine(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
                                                          DevGraph G, State st, HeavyPlan hp, Partial pp, Flags fl) {
+    if (*fl.prev_changed == 0) return;
     constexpr int V = Sub<L>::V;
     const int32_t lane = threadIdx.x & (WAVE - 1);
     const int32_t sub = lane / L, j = lane % L, base = sub * L;
@@ -1571,6 +1575,7 @@ struct spe_table {
     Partial pp{};
     int32_t* counts = nullptr;   // per round: 1 if any vertex changed
     int32_t max_iters = 0;
+    int32_t last_rounds = 0;      // rounds the previous batch needed (sizes the next chunk)
     int32_t* d_srcv = nullptr;     // batch sources, original ids (-1 = padding)
     int32_t* d_srcc = nullptr;     // relaxation ids (-2 = pruned pendant source, -1 = padding)
     int32_t* h_srcv = nullptr;     // pinned staging for both
@@ -2059,7 +2064,8 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     TRY(dev_alloc(t->allocs, &t->d_min, 1));
 #undef TRY
     HIP_TRY(hipHostMalloc((void**)&t->h_srcv, 2 * G * WAVE * sizeof(int32_t), hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void**)&t->h_counts, 64 * sizeof(int32_t), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&t->h_counts, std::max<size_t>(64, (size_t)t->max_iters + 2) * sizeof(int32_t),
+                          hipHostMallocDefault));
     HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
     *out = t;
     return SPE_OK;
@@ -2120,6 +2126,7 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus < 1) cus = 256;
     const int relax_grid = (grid_for((total + 7) / 8 * WAVE, BLOCK, per_cu * cus) + 7) & ~7;
     HIP_TRY(hipMemsetAsync(t->counts, 0, sizeof(int32_t) * ((size_t)t->max_iters + 2), s));
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)t->counts, 1, 1, s));   // round 0 (the sources) changed
     for (int i = 0; i < 2; ++i) {   // consumers clear what they read; this only guards a failed batch
         HIP_TRY(hipMemsetAsync(t->inflag[i], 0, (size_t)groups * std::max(1, nrel), s));
         HIP_TRY(hipMemsetAsync(t->mark[i], 0, ((size_t)total + 8) & ~(size_t)7, s));
@@ -2137,13 +2144,17 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
                                                                      t->hmark[1], t->inflag[1]);
     }
     const int64_t subs_per_wave = WAVE / L;
+    // Rounds are enqueued in chunks sized by the previous batch's round count
+    // (batches of one graph converge in similar counts); rounds after the
+    // converged one exit at once, so one host check per batch is typical.
     int32_t it = 1;
-    int32_t check_every = 8;
+    int32_t chunk = t->last_rounds > 0 ? t->last_rounds + 1 : 8;
     for (;;) {
-        for (int32_t q = 0; q < check_every; ++q, ++it) {
+        for (int32_t q = 0; q < chunk; ++q, ++it) {
             if (it > t->max_iters) return fail(SPE_ESTATE, "relaxation did not converge");
             Flags fl{t->mark[it & 1],   t->mark[(it + 1) & 1],   t->hmark[it & 1],
-                     t->hmark[(it + 1) & 1], t->inflag[it & 1], t->inflag[(it + 1) & 1], t->counts + it};
+                     t->hmark[(it + 1) & 1], t->inflag[it & 1], t->inflag[(it + 1) & 1], t->counts + it,
+                     t->counts + it - 1};
             {
                 LaunchTimer lt(t, s, SPE_K_RELAX);
                 k_relax<L, INFL, OCC><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev, t->st, fl);
@@ -2158,20 +2169,18 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
                                                                                       t->st, g->hp, t->pp, fl);
             }
         }
-        HIP_TRY(hipMemcpyAsync(t->h_counts, t->counts + it - 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(t->h_counts, t->counts, sizeof(int32_t) * (size_t)it, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        t->stats.launches += check_every;
-        if (t->h_counts[0] == 0) break;
-        check_every = 4;
+        t->stats.launches += chunk;
+        if (t->h_counts[it - 1] == 0) break;
+        chunk = 2;
     }
-    // rounds that changed something (work accounting)
-    const int32_t nit = it;
-    if ((int32_t)t->h_hist.size() < nit + 1) t->h_hist.resize(nit + 1);
-    HIP_TRY(hipMemcpy(t->h_hist.data(), t->counts, sizeof(int32_t) * (nit + 1), hipMemcpyDeviceToHost));
-    int32_t active_rounds = 0;
-    for (int32_t i = 1; i <= nit; ++i) active_rounds += t->h_hist[i];
-    t->stats.active_rounds += active_rounds;
-    t->stats.iterations += it - 1;
+    // the first round that changed nothing ends the relaxation (work accounting)
+    int32_t rounds = 1;
+    while (rounds < it && t->h_counts[rounds] != 0) ++rounds;
+    t->stats.active_rounds += rounds - 1;
+    t->stats.iterations += rounds;
+    t->last_rounds = rounds;
     return SPE_OK;
 }
 
