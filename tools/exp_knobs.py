@@ -10,7 +10,7 @@ top = graphs.gen_ba(50000, 3, 3) if cfg == "c3" else graphs.gen_tiered()
 att = np.arange(top.n, dtype=np.int32) if cfg == "c3" else graphs.tiered_attached(top)
 nb = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 g = spe.Graph(top, device=0)
-t = spe.PathTable(g, att, blocks=(0, nb))
+t = spe.PathTable(g, att, blocks=(0, nb), groups=int(os.environ.get("X_GROUPS", "0")))
 t.build_blocks(0, 16)
 t.profile(True)
 t0 = time.perf_counter()
