@@ -192,6 +192,16 @@ int spe_table_get(const spe_table* t, int32_t s_slot, int32_t t_slot, spe_entry*
  * any output pointer may be NULL. */
 int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, double* latency,
                        double* reliability, int32_t* next_hop, int32_t* hops);
+/* Blocked min-plus Floyd-Warshall over the relaxation graph (vertex ids as in
+ * spe_graph_info.n_relax_vertices: undirected pendants pruned), the north
+ * star's dense-regime algorithm, kept as a measured comparison engine and an
+ * independent distance check.  d_dist: caller device buffer of ld x ld doubles
+ * (ld = a multiple of 64 >= n_relax_vertices); d_next (optional, n x n int32):
+ * the first hop, argmin over out-neighbours u of w(i,u) + dist(u,j).  FW sums
+ * path segments in its own association order, so distances agree with the
+ * table's path-order folds only to rounding (the table is what is bit-exact).
+ * `seconds`: device time of the closure (init + pivot steps). */
+int spe_fw_apsp(spe_graph* g, double* d_dist, int64_t ld, int32_t* d_next, void* stream, double* seconds);
 /* Owned rows [row_begin,row_end) of the want_aux field, row-major, to host. */
 int spe_table_download_aux(const spe_table* t, int32_t row_begin, int32_t row_end, double* aux);
 /* Batched per-packet lookups against the HBM-resident table.  d_pairs holds q

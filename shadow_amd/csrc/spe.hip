@@ -1530,6 +1530,144 @@ __global__ __launch_bounds__(BLOCK) void k_min_latency(const double2* __restrict
         atomicMin(out, (unsigned long long)__double_as_longlong(m));  // positive doubles order as integers
 }
 
+
+// ------------------------------------------------------------------------
+// Blocked min-plus Floyd-Warshall (the north star's dense C2 algorithm), kept as
+// a measured comparison engine and an independent distance check: distances
+// over the relaxation graph in FW association order (so within rounding of,
+// not bit-equal to, the path-order folds the table holds) plus a next hop
+// derived from them.  64 x 64 tiles, 256 threads, 4 x 4 elements per thread;
+// per pivot block kb: the diagonal tile, then its row / column panels, then
+// every other tile as a 64-deep min-plus product from two LDS-staged panels.
+// FP64 VALU bound (add + min per relaxation; no MFMA: (min, +) is no FMA).
+#define FWB 64
+__device__ __forceinline__ void fw_load(double (*T)[FWB + 1], const double* __restrict__ D, int64_t ld, int32_t bi,
+                                        int32_t bj) {
+    for (int32_t e = threadIdx.x; e < FWB * FWB; e += 256) {
+        const int32_t r = e / FWB, c = e % FWB;
+        T[r][c] = D[((int64_t)bi * FWB + r) * ld + (int64_t)bj * FWB + c];
+    }
+}
+__device__ __forceinline__ void fw_store(double (*T)[FWB + 1], double* __restrict__ D, int64_t ld, int32_t bi,
+                                         int32_t bj) {
+    for (int32_t e = threadIdx.x; e < FWB * FWB; e += 256) {
+        const int32_t r = e / FWB, c = e % FWB;
+        D[((int64_t)bi * FWB + r) * ld + (int64_t)bj * FWB + c] = T[r][c];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fw_init(int32_t n, int64_t ld, DevGraph G, double* __restrict__ D) {
+    const int64_t total = ld * ld;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        const int64_t i = e / ld, j = e % ld;
+        D[e] = (i == j) ? 0.0 : INF;
+    }
+}
+__global__ __launch_bounds__(256) void k_fw_edges(int32_t nrel, int64_t ld, DevGraph G, double* __restrict__ D) {
+    const int32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k < nrel) D[(int64_t)G.icol[k] * ld + G.irow[k]] = G.iw[k];   // merged: one entry per ordered pair
+}
+
+// phase 1 (diagonal tile, launch with one block, b0 = 0) and phase 2 (its row /
+// column panels, a second launch with b0 = 1): sequential in k
+__global__ __launch_bounds__(256) void k_fw_panel(int32_t kb, int32_t nb, int64_t ld, double* __restrict__ D,
+                                                  int32_t b0) {
+    __shared__ double Dk[FWB][FWB + 1];
+    __shared__ double T[FWB][FWB + 1];
+    const int32_t b = b0 + blockIdx.x;   // 0: diagonal; 1..nb-1: row panel; nb..2nb-2: column panel
+    fw_load(Dk, D, ld, kb, kb);
+    __syncthreads();
+    if (b == 0) {
+        for (int32_t k = 0; k < FWB; ++k) {
+            for (int32_t e = threadIdx.x; e < FWB * FWB; e += 256) {
+                const int32_t r = e / FWB, c = e % FWB;
+                const double a = Dk[r][k] + Dk[k][c];
+                if (a < Dk[r][c]) Dk[r][c] = a;
+            }
+            __syncthreads();
+        }
+        fw_store(Dk, D, ld, kb, kb);
+        return;
+    }
+    const bool row = b < nb;
+    int32_t o = row ? b - 1 : b - nb;
+    if (o >= kb) ++o;   // skip the diagonal
+    if (row) fw_load(T, D, ld, kb, o);
+    else fw_load(T, D, ld, o, kb);
+    __syncthreads();
+    for (int32_t k = 0; k < FWB; ++k) {
+        for (int32_t e = threadIdx.x; e < FWB * FWB; e += 256) {
+            const int32_t r = e / FWB, c = e % FWB;
+            const double a = row ? Dk[r][k] + T[k][c] : T[r][k] + Dk[k][c];
+            if (a < T[r][c]) T[r][c] = a;
+        }
+        __syncthreads();
+    }
+    if (row) fw_store(T, D, ld, kb, o);
+    else fw_store(T, D, ld, o, kb);
+}
+
+// phase 3: every tile off the pivot row / column, 4 x 4 per thread in registers
+__global__ __launch_bounds__(256) void k_fw_rest(int32_t kb, int32_t nb, int64_t ld, double* __restrict__ D) {
+    __shared__ __align__(16) double At[FWB][FWB];   // At[k][r] = D(bi, kb)[r][k]
+    __shared__ __align__(16) double Bk[FWB][FWB];   // Bk[k][c] = D(kb, bj)[k][c]
+    int32_t bi = blockIdx.x / (nb - 1), bj = blockIdx.x % (nb - 1);
+    if (bi >= kb) ++bi;
+    if (bj >= kb) ++bj;
+    for (int32_t e = threadIdx.x; e < FWB * FWB; e += 256) {
+        const int32_t r = e / FWB, c = e % FWB;
+        At[c][r] = D[((int64_t)bi * FWB + r) * ld + (int64_t)kb * FWB + c];
+        Bk[r][c] = D[((int64_t)kb * FWB + r) * ld + (int64_t)bj * FWB + c];
+    }
+    const int32_t tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+    double d[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) d[r][c] = D[((int64_t)bi * FWB + ty * 4 + r) * ld + (int64_t)bj * FWB + tx * 4 + c];
+    __syncthreads();
+#pragma unroll 4
+    for (int32_t k = 0; k < FWB; ++k) {
+        const double2 a01 = *reinterpret_cast<const double2*>(&At[k][ty * 4]);
+        const double2 a23 = *reinterpret_cast<const double2*>(&At[k][ty * 4 + 2]);
+        const double2 b01 = *reinterpret_cast<const double2*>(&Bk[k][tx * 4]);
+        const double2 b23 = *reinterpret_cast<const double2*>(&Bk[k][tx * 4 + 2]);
+        const double a[4] = {a01.x, a01.y, a23.x, a23.y}, bb[4] = {b01.x, b01.y, b23.x, b23.y};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) d[r][c] = fmin(d[r][c], a[r] + bb[c]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) D[((int64_t)bi * FWB + ty * 4 + r) * ld + (int64_t)bj * FWB + tx * 4 + c] = d[r][c];
+}
+
+// next hop from the closure: argmin over out-neighbours u of i of w(i,u) + D[u][j]
+// (first minimum in out-list order); -1 when j is unreachable, j itself for i == j
+__global__ __launch_bounds__(256) void k_fw_next(int32_t n, int64_t ld, DevGraph G, const double* __restrict__ D,
+                                                 int32_t* __restrict__ nxt) {
+    const int64_t total = (int64_t)n * n;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        const int32_t i = (int32_t)(e / n), j = (int32_t)(e % n);
+        int32_t best = -1;
+        if (i == j) {
+            best = i;
+        } else if (D[(int64_t)i * ld + j] < INF) {
+            double bv = INF;
+            for (int32_t k = G.optr[i]; k < G.optr[i + 1]; ++k) {
+                const int32_t u = G.ocol[k];
+                const double v = G.ow[k] + D[(int64_t)u * ld + j];
+                if (v < bv) {
+                    bv = v;
+                    best = u;
+                }
+            }
+        }
+        nxt[(int64_t)i * n + j] = best;
+    }
+}
 }  // namespace
 
 // ================================================================== host side
@@ -2428,6 +2566,39 @@ int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, doub
                                                            d_latency, d_reliability, d_ok);
     HIP_TRY(hipGetLastError());
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
+    return SPE_OK;
+}
+
+int spe_fw_apsp(spe_graph* g, double* d_dist, int64_t ld, int32_t* d_next, void* stream, double* seconds) {
+    if (!g || !d_dist) return fail(SPE_EINVAL, "NULL argument");
+    const int32_t n = g->hg.nc;
+    const int32_t nb = (n + FWB - 1) / FWB;
+    if (ld < (int64_t)nb * FWB) return fail(SPE_EINVAL, "ld must be >= the relaxation vertex count rounded up to 64");
+    if (ld % FWB) return fail(SPE_EINVAL, "ld must be a multiple of 64");
+    HIP_TRY(hipSetDevice(g->device));
+    hipStream_t s = (hipStream_t)stream;
+    hipEvent_t a, b;
+    HIP_TRY(hipEventCreate(&a));
+    HIP_TRY(hipEventCreate(&b));
+    HIP_TRY(hipEventRecord(a, s));
+    k_fw_init<<<grid_for(ld * ld, 256, 16384), 256, 0, s>>>(n, ld, g->dev, d_dist);
+    const int32_t nrel = (int32_t)g->hg.icol.size();
+    if (nrel > 0) k_fw_edges<<<(nrel + 255) / 256, 256, 0, s>>>(nrel, ld, g->dev, d_dist);
+    // padding rows / columns stay +inf off the diagonal: they never shorten a path
+    for (int32_t kb = 0; kb < nb; ++kb) {
+        k_fw_panel<<<1, 256, 0, s>>>(kb, nb, ld, d_dist, 0);
+        if (nb > 1) k_fw_panel<<<2 * nb - 2, 256, 0, s>>>(kb, nb, ld, d_dist, 1);
+        if (nb > 1) k_fw_rest<<<(nb - 1) * (nb - 1), 256, 0, s>>>(kb, nb, ld, d_dist);
+    }
+    HIP_TRY(hipEventRecord(b, s));
+    if (d_next) k_fw_next<<<grid_for((int64_t)n * n, 256, 16384), 256, 0, s>>>(n, ld, g->dev, d_dist, d_next);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, a, b));
+    if (seconds) *seconds = ms / 1e3;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
     return SPE_OK;
 }
 

@@ -80,7 +80,7 @@ EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_
            "spe_table_profile_get", "spe_table_build_stats", "spe_table_layout_get",
            "spe_table_get", "spe_table_download", "spe_lookup_batch", "spe_table_min_latency",
            "spe_table_key", "spe_table_save", "spe_table_load", "spe_table_free",
-           "spe_graph_set_edge_aux", "spe_table_download_aux"]
+           "spe_graph_set_edge_aux", "spe_table_download_aux", "spe_fw_apsp"]
 
 _lib = None
 
@@ -122,6 +122,7 @@ def lib():
         L.spe_table_load.argtypes = [P, C.c_char_p]
         L.spe_graph_set_edge_aux.argtypes = [P, P]
         L.spe_table_download_aux.argtypes = [P, C.c_int32, C.c_int32, P]
+        L.spe_fw_apsp.argtypes = [P, P, C.c_int64, P, P, P]
         L.spe_table_free.argtypes = [P]
         L.spe_table_free.restype = None
         _lib = L
@@ -165,6 +166,13 @@ class Graph:
         if self._aux.shape != (self.top.m,):
             raise ValueError("edge_aux needs one value per edge")
         _check(lib().spe_graph_set_edge_aux(self.h, _p(self._aux)), "spe_graph_set_edge_aux")
+
+    def fw_apsp(self, d_dist: int, ld: int, d_next: int = 0, stream: int = 0) -> float:
+        """Blocked min-plus Floyd-Warshall into caller device buffers; returns device seconds."""
+        sec = C.c_double(0)
+        _check(lib().spe_fw_apsp(self.h, C.c_void_p(d_dist), int(ld), C.c_void_p(d_next or None),
+                                 C.c_void_p(stream or None), C.byref(sec)), "spe_fw_apsp")
+        return float(sec.value)
 
     def info(self) -> dict:
         i = GraphInfo()

@@ -29,6 +29,8 @@ tail -1 $O/bench_c4.log
 timeout -k 10 200 python -u bench.py --config c5 --steps 10 --warmup 2 > $O/bench_c5.log 2>&1 || { tail -20 $O/bench_c5.log; exit 1; }
 tail -1 $O/bench_c5.log
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $O/kt_c5 -o run --output-format csv -- python bench.py --config c5 --steps 4 --warmup 1 > $O/kt_c5.log 2>&1
+timeout -k 10 200 python -u bench.py --config c2fw > $O/bench_c2fw.log 2>&1 || { tail -20 $O/bench_c2fw.log; exit 1; }
+tail -1 $O/bench_c2fw.log
 timeout -k 10 300 python -u bench.py --config complete > $O/bench_complete.log 2>&1 || { tail -20 $O/bench_complete.log; exit 1; }
 tail -1 $O/bench_complete.log
 echo done
