@@ -82,21 +82,23 @@ def complete_paths(top: graphs.Topology, pois: Sequence[int], jitter: Optional[n
     chunk = max(1, min(nblk, int(max_table_bytes // per_block)))
     lat = np.empty((P, P))
     jit = np.empty((P, P))
-    hops = np.empty((P, P), np.int64)
+    hops = np.empty((P, P), np.int32)
     for b0 in range(0, nblk, chunk):
         b1 = min(nblk, b0 + chunk)
         t = spe.PathTable(g, pois, force_sssp=True, want_aux=True, blocks=(b0, b1))
         t.build()
         r0, r1 = b0 * 64, min(P, b1 * 64)
-        d = t.download(r0, r1)
+        d = t.download(r0, r1, fields=("lat", "hops"))
         aux = t.download_aux(r0, r1)
         t.close()
-        ok = d["ok"]
-        h = d["hops"].astype(np.int64)
-        lat[r0:r1] = np.where(ok, d["lat"], np.nan)
-        with np.errstate(invalid="ignore", divide="ignore"):
-            jit[r0:r1] = np.where(ok & (h > 0), aux / np.maximum(h, 1), np.nan)
-        hops[r0:r1] = np.where(ok, h, -1)
+        bad = ~d["ok"]
+        h = d["hops"]
+        lat[r0:r1] = d["lat"]
+        lat[r0:r1][bad] = np.nan
+        np.divide(aux, h, out=jit[r0:r1], where=h > 0)
+        jit[r0:r1][bad | (h <= 0)] = np.nan
+        hops[r0:r1] = h
+        hops[r0:r1][bad] = -1
     idx = np.arange(P)
     lat[idx, idx] = SELF_LATENCY
     jit[idx, idx] = SELF_JITTER

@@ -2497,62 +2497,105 @@ int spe_table_get(const spe_table* t, int32_t s_slot, int32_t t_slot, spe_entry*
     return SPE_OK;
 }
 
-int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, double* latency,
-                       double* reliability, int32_t* next_hop, int32_t* hops) {
+// SB64 block -> 64 row-major rows, on the device (a 64 x 64 LDS tile per
+// workgroup: coalesced reads of the 64 interleaved sources, coalesced row writes).
+__global__ __launch_bounds__(256) void k_sb64_rows(int32_t A, const double2* __restrict__ lr,
+                                                   const int32_t* __restrict__ nx, const uint16_t* __restrict__ hp,
+                                                   const double* __restrict__ ax, double* __restrict__ olat,
+                                                   double* __restrict__ orel, int32_t* __restrict__ onext,
+                                                   int32_t* __restrict__ ohops, double* __restrict__ oaux) {
+    __shared__ double T0[64][65], T1[64][65];
+    __shared__ int32_t I0[64][65], I1[64][65];
+    const int32_t j0 = blockIdx.x * 64;
+    for (int32_t e = threadIdx.x; e < 64 * 64; e += 256) {   // e = (target jj, lane l), lane fastest
+        const int32_t jj = e / 64, l = e % 64, j = j0 + jj;
+        if (j >= A) continue;
+        const size_t o = (size_t)j * WAVE + l;
+        if (olat || orel) {
+            const double2 v = lr[o];
+            T0[l][jj] = v.x;
+            T1[l][jj] = v.y;
+        }
+        if (oaux) T0[l][jj] = ax[o];
+        if (onext) I0[l][jj] = nx[o];
+        if (ohops) I1[l][jj] = hp[o];
+    }
+    __syncthreads();
+    for (int32_t e = threadIdx.x; e < 64 * 64; e += 256) {   // e = (lane l, target jj), target fastest
+        const int32_t l = e / 64, jj = e % 64, j = j0 + jj;
+        if (j >= A) continue;
+        const size_t o = (size_t)l * A + j;
+        if (olat) olat[o] = T0[l][jj];
+        if (orel) orel[o] = T1[l][jj];
+        if (oaux) oaux[o] = T0[l][jj];
+        if (onext) onext[o] = I0[l][jj];
+        if (ohops) ohops[o] = I1[l][jj];
+    }
+}
+
+// Owned rows [row_begin, row_end) to host, row-major: each 64-source block is
+// transposed on the device, then copied as one contiguous span per field.
+// (aux is requested alone: it shares the first staging tile with latency.)
+static int download_rows(const spe_table* t, int32_t row_begin, int32_t row_end, double* latency,
+                         double* reliability, int32_t* next_hop, int32_t* hops, double* aux) {
     if (!t) return fail(SPE_EINVAL, "NULL table");
     if (!t->built) return fail(SPE_ESTATE, "table not built");
     if (row_begin < t->blk0 * WAVE || row_end > std::min(t->A, t->blk1 * WAVE) || row_begin > row_end)
         return fail(SPE_EINVAL, "row range not owned by this table");
+    if (row_begin == row_end) return SPE_OK;
     HIP_TRY(hipSetDevice(t->g->device));
     const int32_t A = t->A;
-    const int32_t b0 = row_begin / WAVE, b1 = (row_end + WAVE - 1) / WAVE;
     const size_t blk_elems = (size_t)A * WAVE;
-    std::vector<double2> blr(blk_elems);
-    std::vector<int32_t> bn(blk_elems);
-    std::vector<uint16_t> bh(blk_elems);
-    for (int32_t b = b0; b < b1; ++b) {
+    std::vector<void*> tmp;
+    double *dl = nullptr, *dr = nullptr, *da = nullptr;
+    int32_t *dn = nullptr, *dh = nullptr;
+    int r = SPE_OK;
+    if (latency && !r) r = dev_alloc(tmp, &dl, blk_elems);
+    if (reliability && !r) r = dev_alloc(tmp, &dr, blk_elems);
+    if (aux && !r) r = dev_alloc(tmp, &da, blk_elems);
+    if (next_hop && !r) r = dev_alloc(tmp, &dn, blk_elems);
+    if (hops && !r) r = dev_alloc(tmp, &dh, blk_elems);
+    hipStream_t s = t->stream;
+    for (int32_t b = row_begin / WAVE; !r && b < (row_end + WAVE - 1) / WAVE; ++b) {
         const size_t off = (size_t)(b - t->blk0) * blk_elems;
-        if (latency || reliability)
-            HIP_TRY(hipMemcpy(blr.data(), t->tb.lr + off, blk_elems * 16, hipMemcpyDeviceToHost));
-        if (next_hop) HIP_TRY(hipMemcpy(bn.data(), t->tb.next + off, blk_elems * 4, hipMemcpyDeviceToHost));
-        if (hops) HIP_TRY(hipMemcpy(bh.data(), t->tb.hops + off, blk_elems * 2, hipMemcpyDeviceToHost));
-        for (int32_t l = 0; l < WAVE; ++l) {
-            const int32_t row = b * WAVE + l;
-            if (row < row_begin || row >= row_end) continue;
-            const size_t ro = (size_t)(row - row_begin) * A;
-            for (int32_t j = 0; j < A; ++j) {
-                const size_t src = (size_t)j * WAVE + l;
-                if (latency) latency[ro + j] = blr[src].x;
-                if (reliability) reliability[ro + j] = blr[src].y;
-                if (next_hop) next_hop[ro + j] = bn[src];
-                if (hops) hops[ro + j] = bh[src];
-            }
+        k_sb64_rows<<<(A + 63) / 64, 256, 0, s>>>(A, t->tb.lr + off, t->tb.next + off, t->tb.hops + off,
+                                                  aux ? t->tb.aux + off : nullptr, dl, dr, dn, dh, da);
+        if (hipGetLastError() != hipSuccess) {
+            r = fail(SPE_EHIP, "k_sb64_rows launch");
+            break;
         }
+        // the rows of this block inside [row_begin, row_end)
+        const int32_t r0 = std::max(row_begin, b * WAVE), r1 = std::min(row_end, (b + 1) * WAVE);
+        const size_t src = (size_t)(r0 - b * WAVE) * A, dst = (size_t)(r0 - row_begin) * A;
+        const size_t cnt = (size_t)(r1 - r0) * A;
+        auto cp = [&](void* h, const void* d, size_t esz) -> int {
+            if (!h) return SPE_OK;
+            if (hipMemcpyAsync((char*)h + dst * esz, (const char*)d + src * esz, cnt * esz, hipMemcpyDeviceToHost,
+                               s) != hipSuccess)
+                return fail(SPE_EHIP, "hipMemcpyAsync (download)");
+            return SPE_OK;
+        };
+        r = cp(latency, dl, 8);
+        if (!r) r = cp(reliability, dr, 8);
+        if (!r) r = cp(aux, da, 8);
+        if (!r) r = cp(next_hop, dn, 4);
+        if (!r) r = cp(hops, dh, 4);
+        if (!r && hipStreamSynchronize(s) != hipSuccess) r = fail(SPE_EHIP, "download sync");
     }
-    return SPE_OK;
+    (void)hipStreamSynchronize(s);
+    for (void* p : tmp) (void)hipFree(p);
+    return r;
+}
+
+int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, double* latency,
+                       double* reliability, int32_t* next_hop, int32_t* hops) {
+    return download_rows(t, row_begin, row_end, latency, reliability, next_hop, hops, nullptr);
 }
 
 int spe_table_download_aux(const spe_table* t, int32_t row_begin, int32_t row_end, double* aux) {
     if (!t || !aux) return fail(SPE_EINVAL, "NULL argument");
     if (!t->tb.aux) return fail(SPE_ESTATE, "table was created without want_aux");
-    if (!t->built) return fail(SPE_ESTATE, "table not built");
-    if (row_begin < t->blk0 * WAVE || row_end > std::min(t->A, t->blk1 * WAVE) || row_begin > row_end)
-        return fail(SPE_EINVAL, "row range not owned by this table");
-    HIP_TRY(hipSetDevice(t->g->device));
-    const int32_t A = t->A;
-    const size_t blk_elems = (size_t)A * WAVE;
-    std::vector<double> ba(blk_elems);
-    for (int32_t b = row_begin / WAVE; b < (row_end + WAVE - 1) / WAVE; ++b) {
-        HIP_TRY(hipMemcpy(ba.data(), t->tb.aux + (size_t)(b - t->blk0) * blk_elems, blk_elems * 8,
-                          hipMemcpyDeviceToHost));
-        for (int32_t l = 0; l < WAVE; ++l) {
-            const int32_t row = b * WAVE + l;
-            if (row < row_begin || row >= row_end) continue;
-            double* o = aux + (size_t)(row - row_begin) * A;
-            for (int32_t j = 0; j < A; ++j) o[j] = ba[(size_t)j * WAVE + l];
-        }
-    }
-    return SPE_OK;
+    return download_rows(t, row_begin, row_end, nullptr, nullptr, nullptr, nullptr, aux);
 }
 
 int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, double* d_latency,

@@ -254,14 +254,16 @@ class PathTable:
         _check(lib().spe_table_get(self.h, int(s_slot), int(t_slot), C.byref(e)), "spe_table_get")
         return {"latency": e.latency, "reliability": e.reliability, "next_hop": e.next_hop, "hops": e.hops}
 
-    def download(self, row_begin: int = 0, row_end: Optional[int] = None) -> dict:
+    def download(self, row_begin: int = 0, row_end: Optional[int] = None,
+                 fields=("lat", "rel", "next", "hops")) -> dict:
         row_end = self.A if row_end is None else row_end
         nr = row_end - row_begin
-        out = {"lat": np.empty((nr, self.A), np.float64), "rel": np.empty((nr, self.A), np.float64),
-               "next": np.empty((nr, self.A), np.int32), "hops": np.empty((nr, self.A), np.int32)}
-        _check(lib().spe_table_download(self.h, int(row_begin), int(row_end), _p(out["lat"]), _p(out["rel"]),
-                                        _p(out["next"]), _p(out["hops"])), "spe_table_download")
-        out["ok"] = out["lat"] > -1.0
+        types = {"lat": np.float64, "rel": np.float64, "next": np.int32, "hops": np.int32}
+        out = {f: np.empty((nr, self.A), types[f]) for f in fields}
+        _check(lib().spe_table_download(self.h, int(row_begin), int(row_end), _p(out.get("lat")), _p(out.get("rel")),
+                                        _p(out.get("next")), _p(out.get("hops"))), "spe_table_download")
+        if "lat" in out:
+            out["ok"] = out["lat"] > -1.0
         return out
 
     def download_aux(self, row_begin: int = 0, row_end: Optional[int] = None) -> np.ndarray:
