@@ -96,3 +96,38 @@ def test_want_aux_argument_checks():
     t.build()
     with pytest.raises(spe.SpeError):
         t.download_aux()
+
+
+def test_complete_paths_directed_graph():
+    """Directed topologies: rows follow out-edges; the aux fold walks the same
+    parent edges (the networkx oracle restates the tool on an undirected nx.Graph,
+    so here the check is against the C oracle's directed rows plus a direct
+    path-order jitter sum along its routes)."""
+    from oracle import Oracle
+    top = graphs.gen_random_small(150, 500, 8, directed=True)
+    jit = np.random.default_rng(8).uniform(0.0, 3.0, top.m)
+    pois = np.arange(0, top.n, 2, dtype=np.int32)
+    got = complete.complete_paths(top, pois, jit)
+    ref = Oracle(top).rows(pois, pois, force_sssp=True, tie_mode=1)
+    off = ~np.eye(len(pois), dtype=bool)
+    assert np.array_equal(got["lat"][off], ref["lat"][off])
+    assert np.array_equal(got["hops"][off], ref["hops"][off])
+    # jitter: path-order sum over the oracle's Dijkstra parent edges (no parallel edges here)
+    o = Oracle(top)
+    for i in range(0, len(pois), 7):
+        s = int(pois[i])
+        dist, peid, _ = o.dijkstra(s)
+        for jx in range(0, len(pois), 5):
+            t = int(pois[jx])
+            if s == t:
+                continue
+            edges = []
+            x = t
+            while x != s:
+                e = int(peid[x])
+                edges.append(e)
+                x = int(top.esrc[e])
+            a = 0.0
+            for e in reversed(edges):
+                a += jit[e]
+            assert got["jitter"][i, jx] == a / len(edges)

@@ -12,10 +12,11 @@ from shadow_amd import graphs, spe
 pytestmark = [pytest.mark.gpu, pytest.mark.engine_fixed]
 
 
-@pytest.mark.parametrize("n,extra,seed", [(70, 150, 1), (300, 900, 2), (700, 1500, 3)])
-def test_fw_distances_and_next_hop(n, extra, seed, monkeypatch):
+@pytest.mark.parametrize("n,extra,seed,directed", [(70, 150, 1, False), (300, 900, 2, False), (700, 1500, 3, False),
+                                                   (200, 700, 5, True)])
+def test_fw_distances_and_next_hop(n, extra, seed, directed, monkeypatch):
     monkeypatch.setenv("SPE_NO_PRUNE", "1")   # FW runs over relaxation ids: keep them = vertex ids
-    top = graphs.gen_random_small(n, extra, seed)
+    top = graphs.gen_random_small(n, extra, seed, directed=directed)
     g = spe.Graph(top)
     ld = (n + 63) // 64 * 64
     D = torch.empty(ld * ld, dtype=torch.float64, device="cuda")
