@@ -185,7 +185,10 @@ class Graph:
             self.h = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except (TypeError, AttributeError):   # interpreter shutdown: module globals already cleared
+            pass
 
 
 class PathTable:
@@ -299,4 +302,7 @@ class PathTable:
             self.h = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except (TypeError, AttributeError):   # interpreter shutdown: module globals already cleared
+            pass
