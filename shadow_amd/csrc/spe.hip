@@ -326,7 +326,10 @@ __device__ __forceinline__ void scan_chunk(uint64_t sm, int32_t c0, int32_t base
         }
 #pragma unroll
         for (int q = 0; q < INFL; ++q)
-            if (us[q] >= 0) dus[q] = st.D[sidx<L>(g, n, us[q], j)];
+            if (us[q] >= 0) {   // uniform row base (L = 64: SGPRs) + per-lane offset: no 64-bit VGPR address per row
+                const double* row = st.D + ((size_t)g * (size_t)n + (size_t)us[q]) * L;
+                dus[q] = row[j];
+            }
 #pragma unroll
         for (int q = 0; q < INFL; ++q) {
             if (us[q] < 0) continue;
