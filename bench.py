@@ -140,6 +140,9 @@ def bench_lookup(args):
     assert bool(ok.all().item())
     value = q * steps / el
     ach = 41.0 * q / kern_s / 1e9
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_lookup_baseline(t.A, args.cpu_seconds)
     line = {"metric": "per-packet lookup queries/s against the GPU-resident path table (config C5)",
             "value": round(value, 1), "unit": "queries/s", "n_gpus": 1, "steps": steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * el / steps, 3), "higher_is_better": True, "scaling": "weak",
@@ -147,8 +150,40 @@ def bench_lookup(args):
             "config": {"workload": f"C5: {q} uniform (s,t) slot pairs (seed 5) on the {desc} table"},
             "roofline": {"bound": "hbm", "kernel": "k_lookup", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, "k_lookup"),
-                         "algorithmic_bytes_per_query": 41}}
+                         "algorithmic_bytes_per_query": 41},
+            "cpu_baseline": cpu}
+    if cpu:
+        line["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)
     print(json.dumps(line), flush=True)
+
+
+def cpu_lookup_baseline(A: int, seconds: float, seed: int = 5):
+    """The reference's per-packet lookup restated on the host (oracle.c orc_cache:
+    IP -> slot hash, then the two-level src -> dst path cache of
+    _topology_getPathEntry, shd-topology.c:1952-2075), 1 core, on a bounded
+    sample: a cache of 4M uniform pairs of this table, queried for those pairs."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import LookupCache
+    rng = np.random.default_rng(seed)
+    npairs = 4_000_000
+    pairs = rng.integers(0, A, size=(npairs, 2)).astype(np.int32)
+    ips = (0x0A000000 + np.arange(A)).astype(np.uint32)
+    c = LookupCache(ips, pairs, rng.uniform(1, 100, npairs), rng.uniform(0.9, 1, npairs))
+    sip, dip = ips[pairs[:, 0]], ips[pairs[:, 1]]
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds / 2:
+        c.lookup(sip, dip, nthreads=1)
+        done += npairs
+    el = time.perf_counter() - t0
+    nt = min(16, os.cpu_count() or 1)
+    t1 = time.perf_counter()
+    c.lookup(sip, dip, nthreads=nt)
+    c.lookup(sip, dip, nthreads=nt)
+    el_all = time.perf_counter() - t1
+    return {"value": round(done / el, 1), "unit": "queries/s", "cores": 1, "kind": "port",
+            "sample": f"{done} lookups over a 4M-pair cache (seed {seed}): 2 IP->slot probes + src and (src,dst) "
+                      f"cache probes per query, {el:.1f} s",
+            "optimistic_all_cores": {"value": round(2 * npairs / el_all, 1), "threads": nt}}
 
 
 def bench_complete(args):

@@ -672,3 +672,96 @@ int32_t orc_rows(const orc_graph* g, const orc_opts* opts, const int32_t* source
     return orc_rows2(g, opts, sources, nsrc, targets, A, lat, rel, next, hops, kind, NULL, double_ties,
                      dijkstra_seconds, nthreads);
 }
+
+/* ---------------------------------------------------------------------------
+ * CPU restatement of the per-packet path lookup, for the C5 CPU baseline:
+ * topology_getLatency / getReliability / isRoutable -> _topology_getPathEntry
+ * (shd-topology.c:1952-2075): the source and destination IPs resolve to
+ * vertices through a hash table (top->virtualIP, :1958-1961), then the
+ * two-level path cache src -> (dst -> Path*) is probed (:1975-1990).  Here:
+ * open-addressing hash tables (linear probing) in place of GHashTable, holding
+ * the pairs of the measured sample.  Test / baseline infrastructure only. */
+typedef struct { uint64_t* key; int32_t* val; uint64_t mask; } orc_hmap;
+
+static uint64_t orc_mix(uint64_t x) {   /* splitmix64 finaliser */
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull; x ^= x >> 27; x *= 0x94d049bb133111ebull; return x ^ (x >> 31);
+}
+static int orc_hmap_init(orc_hmap* h, int64_t n) {
+    uint64_t cap = 16;
+    while (cap < (uint64_t)n * 2) cap <<= 1;
+    h->key = malloc(cap * sizeof(uint64_t));
+    h->val = malloc(cap * sizeof(int32_t));
+    if (!h->key || !h->val) return -1;
+    memset(h->key, 0xff, cap * sizeof(uint64_t));   /* empty = all ones */
+    h->mask = cap - 1;
+    return 0;
+}
+static void orc_hmap_put(orc_hmap* h, uint64_t k, int32_t v) {
+    uint64_t i = orc_mix(k) & h->mask;
+    while (h->key[i] != ~0ull && h->key[i] != k) i = (i + 1) & h->mask;
+    h->key[i] = k;
+    h->val[i] = v;
+}
+static int32_t orc_hmap_get(const orc_hmap* h, uint64_t k) {
+    uint64_t i = orc_mix(k) & h->mask;
+    for (;;) {
+        if (h->key[i] == k) return h->val[i];
+        if (h->key[i] == ~0ull) return -1;
+        i = (i + 1) & h->mask;
+    }
+}
+
+struct orc_cache {
+    orc_hmap ip, src, pair;   /* ip -> slot; src slot -> cache id; (cache id, dst slot) -> path */
+    double* lat;
+    double* rel;
+};
+
+orc_cache* orc_cache_new(int32_t A, const uint32_t* ips, int64_t npairs, const int32_t* pairs, const double* lat,
+                         const double* rel) {
+    orc_cache* c = calloc(1, sizeof(*c));
+    if (!c || orc_hmap_init(&c->ip, A) || orc_hmap_init(&c->src, A) || orc_hmap_init(&c->pair, npairs)) return NULL;
+    c->lat = malloc(sizeof(double) * (size_t)(npairs > 0 ? npairs : 1));
+    c->rel = malloc(sizeof(double) * (size_t)(npairs > 0 ? npairs : 1));
+    for (int32_t s = 0; s < A; ++s) orc_hmap_put(&c->ip, ips[s], s);
+    int32_t nsrc = 0;
+    for (int64_t i = 0; i < npairs; ++i) {
+        const int32_t s = pairs[2 * i], t = pairs[2 * i + 1];
+        int32_t id = orc_hmap_get(&c->src, (uint64_t)s);
+        if (id < 0) orc_hmap_put(&c->src, (uint64_t)s, id = nsrc++);
+        orc_hmap_put(&c->pair, ((uint64_t)id << 32) | (uint32_t)t, (int32_t)i);
+        c->lat[i] = lat[i];
+        c->rel[i] = rel[i];
+    }
+    return c;
+}
+
+void orc_cache_free(orc_cache* c) {
+    if (!c) return;
+    free(c->ip.key); free(c->ip.val); free(c->src.key); free(c->src.val); free(c->pair.key); free(c->pair.val);
+    free(c->lat); free(c->rel); free(c);
+}
+
+/* q queries (src ip, dst ip) -> latency, reliability, routable; returns hits. */
+int64_t orc_cache_lookup(const orc_cache* c, const uint32_t* sip, const uint32_t* dip, int64_t q, double* lat,
+                         double* rel, uint8_t* ok, int32_t nthreads) {
+    int64_t hits = 0;
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : hits) schedule(static)
+    for (int64_t i = 0; i < q; ++i) {
+        double L = -1.0, R = -1.0;
+        const int32_t s = orc_hmap_get(&c->ip, sip[i]), t = orc_hmap_get(&c->ip, dip[i]);
+        if (s >= 0 && t >= 0) {
+            const int32_t id = orc_hmap_get(&c->src, (uint64_t)s);
+            const int32_t p = id >= 0 ? orc_hmap_get(&c->pair, ((uint64_t)id << 32) | (uint32_t)t) : -1;
+            if (p >= 0) {
+                L = c->lat[p];
+                R = c->rel[p];
+                hits++;
+            }
+        }
+        lat[i] = L;
+        rel[i] = R;
+        ok[i] = L > -1.0;
+    }
+    return hits;
+}

@@ -75,6 +75,15 @@ int32_t orc_rows2(const orc_graph* g, const orc_opts* opts,
                   double* lat, double* rel, int32_t* next, int32_t* hops, uint8_t* kind, int32_t* prev,
                   int64_t* double_ties, double* dijkstra_seconds, int32_t nthreads);
 
+/* Per-packet lookup restatement (C5 CPU baseline): IP -> slot hash, then the
+ * two-level path cache src -> (dst -> path), shd-topology.c:1952-2075. */
+typedef struct orc_cache orc_cache;
+orc_cache* orc_cache_new(int32_t A, const uint32_t* ips, int64_t npairs, const int32_t* pairs, const double* lat,
+                         const double* rel);
+void orc_cache_free(orc_cache* c);
+int64_t orc_cache_lookup(const orc_cache* c, const uint32_t* sip, const uint32_t* dip, int64_t q, double* lat,
+                         double* rel, uint8_t* ok, int32_t nthreads);
+
 #ifdef __cplusplus
 }
 #endif

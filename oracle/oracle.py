@@ -167,3 +167,40 @@ class Oracle:
                     out["kind"][s, t] = KIND_FAIL
         out["ok"] = out["kind"] != KIND_FAIL
         return out
+
+
+class LookupCache:
+    """CPU restatement of the per-packet lookup (IP -> slot hash, two-level path
+    cache; oracle.c orc_cache_*), for the C5 CPU baseline and its tests."""
+
+    def __init__(self, ips, pairs, lat, rel):
+        L = lib()
+        L.orc_cache_new.restype = C.c_void_p
+        L.orc_cache_new.argtypes = [C.c_int32, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_cache_free.argtypes = [C.c_void_p]
+        L.orc_cache_lookup.restype = C.c_int64
+        L.orc_cache_lookup.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_int32]
+        self._keep = [np.ascontiguousarray(ips, np.uint32), np.ascontiguousarray(pairs, np.int32),
+                      np.ascontiguousarray(lat, np.float64), np.ascontiguousarray(rel, np.float64)]
+        k = self._keep
+        self.h = L.orc_cache_new(int(k[0].shape[0]), _ptr(k[0]), int(k[1].shape[0]), _ptr(k[1]), _ptr(k[2]),
+                                 _ptr(k[3]))
+        if not self.h:
+            raise RuntimeError("orc_cache_new failed")
+
+    def lookup(self, sip, dip, nthreads: int = 1):
+        sip = np.ascontiguousarray(sip, np.uint32)
+        dip = np.ascontiguousarray(dip, np.uint32)
+        q = sip.shape[0]
+        lat, rel, ok = np.empty(q), np.empty(q), np.empty(q, np.uint8)
+        hits = lib().orc_cache_lookup(self.h, _ptr(sip), _ptr(dip), q, _ptr(lat), _ptr(rel), _ptr(ok), int(nthreads))
+        return lat, rel, ok, int(hits)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            try:
+                lib().orc_cache_free(self.h)
+            except (TypeError, AttributeError):
+                pass
+            self.h = None

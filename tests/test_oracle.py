@@ -151,3 +151,26 @@ def test_self_rules_and_prefer_direct_triangle():
     assert r2["kind"][0, 0] == KIND_SSSP and r2["lat"][0, 0] == 20.0
     assert r2["rel"][0, 0] == ((1.0 * 1.0) * 1.0) * 0.95 * 0.95
     assert r2["next"][0, 0] == 1 and r2["hops"][0, 0] == 2
+
+
+def test_lookup_cache_restatement():
+    """The C5 CPU baseline's lookup (IP hash + two-level path cache) returns the
+    stored record for cached pairs and -1 / not routable otherwise."""
+    from oracle import LookupCache
+    rng = np.random.default_rng(1)
+    A = 500
+    ips = (0x0A000000 + np.arange(A)).astype(np.uint32)
+    pairs = np.unique(rng.integers(0, A, size=(3000, 2)), axis=0).astype(np.int32)
+    lat = rng.uniform(1, 100, pairs.shape[0])
+    rel = rng.uniform(0.9, 1.0, pairs.shape[0])
+    c = LookupCache(ips, pairs, lat, rel)
+    for nt in (1, 4):
+        got_l, got_r, ok, hits = c.lookup(ips[pairs[:, 0]], ips[pairs[:, 1]], nthreads=nt)
+        assert hits == pairs.shape[0] and ok.all()
+        assert np.array_equal(got_l, lat) and np.array_equal(got_r, rel)
+    cached = set(map(tuple, pairs.tolist()))
+    miss = np.array([(s, t) for s, t in rng.integers(0, A, size=(200, 2)).tolist() if (s, t) not in cached])
+    l2, r2, ok2, h2 = c.lookup(ips[miss[:, 0]], ips[miss[:, 1]])
+    assert h2 == 0 and not ok2.any() and (l2 == -1).all() and (r2 == -1).all()
+    l3, _, ok3, _ = c.lookup(np.array([0x7F000001], np.uint32), ips[:1])   # unknown IP
+    assert l3[0] == -1 and ok3[0] == 0
