@@ -83,9 +83,20 @@ def cpu_baseline(top, att, seconds: float, seed: int = 6):
                 break
     except OSError:
         pass
+    # BASELINE.md's "optimistic, all cores" (OpenMP over sources; the reference
+    # serialises Dijkstra under graphLock, so this is a bound it cannot reach)
+    nt = min(16, os.cpu_count() or 1)
+    done_all, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < seconds / 4 and done + done_all < att.shape[0]:
+        src = att[order[done + done_all:done + done_all + 8 * nt]]
+        o.rows(src, att, nthreads=nt)
+        done_all += src.shape[0]
+    el_all = time.perf_counter() - t1
     return {"value": done / el, "unit": "sources/s", "cores": 1, "kind": "port",
             "sample": f"{done} seeded-random sources (seed {seed}) x {att.shape[0]} targets, full row build, "
                       f"{el:.1f} s; Dijkstra-only {done / max(dj, 1e-9):.1f} sources/s",
+            "optimistic_all_cores": {"value": round(done_all / max(el_all, 1e-9), 1), "threads": nt,
+                                     "sample": f"{done_all} further sources"},
             "cpu_model": model, "host_nproc": os.cpu_count()}
 
 
