@@ -42,14 +42,24 @@ def workload(name: str):
         top = graphs.gen_tiered()
         att = graphs.tiered_attached(top)
         desc = "C4: tiered BA core 20k + 180k stubs, A=100000 stubs"
-    elif name == "c1":
+    elif name in ("c1", "c1all"):
         # the reference's shipped topology (resource/topology.graphml.xml.xz, 183 vertices,
-        # complete => DIRECT regime), committed as data in tests/golden; every vertex attached
+        # complete => DIRECT regime), committed as data in tests/golden.  c1: the examples
+        # config's 150 un-hinted hosts attached through Shadow's seed chain;
+        # c1all: every vertex attached
+        from shadow_amd import shadow_random as sr
         z = np.load(os.path.join(ROOT, "tests", "golden", "shipped_topology.npz"))
         top = graphs.Topology(n=int(z["n"]), esrc=z["esrc"], edst=z["edst"], elat=z["elat"], eloss=z["eloss"],
                               vloss=z["vloss"], directed=bool(z["directed"]), prefer_direct=bool(z["prefer_direct"]))
-        att = np.arange(top.n, dtype=np.int32)
-        desc = "C1: shipped resource/topology.graphml.xml.xz (183 V, complete: DIRECT), all 183 vertices attached"
+        if name == "c1all":
+            att = np.arange(top.n, dtype=np.int32)
+            desc = "C1: shipped resource/topology.graphml.xml.xz (183 V, complete: DIRECT), all 183 vertices attached"
+        else:
+            hosts = sr.host_streams([("server", 50), ("webclient", 50), ("bulkclient", 50)], seed=1)
+            verts = [sr.unhinted_vertex(h, top.n) for _, h in hosts]
+            att = np.array(list(dict.fromkeys(verts)), dtype=np.int32)   # slots in first-attach order
+            desc = (f"C1: shipped resource/topology.graphml.xml.xz (183 V, complete: DIRECT) with the examples "
+                    f"config's 150 hosts (seed chain 1): {att.shape[0]} attached vertices")
     elif name == "c2":
         top = graphs.gen_rgg(10000, 2)
         att = np.arange(top.n, dtype=np.int32)

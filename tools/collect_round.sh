@@ -2,7 +2,7 @@
 set -e
 R=${ROUND:-r01}
 O=gpurun_out/$R
-for C in c1 c3 c2 c2fw c4 c4_full c5 complete; do
+for C in c1 c1all c3 c2 c2fw c4 c4_full c5 complete; do
   cp $O/bench_$C.log profiles/${R}_bench_$C.log
   if [ -d $O/kt_$C ]; then
     f=$(find $O/kt_$C -name '*kernel_stats.csv' | head -1)

@@ -24,6 +24,7 @@ tail -1 $O/bench_c2.log
 timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d $O/kt_c2 -o run --output-format csv -- python bench.py --config c2 --no-cpu-baseline > $O/kt_c2.log 2>&1
 timeout -k 10 200 python -u bench.py --config c1 > $O/bench_c1.log 2>&1 || { tail -20 $O/bench_c1.log; exit 1; }
 tail -1 $O/bench_c1.log
+timeout -k 10 200 python -u bench.py --config c1all > $O/bench_c1all.log 2>&1 || { tail -20 $O/bench_c1all.log; exit 1; }
 timeout -k 10 300 python -u bench.py --config c4 --full-table --shares 8 --share-index 0 > $O/bench_c4.log 2>&1 || { tail -20 $O/bench_c4.log; exit 1; }
 tail -1 $O/bench_c4.log
 timeout -k 10 300 python -u bench.py --config c4 --full-table > $O/bench_c4_full.log 2>&1 || { tail -20 $O/bench_c4_full.log; exit 1; }
