@@ -57,6 +57,12 @@ int32_t topology_isRoutable(Topology* top, spe_in_addr_t srcAddress, spe_in_addr
 double topology_getLatency(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
 double topology_getReliability(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
 void topology_incrementPathPacketCounter(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
+/* worker_sendPacket's three per-packet calls (isRoutable, getReliability,
+ * getLatency, shd-worker.c:235-247) answered by one slot resolution and one
+ * table read: returns routable; *latency / *reliability as the two getters
+ * (-1.0 when unroutable).  Either output pointer may be NULL. */
+int32_t topology_getPathInfo(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress, double* latency,
+                             double* reliability);
 
 /* engine hooks */
 void topology_set_log_callback(Topology* top, topology_log_fn fn, void* ctx);

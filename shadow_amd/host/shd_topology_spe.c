@@ -880,6 +880,20 @@ double topology_getReliability(Topology* top, spe_in_addr_t srcAddress, spe_in_a
     return top->rel[(size_t)s * top->A + t];
 }
 
+int32_t topology_getPathInfo(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress, double* latency,
+                             double* reliability) {
+    int32_t s, t;
+    double L = -1.0, R = -1.0;
+    if (top && pair_slots(top, srcAddress, dstAddress, &s, &t)) {
+        const size_t o = (size_t)s * top->A + t;
+        L = top->lat[o];
+        R = top->rel[o];
+    }
+    if (latency) *latency = L;
+    if (reliability) *reliability = R;
+    return L > -1 ? 1 : 0;
+}
+
 int32_t topology_isRoutable(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {
     return topology_getLatency(top, srcAddress, dstAddress) > -1 ? 1 : 0;   /* :2072-2075 */
 }

@@ -14,7 +14,8 @@ EXPORTS = ["topology_new", "topology_new_on_device", "topology_free", "topology_
            "topology_isRoutable", "topology_getLatency", "topology_getReliability",
            "topology_incrementPathPacketCounter", "topology_set_log_callback",
            "topology_set_min_latency_callback", "topology_seal", "topology_vertex_count",
-           "topology_attached_vertex", "topology_path_packet_count", "topology_min_path_latency"]
+           "topology_attached_vertex", "topology_path_packet_count", "topology_min_path_latency",
+           "topology_getPathInfo"]
 
 RANDOM_FN = C.CFUNCTYPE(C.c_double, C.c_void_p)
 MINLAT_FN = C.CFUNCTYPE(None, C.c_double, C.c_void_p)
@@ -43,6 +44,8 @@ def lib():
         L.topology_isRoutable.argtypes = [P, U, U]
         L.topology_isRoutable.restype = C.c_int32
         L.topology_incrementPathPacketCounter.argtypes = [P, U, U]
+        L.topology_getPathInfo.argtypes = [P, U, U, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.topology_getPathInfo.restype = C.c_int32
         L.topology_set_log_callback.argtypes = [P, LOG_FN, P]
         L.topology_set_min_latency_callback.argtypes = [P, MINLAT_FN, P]
         L.topology_seal.argtypes = [P]
@@ -100,6 +103,12 @@ class Topology:
 
     def routable(self, a: int, b: int) -> bool:
         return bool(lib().topology_isRoutable(self.h, a, b))
+
+    def path_info(self, a: int, b: int):
+        """(routable, latency, reliability) in one lookup (topology_getPathInfo)."""
+        lat, rel = C.c_double(0), C.c_double(0)
+        ok = lib().topology_getPathInfo(self.h, a, b, C.byref(lat), C.byref(rel))
+        return bool(ok), lat.value, rel.value
 
     def count_packet(self, a: int, b: int):
         lib().topology_incrementPathPacketCounter(self.h, a, b)

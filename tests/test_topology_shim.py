@@ -73,6 +73,8 @@ def test_examples_config_one_vertex(tmp_path, golden_dir):
     assert top.packets(hosts[0], hosts[1]) == 2 and top.packets(hosts[5], hosts[9]) == 2
     unknown = T.ip("12.0.0.1")
     assert top.latency(hosts[0], unknown) == -1.0 and not top.routable(unknown, hosts[0])
+    assert top.path_info(hosts[0], unknown) == (False, -1.0, -1.0)
+    assert top.path_info(hosts[0], hosts[1]) == (True, 50.0, 0.95)
     assert top.min_latency() == 50.0
     top.close()
 
@@ -102,6 +104,7 @@ def test_attach_by_ip_and_query_against_oracle(tmp_path):
         for j in range(40):
             assert top.latency(addrs[i], addrs[j]) == ref["lat"][i, j]
             assert top.reliability(addrs[i], addrs[j]) == ref["rel"][i, j]
+            assert top.path_info(addrs[i], addrs[j]) == (True, ref["lat"][i, j], ref["rel"][i, j])
     top.close()
 
 
