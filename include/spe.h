@@ -54,7 +54,7 @@ extern "C" {
 
 #define SPE_ENGINE_AUTO 0    /* LDS engine when the relaxation graph fits one CU's LDS, else BATCH */
 #define SPE_ENGINE_BATCH 1   /* 64-source lane groups, HBM-resident state, frontier rounds */
-#define SPE_ENGINE_LDS 2     /* one workgroup per source row, state resident in LDS (<= ~11k vertices) */
+#define SPE_ENGINE_LDS 2     /* one workgroup per source row, state resident in LDS (<= 10,240 relaxation vertices) */
 
 typedef struct spe_graph spe_graph;
 typedef struct spe_table spe_table;

@@ -24,7 +24,7 @@
 //                  targets with vertex loss or multigraph get_eid latencies)
 //   k_rows_direct  complete graphs: every pair is the direct edge
 //   k_direct_overlay  preferdirectpaths: adjacent pairs get the direct edge
-//   k_sssp_lds     small graphs (<= ~11k relaxation vertices): one workgroup per
+//   k_sssp_lds     small graphs (<= 10,240 relaxation vertices): one workgroup per
 //                  source row, relaxation state in LDS, rows written directly
 //   k_owner_replay compat: the reference's first-writer-wins path cache
 //   k_lookup       batched per-packet (s, t) -> (latency, reliability, ok)
@@ -889,7 +889,7 @@ __global__ __launch_bounds__(BLOCK) void k_direct_overlay(int32_t groups, int32_
 
 // ------------------------------------------------------------------------
 // LDS engine: one workgroup per source row with the row's relaxation state
-// resident in LDS.  For graphs up to ~11k relaxation vertices (Shadow's own
+// resident in LDS.  For graphs up to 10,240 relaxation vertices (Shadow's own
 // topologies, C2) this replaces the 64-lane HBM-resident batch relaxation.
 // Per source row:
 //   1. push Bellman-Ford over a changed-vertex bitset: LDS 64-bit atomic min on
@@ -899,10 +899,11 @@ __global__ __launch_bounds__(BLOCK) void k_direct_overlay(int32_t groups, int32_
 //   2. canonical parent = argmin (d[u], u) over {u : fl(d[u] + w) == d[v]},
 //      in-edges spread over lanes the same way, per-vertex argmin in LDS;
 //   3. latencies of every target (d is final);
-//   4. child lists of the parent tree (count, scan, scatter in LDS), then one
-//      top-down pass over the tree by hop level: hops, the path-order
-//      reliability fold r(v) = r(parent) * (1 - p_e) and the first hop of every
-//      vertex, each computed once from its parent's final values;
+//   4. top-down over the parent tree by hop level, entirely in LDS: every
+//      thread keeps its vertices' parent and parent-edge factor in registers and
+//      a level settles each vertex whose parent settled in the previous one:
+//      hops, the path-order reliability fold r(v) = r(parent) * (1 - p_e) and
+//      the first hop, each computed once from the parent's final values;
 //   5. reliability / next hop / hops of every target into the SB64 table.
 // Distances are the least fixpoint of d[v] = min fl(d[u] + w), as in the batch
 // engine, so rows are bit-identical (tests/test_gpu_lds.py).
@@ -910,7 +911,8 @@ constexpr int LDS_T = 1024;                 // threads per workgroup (16 waves)
 constexpr int LDS_WAVES = LDS_T / WAVE;
 constexpr int LDS_MAX_BYTES = 160 * 1024 - 1024;   // dynamic share; the rest covers static __shared__
 constexpr int LDS_WL = 256;                 // per-wave marked-vertex list of the push pass
-constexpr int LDS_CAND_BYTES = LDS_WAVES * (LDS_WL * 4 + 2 * WAVE);   // push lists + owner maps (H space)
+constexpr int LDS_WIN = 2;                  // 64-edge windows per global round trip of the push pass
+constexpr int LDS_CAND_BYTES = LDS_WAVES * (LDS_WL * 4 + LDS_WIN * WAVE);   // push lists + owner maps (H space)
 
 __host__ __device__ constexpr size_t lds_align(size_t b) { return (b + 15) & ~(size_t)15; }
 // D f64 | X i32 (out-row starts, then parent entry) | H u16 / argmin scratch | 2 bitsets
@@ -932,19 +934,16 @@ struct alignas(16) SlotInfo {
     double pa;      // 1 - p of the pendant edge (get_eid edge), 1 otherwise
 };
 
-// per-workgroup global scratch of the tree pass (L2-resident: 32 B per vertex)
-struct alignas(16) TreeItem {
-    int32_t v;
-    int32_t f;      // first hop (original id), -1 at a core source
-    double r;       // reliability fold up to v
-};
+// per-workgroup global scratch: the parent entries, kept for pass 5's rare
+// path walks once the LDS parent array holds first hops
 struct LdsScratch {
-    int32_t* child;     // [grid][nc]
-    double* cia;        // [grid][nc] 1 - p of each child's parent edge, aligned with child
-    TreeItem* q;        // [grid][nc] vertices in hop-level order
-    double* r;          // [grid][nc]
-    int32_t* f;         // [grid][nc]
+    int32_t* par;       // [grid][nc] in-CSR entry of each vertex's parent edge
 };
+
+// vertices per thread of the tree pass (registers): the LDS engine takes graphs
+// of at most LDS_VPT * LDS_T = 10,240 relaxation vertices (C2's 9,998 fit; the
+// register budget of 4 waves per SIMD leaves no room for 11)
+constexpr int LDS_VPT = 10;
 
 __device__ __forceinline__ int32_t par_vertex(const DevGraph& G, int32_t k) { return G.icol[k]; }
 
@@ -974,12 +973,18 @@ __device__ __forceinline__ void wave_expand(int32_t lane, int32_t deg, F&& body)
     }
 }
 
-__device__ __forceinline__ int32_t wave_append(bool ok, int32_t lane, int32_t* tail) {
-    const uint64_t m = __ballot(ok);
-    int32_t b = 0;
-    if (lane == 0 && m) b = atomicAdd(tail, __popcll(m));
-    b = __shfl(b, 0);
-    return b + __popcll(m & ((1ull << lane) - 1ull));
+// Workgroup-wide OR with ONE barrier (__syncthreads_or costs three): call ix
+// ORs into flag[ix % 3] and thread 0 clears flag[(ix + 2) % 3], which every
+// thread read before this call's barrier and nobody writes before call ix + 2.
+// ix must be workgroup-uniform and increase by one per call; flags start zero.
+__device__ __forceinline__ bool wg_any(bool p, uint32_t& ix, int32_t* flag) {
+    const uint32_t k = ix % 3u;
+    if (__ballot(p) && (threadIdx.x & (WAVE - 1)) == 0) flag[k] = 1;
+    __syncthreads();
+    const bool r = flag[k] != 0;
+    if (threadIdx.x == 0) flag[(k + 2u) % 3u] = 0;
+    ++ix;
+    return r;
 }
 
 __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1, const SlotInfo* __restrict__ slots,
@@ -995,11 +1000,13 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
     uint16_t* H = reinterpret_cast<uint16_t*>(hs);
     uint32_t* F0 = reinterpret_cast<uint32_t*>(hs + lds_hs_bytes(nc));
     uint32_t* F1 = F0 + lds_align((size_t)nw * 4) / 4;
-    // after the latency pass the distance space holds the tree's child offsets + parent ids
-    int32_t* coff = reinterpret_cast<int32_t*>(smem);
-    int32_t* pvt = coff + nc;
-    __shared__ int32_t s_tail, s_total, s_wsum[LDS_WAVES];
+    // after the latency pass the distance space holds the reliability fold and X
+    // (parent, first hop); the parent entries move to Xg
+    double* Rl = D;
+    __shared__ int32_t s_any[3];
+    uint32_t syncix = 0;
     const int32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
+    if (tid < 3) s_any[tid] = 0;   // (the first slot's init barrier publishes it)
     const unsigned long long INF_BITS = 0x7FF0000000000000ull;
     const int32_t oend = G.optr[nc];
     // Workgroups are dealt round-robin over the 8 XCDs; give the workgroups of
@@ -1007,11 +1014,7 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
     // writes meet in the same L2 before write-back.
     const int32_t gx = gridDim.x;
     const int32_t bx = (gx % 8 == 0) ? (blockIdx.x % 8) * (gx / 8) + blockIdx.x / 8 : blockIdx.x;
-    int32_t* child = sc_.child + (size_t)blockIdx.x * nc;
-    double* cia = sc_.cia + (size_t)blockIdx.x * nc;
-    TreeItem* Q = sc_.q + (size_t)blockIdx.x * nc;
-    double* Rg = sc_.r + (size_t)blockIdx.x * nc;
-    int32_t* Fg = sc_.f + (size_t)blockIdx.x * nc;
+    int32_t* Xg = sc_.par + (size_t)blockIdx.x * nc;
     for (int32_t slot = slot0 + bx; slot < slot1; slot += gx) {
         const int32_t s = slots[slot].t;
         unsigned long long tph = dbg && tid == 0 ? wall_clock64() : 0, nround = 0, nlev = 0;
@@ -1046,7 +1049,7 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
         uint32_t* cur = F0;
         uint32_t* nxt = F1;
         int32_t* wl = reinterpret_cast<int32_t*>(hs) + wave * LDS_WL;   // H space is idle here
-        uint8_t* om = hs + LDS_WAVES * LDS_WL * 4 + wave * 2 * WAVE;
+        uint8_t* om = hs + LDS_WAVES * LDS_WL * 4 + wave * LDS_WIN * WAVE;
         for (;;) {
             bool any = false;
             int32_t cnt = 0;   // wave-uniform list length
@@ -1070,18 +1073,18 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                 }
                 const int32_t total = __shfl(incl, WAVE - 1);
                 const int32_t excl = incl - deg;
-                for (int32_t base = 0; base < total; base += 2 * WAVE) {
-                    int32_t x[2];
-                    double cand[2];
-                    bool ok[2];
-                    // owner map of this 128-edge window: each lane stamps its own edges
-                    for (int32_t i = max(excl, base), ie = min(incl, base + 2 * WAVE); i < ie; ++i)
+                for (int32_t base = 0; base < total; base += LDS_WIN * WAVE) {
+                    int32_t x[LDS_WIN];
+                    double cand[LDS_WIN];
+                    bool ok[LDS_WIN];
+                    // owner map of this window: each lane stamps its own edges
+                    for (int32_t i = max(excl, base), ie = min(incl, base + LDS_WIN * WAVE); i < ie; ++i)
                         om[i - base] = (uint8_t)lane;
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
+                    for (int h = 0; h < LDS_WIN; ++h) {
                         const int32_t e = base + h * WAVE + lane;
                         const int32_t o = e < total ? om[e - base] : 0;
                         const int32_t k = __shfl(k0, o) + e - __shfl(excl, o);
@@ -1091,7 +1094,7 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                         cand[h] = ok[h] ? du + G.ow[k] : 0.0;
                     }
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
+                    for (int h = 0; h < LDS_WIN; ++h) {
                         if (!ok[h]) continue;
                         const unsigned long long cb = (unsigned long long)__double_as_longlong(cand[h]);
                         if (cb < atomicMin(&Db[x[h]], cb)) {
@@ -1141,7 +1144,7 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
             if (cnt) flush();
             ++nround;
             const unsigned long long tb0 = (dbg && tid == 0) ? wall_clock64() : 0;
-            const bool more = __syncthreads_or(any);
+            const bool more = wg_any(any, syncix, s_any);
             if (dbg && tid == 0) {
                 atomicAdd(&dbg[11], tfl);
                 atomicAdd(&dbg[12], wall_clock64() - tb0);
@@ -1231,124 +1234,67 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
         }
         __syncthreads();
         LDS_PHASE(3)
-        // 4a. child lists of the parent tree: coff[u] = first child slot of u
-        for (int32_t v = tid; v < nc; v += LDS_T) {
-            coff[v] = 0;
-            H[v] = 0xFFFF;
+        // 4. the parent tree top-down by hop level.  Thread-owned vertices
+        // v = tid + i * LDS_T keep (parent, 1 - p of the parent edge) in registers.
+        // X becomes PF: parent (low 16 bits) | first hop (high 16 bits, 0xFFFF =
+        // none), both relaxation-vertex ids (nc <= LDS_VPT * LDS_T < 2^16).  Each
+        // vertex is read and rewritten by its owning thread only.
+        uint32_t* PF = reinterpret_cast<uint32_t*>(X);
+        double pa[LDS_VPT];
+        uint32_t todo = 0;
+#pragma unroll
+        for (int i = 0; i < LDS_VPT; ++i) {
+            const int32_t v = tid + i * LDS_T;
+            int32_t k = -1;
+            if (v < nc) {
+                k = X[v];
+                Xg[v] = k;
+                PF[v] = k >= 0 ? (0xFFFF0000u | (uint32_t)par_vertex(G, k)) : 0xFFFFFFFFu;
+            }
+            pa[i] = k >= 0 ? G.ia[k] : 0.0;
+            if (k >= 0) todo |= 1u << i;
         }
+        for (int32_t v = tid; v < nc; v += LDS_T) H[v] = 0xFFFF;
         __syncthreads();
-        for (int32_t v0 = tid; v0 < nc; v0 += 4 * LDS_T) {   // 4 vertices' loads in flight
-            int32_t p[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int32_t v = v0 + q * LDS_T;
-                const int32_t k = v < nc ? X[v] : -1;
-                p[q] = k >= 0 ? par_vertex(G, k) : -1;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int32_t v = v0 + q * LDS_T;
-                if (v >= nc) continue;
-                pvt[v] = p[q];
-                if (p[q] >= 0) atomicAdd(&coff[p[q]], 1);
-            }
-        }
-        __syncthreads();
-        {   // inclusive scan of the child counts (thread = contiguous segment)
-            const int32_t per = (nc + LDS_T - 1) / LDS_T;
-            const int32_t b0 = min(nc, tid * per), b1 = min(nc, b0 + per);
-            int32_t sum = 0;
-            for (int32_t i = b0; i < b1; ++i) sum += coff[i];
-            int32_t incl = sum;
-#pragma unroll
-            for (int d = 1; d < WAVE; d <<= 1) {
-                const int32_t y = __shfl_up(incl, d);
-                if (lane >= d) incl += y;
-            }
-            if (lane == WAVE - 1) s_wsum[wave] = incl;
-            __syncthreads();
-            int32_t wbase = 0;
-            for (int32_t q = 0; q < wave; ++q) wbase += s_wsum[q];
-            int32_t run = wbase + incl - sum;
-            for (int32_t i = b0; i < b1; ++i) {
-                run += coff[i];
-                coff[i] = run;
-            }
-            if (tid == LDS_T - 1) s_total = run;
-        }
-        __syncthreads();
-        for (int32_t v0 = tid; v0 < nc; v0 += 4 * LDS_T) {
-            int32_t p[4];
-            double a[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int32_t v = v0 + q * LDS_T;
-                p[q] = v < nc ? pvt[v] : -1;
-                a[q] = p[q] >= 0 ? G.ia[X[v]] : 0.0;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (p[q] < 0) continue;
-                const int32_t pos = atomicSub(&coff[p[q]], 1) - 1;
-                child[pos] = v0 + q * LDS_T;
-                cia[pos] = a[q];
-            }
-        }
         if (tid == 0) {
             const double fs = G.vfac[s];
             const double r0 = has_attr(fs) ? 1.0 * fs : 1.0;   // shd-topology.c:1428-1430
-            TreeItem it;
-            it.v = seed;
-            it.f = sc >= 0 ? -1 : G.corev[seed];
-            it.r = sc >= 0 ? r0 : r0 * G.fia[G.fiptr[s]];
-            Q[0] = it;
-            Rg[seed] = it.r;
-            Fg[seed] = it.f;
+            Rl[seed] = sc >= 0 ? r0 : r0 * G.fia[G.fiptr[s]];
+            PF[seed] = sc >= 0 ? 0xFFFFFFFFu : (((uint32_t)seed << 16) | 0xFFFFu);
             H[seed] = sc >= 0 ? 0 : 1;
-            s_tail = 1;
         }
         __syncthreads();
         LDS_PHASE(4)
-        // 4b. top-down over the tree, one hop level per step
         {
-            const int32_t total = s_total;
-            int32_t lb = 0, le = 1;
-            uint16_t hl = sc >= 0 ? 1 : 2;   // hop count of the next level
-            while (lb < le) {
-                for (int32_t i0 = lb + wave * WAVE; i0 < le; i0 += LDS_T) {
-                    const int32_t i = i0 + lane;
-                    int32_t u = -1, fu = -1, cs = 0, cn = 0;
-                    double ru = 0.0;
-                    if (i < le) {
-                        const TreeItem it = Q[i];
-                        u = it.v;
-                        fu = it.f;
-                        ru = it.r;
-                        cs = coff[u];
-                        cn = (u + 1 < nc ? coff[u + 1] : total) - cs;
-                    }
-                    wave_expand(lane, cn, [&](bool ok, int32_t o, int32_t off, int32_t, int32_t, int32_t) {
-                        const int32_t uo = __shfl(u, o), fo = __shfl(fu, o), co = __shfl(cs, o);
-                        const double ro = __shfl(ru, o);
-                        TreeItem it;
-                        if (ok) {
-                            it.v = child[co + off];
-                            it.r = ro * cia[co + off];
-                            it.f = (uo == sc) ? G.corev[it.v] : fo;
-                            H[it.v] = hl;
-                            Rg[it.v] = it.r;
-                            Fg[it.v] = it.f;
-                        }
-                        const int32_t pos = wave_append(ok, lane, &s_tail);
-                        if (ok) Q[pos] = it;
-                    });
+            // level hl settles v when H[parent] == hl - 1; a vertex settled in this
+            // level already reads hl, so no level sees a half-written parent
+            uint16_t hl = sc >= 0 ? 1 : 2;
+            for (;;) {
+                // readiness first (loads only, so the owned vertices' LDS reads can
+                // be in flight together), then the few settling vertices
+                // (branch-free: a branch per vertex would serialise the loads)
+                uint32_t ready = 0;
+#pragma unroll
+                for (int i = 0; i < LDS_VPT; ++i) {
+                    const bool t = (todo >> i) & 1u;
+                    const uint32_t p = t ? (PF[min(tid + i * LDS_T, nc - 1)] & 0xFFFFu) : 0u;
+                    ready |= (t && H[p] == (uint16_t)(hl - 1)) ? (1u << i) : 0u;
+                }
+                const bool any = ready != 0;
+                todo &= ~ready;
+#pragma unroll
+                for (int i = 0; i < LDS_VPT; ++i) {
+                    if (!((ready >> i) & 1u)) continue;
+                    const int32_t v = tid + i * LDS_T;
+                    const uint32_t p = PF[v] & 0xFFFFu;
+                    Rl[v] = Rl[p] * pa[i];
+                    const uint32_t f = ((int32_t)p == sc) ? (uint32_t)v : (PF[p] >> 16);
+                    PF[v] = (f << 16) | p;
+                    H[v] = hl;
                 }
                 ++nlev;
-                __syncthreads();
-                lb = le;
-                le = s_tail;
+                if (!wg_any(any, syncix, s_any)) break;
                 ++hl;
-                __syncthreads();
             }
         }
         LDS_PHASE(5)
@@ -1374,7 +1320,7 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
             const double ft = G.vfac[t];
             double R;
             if (!has_attr(ft) || ft == 1.0) {
-                R = Rg[c] * si.pa;   // pa = 1.0 for relaxation vertices (exact)
+                R = Rl[c] * si.pa;   // pa = 1.0 for relaxation vertices (exact)
             } else {   // ((1 * fs) * ft) * a1 * a2 ... : the target factor comes second
                 const double fs = G.vfac[s];
                 double r = 1.0;
@@ -1388,8 +1334,8 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                     } else {
                         int32_t x = c;
                         if (kt >= 0) back -= 1;
-                        for (int32_t q = 0; q < back; ++q) x = par_vertex(G, X[x]);
-                        ea = X[x] >= 0 ? G.ia[X[x]] : G.fia[G.fiptr[s]];
+                        for (int32_t q = 0; q < back; ++q) x = par_vertex(G, Xg[x]);
+                        ea = Xg[x] >= 0 ? G.ia[Xg[x]] : G.fia[G.fiptr[s]];
                     }
                     r *= ea;
                 }
@@ -1405,8 +1351,8 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                     } else {
                         int32_t x = c;
                         if (kt >= 0) back -= 1;
-                        for (int32_t q = 0; q < back; ++q) x = par_vertex(G, X[x]);
-                        ew = X[x] >= 0 ? G.iwrep[X[x]] : G.fiwrep[G.fiptr[s]];
+                        for (int32_t q = 0; q < back; ++q) x = par_vertex(G, Xg[x]);
+                        ew = Xg[x] >= 0 ? G.iwrep[Xg[x]] : G.fiwrep[G.fiptr[s]];
                     }
                     l += ew;
                 }
@@ -1414,9 +1360,10 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                 tb.lr[o].x = l;
             }
             tb.lr[o].y = R;
-            tb.next[o] = kt >= 0 && hc == 0 ? t : Fg[c];
+            const uint32_t fc = PF[c] >> 16;
+            tb.next[o] = kt >= 0 && hc == 0 ? t : (fc == 0xFFFFu ? -1 : G.corev[fc]);
             tb.hops[o] = (uint16_t)Hh;
-            if (tb.prev) tb.prev[o] = kt >= 0 ? G.corev[c] : (X[c] >= 0 ? G.corev[par_vertex(G, X[c])] : s);
+            if (tb.prev) tb.prev[o] = kt >= 0 ? G.corev[c] : (Xg[c] >= 0 ? G.corev[par_vertex(G, Xg[c])] : s);
         }
         __syncthreads();
         LDS_PHASE(6)
@@ -1703,7 +1650,7 @@ struct spe_table {
     Table tb{};
     int32_t* d_slot_vertex = nullptr;
     SlotInfo* d_slots = nullptr;   // LDS engine: per-target constants
-    LdsScratch lsc{};              // LDS engine: per-workgroup tree scratch
+    LdsScratch lsc{};              // LDS engine: per-workgroup parent-entry scratch
     int32_t lds_grid = 0;          // LDS engine: workgroups per launch (scratch is sized for it)
     int32_t* d_rank = nullptr;     // owner replay: position of each slot in the source-run order
     int32_t* d_vertex_slot = nullptr;
@@ -2073,7 +2020,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     }
     t->lanes = lanes;
     {
-        const bool fits = lds_bytes(g->hg.nc) <= (size_t)LDS_MAX_BYTES;
+        const bool fits = lds_bytes(g->hg.nc) <= (size_t)LDS_MAX_BYTES && g->hg.nc <= LDS_VPT * LDS_T;
         int32_t e = o.engine;
         bool from_env = false;
         if (e == SPE_ENGINE_AUTO && !o.want_aux && getenv("SPE_ENGINE")) {   // test / diagnostic override
@@ -2173,11 +2120,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, LDS_MAX_BYTES / lds_bytes(h.nc)));
         t->lds_grid = cus * per_cu;
         const size_t per = (size_t)t->lds_grid * std::max(1, h.nc);
-        TRY(dev_alloc(t->allocs, &t->lsc.child, per));
-        TRY(dev_alloc(t->allocs, &t->lsc.cia, per));
-        TRY(dev_alloc(t->allocs, &t->lsc.q, per));
-        TRY(dev_alloc(t->allocs, &t->lsc.r, per));
-        TRY(dev_alloc(t->allocs, &t->lsc.f, per));
+        TRY(dev_alloc(t->allocs, &t->lsc.par, per));
     }
     const size_t G = (size_t)t->groups;
     const size_t GL = G * (WAVE / t->lanes);   // lane groups per batch
