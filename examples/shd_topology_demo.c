@@ -1,0 +1,144 @@
+/* A Shadow-worker-shaped user of the drop-in topology API
+ * (include/shd_topology_spe.h, which re-hosts src/main/routing/shd-topology.h).
+ *
+ * What Shadow does with a topology, in order:
+ *   master:  topology_new(graphml)                       shd-master.c:209
+ *   hosts:   topology_attach(addr, random, hints...)     shd-host.c:140
+ *   workers: per packet isRoutable / getReliability / getLatency
+ *            (shd-worker.c:235-247) + incrementPathPacketCounter,
+ *            concurrently from --workers pthreads
+ *   master:  topology_free                               shd-master.c:100
+ * Here the three per-packet calls are topology_getPathInfo (one table read);
+ * every 64th packet is re-asked through the three separate getters, which must
+ * agree bit for bit.
+ *
+ *   shd_topology_demo <graph.graphml> <hosts> <packets> [threads] [seed]
+ * prints one JSON line; exit 0 ok, 1 disagreement, 2 setup failure. */
+#include <arpa/inet.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "shd_topology_spe.h"
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+/* host attachment draws, like Shadow's per-host Random (rand_r based) */
+static double next_double(void* ctx) { return (double)rand_r((unsigned*)ctx) / (double)RAND_MAX; }
+
+static spe_in_addr_t host_addr(int32_t i) { return htonl((11u << 24) | (uint32_t)(i + 1)); }
+
+typedef struct {
+    Topology* top;
+    int32_t hosts;
+    int64_t packets;
+    unsigned seed;
+    int64_t routable, mismatches;
+    double latency_sum;
+} Worker;
+
+static void* worker_run(void* arg) {
+    Worker* w = (Worker*)arg;
+    for (int64_t p = 0; p < w->packets; ++p) {
+        const spe_in_addr_t s = host_addr(rand_r(&w->seed) % w->hosts);
+        const spe_in_addr_t d = host_addr(rand_r(&w->seed) % w->hosts);
+        double lat = 0.0, rel = 0.0;
+        const int32_t ok = topology_getPathInfo(w->top, s, d, &lat, &rel);
+        if (ok) {
+            ++w->routable;
+            w->latency_sum += lat;
+            topology_incrementPathPacketCounter(w->top, s, d);
+        }
+        if ((p & 63) == 0) {   /* worker_sendPacket's original three calls */
+            const int32_t ok3 = topology_isRoutable(w->top, s, d);
+            const double rel3 = topology_getReliability(w->top, s, d);
+            const double lat3 = topology_getLatency(w->top, s, d);
+            if (ok3 != ok || rel3 != rel || lat3 != lat) ++w->mismatches;
+        }
+    }
+    return NULL;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 4) {
+        fprintf(stderr, "usage: %s <graph.graphml> <hosts> <packets> [threads] [seed]\n", argv[0]);
+        return 2;
+    }
+    const int32_t hosts = atoi(argv[2]);
+    const int64_t packets = atoll(argv[3]);
+    const int32_t threads = argc > 4 ? atoi(argv[4]) : 4;
+    unsigned seed = argc > 5 ? (unsigned)atoi(argv[5]) : 1u;
+    if (hosts < 1 || packets < 0 || threads < 1) return 2;
+
+    const double t0 = now_s();
+    Topology* top = topology_new(argv[1]);
+    if (!top) {
+        fprintf(stderr, "topology_new failed for %s\n", argv[1]);
+        return 2;
+    }
+    const double t1 = now_s();
+    for (int32_t i = 0; i < hosts; ++i) {
+        uint64_t bw_down = 0, bw_up = 0;
+        topology_attach(top, host_addr(i), next_double, &seed, NULL, NULL, NULL, NULL, NULL, &bw_down, &bw_up);
+    }
+    int32_t distinct = 0;
+    {   /* attached vertices (a host maps to one vertex; several hosts may share it) */
+        const int32_t n = topology_vertex_count(top);
+        uint8_t* seen = (uint8_t*)calloc((size_t)n, 1);
+        for (int32_t i = 0; i < hosts; ++i) {
+            const int32_t v = topology_attached_vertex(top, host_addr(i));
+            if (v >= 0 && v < n && !seen[v]) {
+                seen[v] = 1;
+                ++distinct;
+            }
+        }
+        free(seen);
+    }
+    const double t2 = now_s();
+    if (topology_seal(top) != 0) {
+        fprintf(stderr, "topology_seal failed\n");
+        topology_free(top);
+        return 2;
+    }
+    const double t3 = now_s();
+
+    Worker* ws = (Worker*)calloc((size_t)threads, sizeof(Worker));
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    for (int32_t k = 0; k < threads; ++k) {
+        ws[k].top = top;
+        ws[k].hosts = hosts;
+        ws[k].packets = packets / threads + (k < packets % threads ? 1 : 0);
+        ws[k].seed = seed + 7919u * (unsigned)(k + 1);
+        pthread_create(&th[k], NULL, worker_run, &ws[k]);
+    }
+    int64_t routable = 0, mismatches = 0;
+    double latency_sum = 0.0;
+    for (int32_t k = 0; k < threads; ++k) {
+        pthread_join(th[k], NULL);
+        routable += ws[k].routable;
+        mismatches += ws[k].mismatches;
+        latency_sum += ws[k].latency_sum;
+    }
+    const double t4 = now_s();
+    /* the counters are per (src, dst) pair and atomic: re-count one pair */
+    const uint64_t c00 = topology_path_packet_count(top, host_addr(0), host_addr(0));
+    const double min_lat = topology_min_path_latency(top);
+    printf("{\"graph\": \"%s\", \"vertices\": %d, \"hosts\": %d, \"attached_vertices\": %d, "
+           "\"load_s\": %.4f, \"attach_s\": %.4f, \"seal_s\": %.4f, \"packets\": %lld, \"threads\": %d, "
+           "\"packets_per_s\": %.1f, \"routable\": %lld, \"latency_sum\": %.6f, \"min_path_latency\": %.6f, "
+           "\"count_pair_0_0\": %llu, \"mismatches\": %lld}\n",
+           argv[1], topology_vertex_count(top), hosts, distinct, t1 - t0, t2 - t1, t3 - t2, (long long)packets,
+           threads, packets > 0 ? (double)packets / (t4 - t3) : 0.0, (long long)routable, latency_sum, min_lat,
+           (unsigned long long)c00, (long long)mismatches);
+    free(th);
+    free(ws);
+    topology_free(top);
+    return mismatches == 0 ? 0 : 1;
+}

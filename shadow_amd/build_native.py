@@ -1,5 +1,6 @@
-"""Build libspe.so (gfx950 HIP kernels + C ABI) and libshdtopo.so (C host shim)
-in-tree with hipcc / gcc.  Used by __graft_entry__.build()."""
+"""Build libspe.so (gfx950 HIP kernels + C ABI), libshdtopo.so (C host shim) and
+the C demo in-tree with hipcc / gcc.  Used by __graft_entry__.build(); the
+CMake build (CMakeLists.txt) produces the same artefacts for a Shadow build."""
 from __future__ import annotations
 
 import os
@@ -12,6 +13,7 @@ CSRC = os.path.join(HERE, "csrc")
 HOST = os.path.join(HERE, "host")
 LIB_SPE = os.path.join(HERE, "libspe.so")
 LIB_TOPO = os.path.join(HERE, "libshdtopo.so")
+DEMO = os.path.join(HERE, "shd_topology_demo")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HIP_FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
@@ -51,9 +53,19 @@ def build_topo(force: bool = False) -> str:
     return LIB_TOPO
 
 
+def build_demo(force: bool = False) -> str:
+    """examples/shd_topology_demo.c: a Shadow-worker-shaped C user of libshdtopo."""
+    src = os.path.join(ROOT, "examples", "shd_topology_demo.c")
+    if force or _stale(DEMO, [src, LIB_TOPO, os.path.join(ROOT, "include", "shd_topology_spe.h")]):
+        _run(["gcc", "-O2", "-std=c11", "-D_GNU_SOURCE", "-Wall", "-o", DEMO, src, "-I", os.path.join(ROOT, "include"),
+              "-L", HERE, "-lshdtopo", "-lspe", "-Wl,-rpath,$ORIGIN", "-lpthread"])
+    return DEMO
+
+
 def build_all(force: bool = False) -> None:
     build_spe(force)
     build_topo(force)
+    build_demo(force)
 
 
 if __name__ == "__main__":

@@ -1468,10 +1468,14 @@ __global__ __launch_bounds__(BLOCK) void k_lookup(const int2* __restrict__ pairs
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_min_latency(const double2* __restrict__ lr, int64_t elems,
-                                                       unsigned long long* out) {
+// SB64 elements ((block - blk0) * A + t) * 64 + lane; lanes of the last block at
+// or past A are padding (no source) and never count
+__global__ __launch_bounds__(BLOCK) void k_min_latency(const double2* __restrict__ lr, int64_t elems, int32_t A,
+                                                       int32_t blk0, unsigned long long* out) {
     double m = INF;
     for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < elems; i += (int64_t)gridDim.x * BLOCK) {
+        const int64_t slot = (i / ((int64_t)A * WAVE) + blk0) * WAVE + (i & (WAVE - 1));
+        if (slot >= A) continue;
         const double l = lr[i].x;
         if (l > -1.0 && l < m) m = l;
     }
@@ -2598,7 +2602,8 @@ int spe_table_min_latency(const spe_table* t, double* out) {
     const unsigned long long init = 0x7FF0000000000000ull;  // +inf
     HIP_TRY(hipMemcpyAsync(t->d_min, &init, sizeof(init), hipMemcpyHostToDevice, t->stream));
     const int64_t elems = (int64_t)(t->blk1 - t->blk0) * t->A * WAVE;
-    k_min_latency<<<grid_for(elems, BLOCK, 4096), BLOCK, 0, t->stream>>>(t->tb.lr, elems, t->d_min);
+    k_min_latency<<<grid_for(elems, BLOCK, 4096), BLOCK, 0, t->stream>>>(t->tb.lr, elems, t->A, t->blk0,
+                                                                        t->d_min);
     HIP_TRY(hipGetLastError());
     unsigned long long bits = 0;
     HIP_TRY(hipMemcpyAsync(&bits, t->d_min, sizeof(bits), hipMemcpyDeviceToHost, t->stream));

@@ -236,3 +236,14 @@ def test_external_storage_and_prefilled_table(spe):
     e = ((s // 64) * top.n + tt) * 64 + s % 64
     assert bufs[0][e, 0].item() == out["lat"][s, tt] and bufs[0][e, 1].item() == out["rel"][s, tt]
     assert bufs[1][e].item() == out["next"][s, tt]
+
+
+def test_min_latency_ignores_padding_lanes(spe):
+    """minimumPathLatency (shd-topology.c:1359-1370) over a table whose last
+    64-source block is partly padding (A = 100): the min over real entries only."""
+    top = graphs.gen_random_small(600, 1800, 23)
+    A = np.sort(np.random.default_rng(23).choice(top.n, 100, replace=False)).astype(np.int32)
+    out, t, _ = run_gpu(spe, top, A)
+    ref = Oracle(top).rows(A, A)
+    ok = ref["kind"] != 0
+    assert t.min_latency() == ref["lat"][ok].min() > 0
