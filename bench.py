@@ -363,8 +363,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--blocks-per-step", type=int, default=16)
     ap.add_argument("--groups", type=int, default=0)
-    ap.add_argument("--engine", type=int, default=0, help="0 auto, 1 batch (64-lane HBM state), 2 LDS-resident rows, "
-                    "3 L2-resident distances")
+    ap.add_argument("--engine", type=int, default=0, help="0 auto, 1 batch (64-lane HBM state), 2 LDS-resident rows")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
@@ -456,23 +455,19 @@ def main():
     roof = None
     extra = {}
     lds = kp is not None and kp["lds"]["launches"] > 0
-    l2 = kp is not None and kp["l2"]["launches"] > 0
-    fused = lds or l2   # one kernel per source row: relaxation + row writes
-    direct = kp is not None and kp["direct"]["launches"] > 0 and kp["relax"]["launches"] == 0 and not fused
-    if fused:
+    direct = kp is not None and kp["direct"]["launches"] > 0 and kp["relax"]["launches"] == 0 and not lds
+    if lds:   # one fused kernel: relaxation in LDS + row writes
         b_relax += b_rows
     if direct:   # complete graph: every row is DIRECT, 38 B per pair
         b_relax = 38.0 * A
     if kp is not None:
-        kind = "lds" if lds else ("l2" if l2 else ("direct" if direct else "relax"))
-        kname = {"lds": "k_sssp_lds", "l2": "k_sssp_l2", "direct": "k_rows_direct", "relax": "k_relax"}[kind]
-        rl = kp[kind]
+        kname = "k_sssp_lds" if lds else ("k_rows_direct" if direct else "k_relax")
+        rl = kp["lds" if lds else ("direct" if direct else "relax")]
         relax_s = rl["ms"] / 1e3
         ach = b_relax * done / relax_s / 1e9 if relax_s > 0 else 0.0
         traffic = pmc_traffic(args, kname)
-        note = {"lds": " (SSSP + rows, LDS-resident state)", "l2": " (SSSP + rows, L2-resident distances, LDS bounds)",
-                "direct": " (DIRECT rows)", "relax": " (SSSP stage)"}[kind]
-        roof = {"bound": "hbm", "kernel": kname + note,
+        roof = {"bound": "hbm", "kernel": kname + (" (SSSP + rows, LDS-resident state)" if lds else
+                                                   (" (DIRECT rows)" if direct else " (SSSP stage)")),
                 "achieved": round(ach, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "launches": rl["launches"], "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
@@ -485,8 +480,8 @@ def main():
                                   "algorithmic_bytes_per_source": b_rows}
         extra["kernel_ms"] = {k: round(v["ms"], 3) for k, v in kp.items()}
         extra["kernel_launches"] = {k: v["launches"] for k, v in kp.items()}
-        extra["pipeline_frac_of_hbm"] = round((b_relax + (0 if fused else b_rows)) * value / 1e9 / HBM_PEAK_GBS, 4)
-        extra["engine"] = {"lds": "lds", "l2": "l2", "direct": "direct", "relax": "batch"}[kind]
+        extra["pipeline_frac_of_hbm"] = round((b_relax + (0 if lds else b_rows)) * value / 1e9 / HBM_PEAK_GBS, 4)
+        extra["engine"] = "lds" if lds else ("direct" if direct else "batch")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(top, att, args.cpu_seconds)

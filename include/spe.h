@@ -55,7 +55,6 @@ extern "C" {
 #define SPE_ENGINE_AUTO 0    /* LDS engine when the relaxation graph fits one CU's LDS, else BATCH */
 #define SPE_ENGINE_BATCH 1   /* 64-source lane groups, HBM-resident state, frontier rounds */
 #define SPE_ENGINE_LDS 2     /* one workgroup per source row, state resident in LDS (<= 10,240 relaxation vertices) */
-#define SPE_ENGINE_L2 3      /* one workgroup per source row, distances in L2-resident scratch, bf16 bounds in LDS (<= ~58k) */
 
 typedef struct spe_graph spe_graph;
 typedef struct spe_table spe_table;
@@ -178,7 +177,7 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
 /* Per-kernel device time, from HIP events recorded around every launch on the
  * build stream while profiling is enabled (costs one event pair per launch). */
 enum { SPE_K_INIT = 0, SPE_K_SEED, SPE_K_HEAVY, SPE_K_RELAX, SPE_K_ROWS, SPE_K_DIRECT, SPE_K_LDS, SPE_K_FW,
-       SPE_K_L2, SPE_K_COUNT };
+       SPE_K_COUNT };
 typedef struct spe_kernel_profile {
     double ms[SPE_K_COUNT];
     int64_t launches[SPE_K_COUNT];

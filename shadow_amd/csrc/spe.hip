@@ -1376,518 +1376,6 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
 #undef LDS_PHASE
 }
 
-// ------------------------------------------------------------------------
-// L2 engine: one workgroup per source row like the LDS engine, for relaxation
-// graphs too large for LDS-resident distances (C3's 50k, C4's 20k core: up to
-// ~60k vertices).  The exact f64 distances live in a per-workgroup global
-// array (L2 / Infinity-Cache resident: 8 B per vertex, 256 rows in flight) and
-// are updated with 64-bit atomicMin at L2; LDS holds a bf16 upper bound of
-// every distance (2 B per vertex), the two frontier bitsets and the push lists.
-// A candidate above the bound cannot improve and costs no global atomic, so
-// only (near-)improving relaxations reach L2.  The bound stays an upper bound
-// under races: it is only ever written after a successful atomicMin with that
-// candidate, and distances only decrease.
-// Parent pass, tree pass (child lists + level queue in global scratch, hops in
-// LDS) and rows as in the LDS engine; same bit-exactness argument (least
-// fixpoint of d[v] = min fl(d[u] + w); path-order folds from final parents).
-struct alignas(16) TreeItem {
-    int32_t v;
-    int32_t f;      // first hop (original id), -1 at a core source
-    double r;       // reliability fold up to v
-};
-struct L2Scratch {              // [grid][nc] each
-    unsigned long long* d;      // distance bits (non-negative doubles order as integers)
-    int32_t* par;               // in-CSR entry of the parent edge
-    int32_t* coff;              // child-list offsets
-    int32_t* pvt;               // parent vertex
-    int32_t* child;
-    double* cia;                // 1 - p of each child's parent edge, aligned with child
-    TreeItem* q;                // vertices in hop-level order
-    double* r;                  // reliability fold
-    int32_t* f;                 // first hop
-};
-
-// bf16 (top half of an f32) upper bound of a non-negative double, and its value
-__device__ __forceinline__ uint16_t bf16_up(double x) {
-    float f = (float)x;
-    if ((double)f < x) f = __uint_as_float(__float_as_uint(f) + 1u);
-    return (uint16_t)((__float_as_uint(f) + 0xFFFFu) >> 16);
-}
-__device__ __forceinline__ double bf16_val(uint16_t k) { return (double)__uint_as_float((uint32_t)k << 16); }
-
-// Every global array of the L2 engine is private to one workgroup, hence one
-// CU: workgroup scope is the coherence it needs.  (Agent scope would write back
-// and invalidate the whole L2 at every barrier on this multi-XCD part, and send
-// atomic loads past the L2.)  Atomics execute in the L2; workgroup-scope atomic
-// loads (sc0) read there too, so a wave sees its siblings' atomicMin results.
-__device__ __forceinline__ void gsync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-template <typename T>
-__device__ __forceinline__ T ld_wg(const T* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ double load_d(const unsigned long long* p) {
-    return __longlong_as_double((long long)ld_wg(p));
-}
-__device__ __forceinline__ unsigned long long amin_wg(unsigned long long* p, unsigned long long v) {
-    return __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ int32_t wave_append(bool ok, int32_t lane, int32_t* tail) {
-    const uint64_t m = __ballot(ok);
-    int32_t b = 0;
-    if (lane == 0 && m) b = atomicAdd(tail, __popcll(m));
-    b = __shfl(b, 0);
-    return b + __popcll(m & ((1ull << lane) - 1ull));
-}
-
-// FB u16 (bf16 bound during the push, hops afterwards) | 2 bitsets | push lists + owner maps
-__host__ __device__ constexpr size_t l2e_bytes(int32_t nc) {
-    return lds_align((size_t)nc * 2) + 2 * lds_align((size_t)((nc + 31) / 32) * 4) + (size_t)LDS_CAND_BYTES;
-}
-
-__global__ __launch_bounds__(LDS_T) void k_sssp_l2(int32_t slot0, int32_t slot1, const SlotInfo* __restrict__ slots,
-                                                    int32_t blk0, DevGraph G, RowMode md, Table tb, L2Scratch sc_,
-                                                    unsigned long long* __restrict__ dbg) {
-    extern __shared__ __align__(16) unsigned char smem[];
-    const int32_t nc = G.n;
-    const int32_t nw = (nc + 31) / 32;
-    uint16_t* FB = reinterpret_cast<uint16_t*>(smem);
-    uint16_t* H = FB;   // hop counts once the push is done
-    uint32_t* F0 = reinterpret_cast<uint32_t*>(smem + lds_align((size_t)nc * 2));
-    uint32_t* F1 = F0 + lds_align((size_t)nw * 4) / 4;
-    unsigned char* hs = reinterpret_cast<unsigned char*>(F1 + lds_align((size_t)nw * 4) / 4);
-    __shared__ int32_t s_any[3], s_tail, s_total, s_wsum[LDS_WAVES];
-    uint32_t syncix = 0;
-    const int32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
-    if (tid < 3) s_any[tid] = 0;
-    const unsigned long long INF_BITS = 0x7FF0000000000000ull;
-    const int32_t gx = gridDim.x;
-    const int32_t bx = (gx % 8 == 0) ? (blockIdx.x % 8) * (gx / 8) + blockIdx.x / 8 : blockIdx.x;
-    const size_t wo = (size_t)blockIdx.x * nc;
-    unsigned long long* Dg = sc_.d + wo;
-    int32_t* Xg = sc_.par + wo;
-    int32_t* coff = sc_.coff + wo;
-    int32_t* pvt = sc_.pvt + wo;
-    int32_t* child = sc_.child + wo;
-    double* cia = sc_.cia + wo;
-    TreeItem* Q = sc_.q + wo;
-    double* Rg = sc_.r + wo;
-    int32_t* Fg = sc_.f + wo;
-    for (int32_t slot = slot0 + bx; slot < slot1; slot += gx) {
-        const int32_t s = slots[slot].t;
-        unsigned long long tph = dbg && tid == 0 ? wall_clock64() : 0, nround = 0, nlev = 0;
-#define L2_PHASE(i)                                                         \
-    if (dbg && tid == 0) {                                                  \
-        const unsigned long long now = wall_clock64();                      \
-        atomicAdd(&dbg[i], now - tph);                                      \
-        tph = now;                                                          \
-    }
-        const int32_t sc = G.core_id[s];
-        const int32_t seed = sc >= 0 ? sc : G.anchor_core[s];
-        for (int32_t v = tid; v < nc; v += LDS_T) {
-            Dg[v] = INF_BITS;
-            FB[v] = 0x7F80;   // +inf
-        }
-        for (int32_t w = tid; w < nw; w += LDS_T) {
-            F0[w] = 0;
-            F1[w] = 0;
-        }
-        gsync();
-        if (tid == 0) {
-            // pruned pendant source: its first step s -> anchor is fixed (see k_init_state)
-            const double d0 = sc >= 0 ? 0.0 : 0.0 + G.fiw[G.fiptr[s]];
-            amin_wg(&Dg[seed], (unsigned long long)__double_as_longlong(d0));
-            FB[seed] = bf16_up(d0);
-            F0[seed >> 5] = 1u << (seed & 31);
-        }
-        gsync();
-        L2_PHASE(0)
-        // 1. push relaxation to the fixpoint (lists as in the LDS engine)
-        uint32_t* cur = F0;
-        uint32_t* nxt = F1;
-        int32_t* wl = reinterpret_cast<int32_t*>(hs) + wave * LDS_WL;
-        uint8_t* om = hs + LDS_WAVES * LDS_WL * 4 + wave * LDS_WIN * WAVE;
-        for (;;) {
-            bool any = false;
-            int32_t cnt = 0;
-            auto flush = [&]() {
-                for (int32_t lb = 0; lb < cnt; lb += WAVE) {
-                    const int32_t v = lb + lane < cnt ? wl[lb + lane] : -1;
-                    int32_t k0 = 0, deg = 0;
-                    double dv = 0.0;
-                    if (v >= 0) {
-                        k0 = G.optr[v];
-                        deg = G.optr[v + 1] - k0;
-                        dv = load_d(&Dg[v]);
-                    }
-                    int32_t incl = deg;
-#pragma unroll
-                    for (int d = 1; d < WAVE; d <<= 1) {
-                        const int32_t y = __shfl_up(incl, d);
-                        if (lane >= d) incl += y;
-                    }
-                    const int32_t total = __shfl(incl, WAVE - 1);
-                    const int32_t excl = incl - deg;
-                    for (int32_t base = 0; base < total; base += LDS_WIN * WAVE) {
-                        int32_t x[LDS_WIN];
-                        double cand[LDS_WIN];
-                        bool ok[LDS_WIN];
-                        for (int32_t i = max(excl, base), ie = min(incl, base + LDS_WIN * WAVE); i < ie; ++i)
-                            om[i - base] = (uint8_t)lane;
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-                        for (int h = 0; h < LDS_WIN; ++h) {
-                            const int32_t e = base + h * WAVE + lane;
-                            const int32_t o = e < total ? om[e - base] : 0;
-                            const int32_t k = __shfl(k0, o) + e - __shfl(excl, o);
-                            const double du = __shfl(dv, o);
-                            ok[h] = e < total;
-                            x[h] = ok[h] ? G.ocol[k] : 0;
-                            cand[h] = ok[h] ? du + G.ow[k] : 0.0;
-                        }
-#pragma unroll
-                        for (int h = 0; h < LDS_WIN; ++h) {
-                            if (!ok[h] || cand[h] > bf16_val(FB[x[h]])) continue;   // cannot improve
-                            const unsigned long long cb = (unsigned long long)__double_as_longlong(cand[h]);
-                            if (cb < amin_wg(&Dg[x[h]], cb)) {
-                                FB[x[h]] = bf16_up(cand[h]);
-                                atomicOr(&nxt[x[h] >> 5], 1u << (x[h] & 31));
-                                any = true;
-                            }
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                    }
-                }
-                cnt = 0;
-            };
-            for (int32_t w0 = wave; w0 < nw; w0 += LDS_WAVES * WAVE) {
-                const int32_t wi = w0 + lane * LDS_WAVES;
-                uint32_t W = wi < nw ? cur[wi] : 0u;
-                uint64_t pend = __ballot(W != 0);
-                if (!pend) continue;
-                if (W) cur[wi] = 0;
-                while (pend) {
-                    const bool mine = (pend >> lane) & 1ull;
-                    const int32_t c = mine ? __popc(W) : 0;
-                    int32_t incl = c;
-#pragma unroll
-                    for (int d = 1; d < WAVE; d <<= 1) {
-                        const int32_t y = __shfl_up(incl, d);
-                        if (lane >= d) incl += y;
-                    }
-                    const bool fit = mine && incl <= LDS_WL - cnt;
-                    const uint64_t fm = __ballot(fit);
-                    if (!fm) {
-                        flush();
-                        continue;
-                    }
-                    if (fit) {
-                        int32_t pos = cnt + incl - c;
-                        for (uint32_t x = W; x; x &= x - 1) wl[pos++] = wi * 32 + __builtin_ctz(x);
-                    }
-                    cnt += __shfl(incl, 63 - __builtin_clzll(fm));
-                    pend &= ~fm;
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    if (pend) flush();
-                }
-            }
-            if (cnt) flush();
-            ++nround;
-            if (!wg_any(any, syncix, s_any)) break;
-            uint32_t* tmp = cur;
-            cur = nxt;
-            nxt = tmp;
-        }
-        gsync();   // distances final
-        L2_PHASE(1)
-        auto D = [&](int32_t v) { return load_d(&Dg[v]); };
-        // 2. canonical parents into Xg (as the LDS engine's pass 2)
-        for (int32_t v = tid; v < nc; v += LDS_T) Xg[v] = (v == seed) ? (sc >= 0 ? -1 : -2) : -1;
-        for (int32_t w = tid; w < nw; w += LDS_T) {
-            F0[w] = 0;
-            F1[w] = 0;
-        }
-        gsync();
-        {
-            const int32_t m_rel = G.iptr[nc];
-            constexpr int U = 4;
-            for (int32_t e0 = tid; e0 < m_rel; e0 += U * LDS_T) {
-                int32_t u[U], v[U];
-                double w[U], du[U], dv[U];
-#pragma unroll
-                for (int q = 0; q < U; ++q) {
-                    const int32_t e = e0 + q * LDS_T;
-                    u[q] = -1;
-                    if (e < m_rel) {
-                        u[q] = G.icol[e];
-                        v[q] = G.irow[e];
-                        w[q] = G.iw[e];
-                    }
-                }
-#pragma unroll
-                for (int q = 0; q < U; ++q) {
-                    du[q] = u[q] >= 0 ? D(u[q]) : INF;
-                    dv[q] = u[q] >= 0 ? D(v[q]) : INF;
-                }
-#pragma unroll
-                for (int q = 0; q < U; ++q) {
-                    if (u[q] < 0 || v[q] == seed) continue;
-                    const double alt = du[q] + w[q];
-                    if (du[q] < INF && alt == dv[q] && alt > du[q]) {
-                        const uint32_t bit = 1u << (v[q] & 31);
-                        if (atomicOr(&F0[v[q] >> 5], bit) & bit) atomicOr(&F1[v[q] >> 5], bit);
-                        else Xg[v[q]] = e0 + q * LDS_T;
-                    }
-                }
-            }
-        }
-        gsync();
-        for (int32_t v = tid; v < nc; v += LDS_T) {   // exact ties: canonical argmin (d[u], u)
-            if (!((F1[v >> 5] >> (v & 31)) & 1u)) continue;
-            const double dv = D(v);
-            double bdu = INF;
-            int32_t bu = -1, bk = -1;
-            for (int32_t k = G.iptr[v]; k < G.iptr[v + 1]; ++k) {
-                const int32_t u = G.icol[k];
-                const double du = D(u);
-                if (!(du < INF)) continue;
-                const double alt = du + G.iw[k];
-                if (alt == dv && alt > du && (du < bdu || (du == bdu && u < bu))) {
-                    bdu = du;
-                    bu = u;
-                    bk = k;
-                }
-            }
-            Xg[v] = bk;
-        }
-        gsync();
-        L2_PHASE(2)
-        // 3. latencies
-        const int32_t sb_local = slot / WAVE - blk0, lane_s = slot % WAVE;
-        for (int32_t j = tid; j < tb.A; j += LDS_T) {
-            const SlotInfo si = slots[j];
-            if (si.t == s) continue;
-            const size_t o = tidx(sb_local, tb.A, j, lane_s);
-            const double dc = D(si.c);
-            if (!(dc < INF)) {
-                tb.lr[o] = make_double2(-1.0, -1.0);
-                tb.next[o] = -1;
-                tb.hops[o] = 0;
-                if (tb.prev) tb.prev[o] = -1;
-            } else if (!md.multi_rep) {
-                double l = si.kt >= 0 ? dc + si.pw : dc;
-                if (l == 0) l = 1;   // shd-topology.c:1833-1837
-                tb.lr[o].x = l;
-            }
-        }
-        L2_PHASE(3)
-        // 4a. child lists of the parent tree (global scratch), hops in LDS
-        for (int32_t v = tid; v < nc; v += LDS_T) {
-            coff[v] = 0;
-            H[v] = 0xFFFF;
-        }
-        gsync();
-        for (int32_t v0 = tid; v0 < nc; v0 += 4 * LDS_T) {
-            int32_t p[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int32_t v = v0 + q * LDS_T;
-                const int32_t k = v < nc ? Xg[v] : -1;
-                p[q] = k >= 0 ? par_vertex(G, k) : -1;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int32_t v = v0 + q * LDS_T;
-                if (v >= nc) continue;
-                pvt[v] = p[q];
-                if (p[q] >= 0) __hip_atomic_fetch_add(&coff[p[q]], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        }
-        gsync();
-        {   // inclusive scan of the child counts (thread = contiguous segment)
-            const int32_t per = (nc + LDS_T - 1) / LDS_T;
-            const int32_t b0 = min(nc, tid * per), b1 = min(nc, b0 + per);
-            int32_t sum = 0;
-            for (int32_t i = b0; i < b1; ++i) sum += ld_wg(&coff[i]);
-            int32_t incl = sum;
-#pragma unroll
-            for (int d = 1; d < WAVE; d <<= 1) {
-                const int32_t y = __shfl_up(incl, d);
-                if (lane >= d) incl += y;
-            }
-            if (lane == WAVE - 1) s_wsum[wave] = incl;
-            __syncthreads();
-            int32_t wbase = 0;
-            for (int32_t q = 0; q < wave; ++q) wbase += s_wsum[q];
-            int32_t run = wbase + incl - sum;
-            for (int32_t i = b0; i < b1; ++i) {
-                run += ld_wg(&coff[i]);
-                coff[i] = run;
-            }
-            if (tid == LDS_T - 1) s_total = run;
-        }
-        gsync();
-        for (int32_t v0 = tid; v0 < nc; v0 += 4 * LDS_T) {
-            int32_t p[4];
-            double a[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int32_t v = v0 + q * LDS_T;
-                p[q] = v < nc ? pvt[v] : -1;
-                a[q] = p[q] >= 0 ? G.ia[Xg[v]] : 0.0;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (p[q] < 0) continue;
-                const int32_t pos = __hip_atomic_fetch_add(&coff[p[q]], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) - 1;
-                child[pos] = v0 + q * LDS_T;
-                cia[pos] = a[q];
-            }
-        }
-        if (tid == 0) {
-            const double fs = G.vfac[s];
-            const double r0 = has_attr(fs) ? 1.0 * fs : 1.0;   // shd-topology.c:1428-1430
-            TreeItem it;
-            it.v = seed;
-            it.f = sc >= 0 ? -1 : G.corev[seed];
-            it.r = sc >= 0 ? r0 : r0 * G.fia[G.fiptr[s]];
-            Q[0] = it;
-            Rg[seed] = it.r;
-            Fg[seed] = it.f;
-            H[seed] = sc >= 0 ? 0 : 1;
-            s_tail = 1;
-        }
-        gsync();
-        L2_PHASE(4)
-        // 4b. top-down over the tree, one hop level per step
-        {
-            const int32_t total = s_total;
-            int32_t lb = 0, le = 1;
-            uint16_t hl = sc >= 0 ? 1 : 2;
-            while (lb < le) {
-                for (int32_t i0 = lb + wave * WAVE; i0 < le; i0 += LDS_T) {
-                    const int32_t i = i0 + lane;
-                    int32_t u = -1, fu = -1, cs = 0, cn = 0;
-                    double ru = 0.0;
-                    if (i < le) {
-                        const TreeItem it = Q[i];
-                        u = it.v;
-                        fu = it.f;
-                        ru = it.r;
-                        cs = ld_wg(&coff[u]);
-                        cn = (u + 1 < nc ? ld_wg(&coff[u + 1]) : total) - cs;
-                    }
-                    wave_expand(lane, cn, [&](bool ok, int32_t o, int32_t off, int32_t, int32_t, int32_t) {
-                        const int32_t uo = __shfl(u, o), fo = __shfl(fu, o), co = __shfl(cs, o);
-                        const double ro = __shfl(ru, o);
-                        TreeItem it;
-                        if (ok) {
-                            it.v = child[co + off];
-                            it.r = ro * cia[co + off];
-                            it.f = (uo == sc) ? G.corev[it.v] : fo;
-                            H[it.v] = hl;
-                            Rg[it.v] = it.r;
-                            Fg[it.v] = it.f;
-                        }
-                        const int32_t pos = wave_append(ok, lane, &s_tail);
-                        if (ok) Q[pos] = it;
-                    });
-                }
-                ++nlev;
-                gsync();
-                lb = le;
-                le = s_tail;
-                ++hl;
-                __syncthreads();
-            }
-        }
-        L2_PHASE(5)
-        // 5. reliability, next hop, hops (+ latency re-fold for multigraphs)
-        for (int32_t j = tid; j < tb.A; j += LDS_T) {
-            const SlotInfo si = slots[j];
-            const int32_t t = si.t;
-            const size_t o = tidx(sb_local, tb.A, j, lane_s);
-            if (t == s) {
-                double Lt = -1.0, R = -1.0;
-                int32_t N = -1, Hh = 0;
-                self_entry(G, md, s, Lt, R, N, Hh);
-                tb.lr[o] = make_double2(Lt, R);
-                tb.next[o] = N;
-                tb.hops[o] = (uint16_t)Hh;
-                if (tb.prev) tb.prev[o] = (Hh == 2) ? N : (Hh > 0 ? s : -1);
-                continue;
-            }
-            const int32_t c = si.c, kt = si.kt;
-            const uint16_t hc = H[c];
-            if (hc == 0xFFFF) continue;   // unreachable: written in pass 3
-            const int32_t Hh = hc + (kt >= 0 ? 1 : 0);
-            const double ft = G.vfac[t];
-            double R;
-            if (!has_attr(ft) || ft == 1.0) {
-                R = Rg[c] * si.pa;
-            } else {   // ((1 * fs) * ft) * a1 * a2 ... : the target factor comes second
-                const double fs = G.vfac[s];
-                double r = 1.0;
-                if (has_attr(fs)) r *= fs;
-                r *= ft;
-                for (int32_t i = 1; i <= Hh; ++i) {
-                    int32_t back = Hh - i;
-                    double ea;
-                    if (kt >= 0 && back == 0) {
-                        ea = si.pa;
-                    } else {
-                        int32_t x = c;
-                        if (kt >= 0) back -= 1;
-                        for (int32_t q = 0; q < back; ++q) x = par_vertex(G, Xg[x]);
-                        ea = Xg[x] >= 0 ? G.ia[Xg[x]] : G.fia[G.fiptr[s]];
-                    }
-                    r *= ea;
-                }
-                R = r;
-            }
-            if (md.multi_rep) {
-                double l = 0.0;
-                for (int32_t i = 1; i <= Hh; ++i) {
-                    int32_t back = Hh - i;
-                    double ew;
-                    if (kt >= 0 && back == 0) {
-                        ew = G.fiwrep[kt];
-                    } else {
-                        int32_t x = c;
-                        if (kt >= 0) back -= 1;
-                        for (int32_t q = 0; q < back; ++q) x = par_vertex(G, Xg[x]);
-                        ew = Xg[x] >= 0 ? G.iwrep[Xg[x]] : G.fiwrep[G.fiptr[s]];
-                    }
-                    l += ew;
-                }
-                if (l == 0) l = 1;
-                tb.lr[o].x = l;
-            }
-            tb.lr[o].y = R;
-            tb.next[o] = kt >= 0 && hc == 0 ? t : Fg[c];
-            tb.hops[o] = (uint16_t)Hh;
-            if (tb.prev) tb.prev[o] = kt >= 0 ? G.corev[c] : (Xg[c] >= 0 ? G.corev[par_vertex(G, Xg[c])] : s);
-        }
-        gsync();   // the next slot reuses every scratch array
-        L2_PHASE(6)
-        if (dbg && tid == 0) {
-            atomicAdd(&dbg[8], nround);
-            atomicAdd(&dbg[9], nlev);
-            atomicAdd(&dbg[10], 1ull);
-        }
-    }
-#undef L2_PHASE
-}
-
 // Owner replay (compat with the reference's first-writer-wins path cache,
 // _topology_shouldStorePath shd-topology.c:1292-1321 + the either-direction
 // lookup of _topology_getPathEntry :1952-2034): for each unordered slot pair,
@@ -2167,8 +1655,7 @@ struct spe_table {
     int32_t* d_slot_vertex = nullptr;
     SlotInfo* d_slots = nullptr;   // LDS engine: per-target constants
     LdsScratch lsc{};              // LDS engine: per-workgroup parent-entry scratch
-    int32_t lds_grid = 0;          // LDS / L2 engine: workgroups per launch (scratch is sized for it)
-    L2Scratch l2s{};               // L2 engine: per-workgroup distances + tree scratch
+    int32_t lds_grid = 0;          // LDS engine: workgroups per launch (scratch is sized for it)
     int32_t* d_rank = nullptr;     // owner replay: position of each slot in the source-run order
     int32_t* d_vertex_slot = nullptr;
     std::vector<int32_t> attached;
@@ -2511,7 +1998,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
             return fail(SPE_EUNSUPPORTED, "want_aux needs SSSP rows (force_sssp on complete/preferdirect graphs, "
                                           "no owner replay)");
         }
-        if (o.engine == SPE_ENGINE_LDS || o.engine == SPE_ENGINE_L2) {
+        if (o.engine == SPE_ENGINE_LDS) {
             delete t;
             return fail(SPE_EUNSUPPORTED, "want_aux runs on the batch engine");
         }
@@ -2544,24 +2031,19 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
             e = atoi(getenv("SPE_ENGINE"));
             from_env = true;
         }
-        const bool fits_l2 = l2e_bytes(g->hg.nc) <= (size_t)LDS_MAX_BYTES;
-        if ((e == SPE_ENGINE_LDS && !fits) || (e == SPE_ENGINE_L2 && !fits_l2)) {
+        if (e == SPE_ENGINE_LDS && !fits) {
             if (!from_env) {
                 delete t;
-                return fail(SPE_EUNSUPPORTED, "relaxation graph too large for the LDS / L2 engine");
+                return fail(SPE_EUNSUPPORTED, "relaxation graph too large for the LDS engine");
             }
             e = SPE_ENGINE_BATCH;
         }
         t->engine = (e == SPE_ENGINE_AUTO) ? (fits ? SPE_ENGINE_LDS : SPE_ENGINE_BATCH) : e;
-        if ((t->engine == SPE_ENGINE_LDS || t->engine == SPE_ENGINE_L2) && !t->md.complete) {
-            // no HBM batch state: one launch covers every owned block (unless asked otherwise)
+        if (t->engine == SPE_ENGINE_LDS && !t->md.complete) {
+            // no HBM state: one launch covers every owned block (unless asked otherwise)
             if (o.groups_per_launch <= 0) t->groups = std::max(1, t->blk1 - t->blk0);
-            if (t->engine == SPE_ENGINE_LDS)
-                HIP_TRY(hipFuncSetAttribute((const void*)k_sssp_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)lds_bytes(g->hg.nc)));
-            else
-                HIP_TRY(hipFuncSetAttribute((const void*)k_sssp_l2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)l2e_bytes(g->hg.nc)));
+            HIP_TRY(hipFuncSetAttribute((const void*)k_sssp_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds_bytes(g->hg.nc)));
         }
     }
     t->infl = lanes == 64 ? 8 : 4;
@@ -2614,7 +2096,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     t->d_slot_vertex = const_cast<int32_t*>(tmp);
     TRY(dev_upload(t->allocs, vslot, &tmp));
     t->d_vertex_slot = const_cast<int32_t*>(tmp);
-    if (!t->md.complete && (t->engine == SPE_ENGINE_LDS || t->engine == SPE_ENGINE_L2)) {
+    if (!t->md.complete && t->engine == SPE_ENGINE_LDS) {
         const spe::HostGraph& h = g->hg;
         std::vector<SlotInfo> si(n_attached);
         for (int32_t j = 0; j < n_attached; ++j) {
@@ -2639,23 +2121,10 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         t->d_slots = const_cast<SlotInfo*>(tsi);
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device);
-        const size_t lb = t->engine == SPE_ENGINE_LDS ? lds_bytes(h.nc) : l2e_bytes(h.nc);
-        const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, LDS_MAX_BYTES / lb));
+        const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, LDS_MAX_BYTES / lds_bytes(h.nc)));
         t->lds_grid = cus * per_cu;
         const size_t per = (size_t)t->lds_grid * std::max(1, h.nc);
-        if (t->engine == SPE_ENGINE_LDS) {
-            TRY(dev_alloc(t->allocs, &t->lsc.par, per));
-        } else {
-            TRY(dev_alloc(t->allocs, &t->l2s.d, per));
-            TRY(dev_alloc(t->allocs, &t->l2s.par, per));
-            TRY(dev_alloc(t->allocs, &t->l2s.coff, per));
-            TRY(dev_alloc(t->allocs, &t->l2s.pvt, per));
-            TRY(dev_alloc(t->allocs, &t->l2s.child, per));
-            TRY(dev_alloc(t->allocs, &t->l2s.cia, per));
-            TRY(dev_alloc(t->allocs, &t->l2s.q, per));
-            TRY(dev_alloc(t->allocs, &t->l2s.r, per));
-            TRY(dev_alloc(t->allocs, &t->l2s.f, per));
-        }
+        TRY(dev_alloc(t->allocs, &t->lsc.par, per));
     }
     const size_t G = (size_t)t->groups;
     const size_t GL = G * (WAVE / t->lanes);   // lane groups per batch
@@ -2870,35 +2339,6 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
         if (t->md.complete) {
             LaunchTimer lt(t, s, SPE_K_DIRECT);
             k_rows_direct<<<row_grid, BLOCK, 0, s>>>(groups, sb0, t->d_srcv, t->d_slot_vertex, g->dev, t->md, t->tb);
-        } else if (t->engine == SPE_ENGINE_L2) {
-            {
-                LaunchTimer lt(t, s, SPE_K_L2);
-                const int32_t s0 = b * WAVE, s1 = std::min(t->A, (b + groups) * WAVE);
-                int grid = std::min(s1 - s0, t->lds_grid);
-                if (getenv("SPE_L2_GRID")) grid = std::min(grid, std::max(8, atoi(getenv("SPE_L2_GRID"))));   // diagnostic
-                if (grid >= 8) grid -= grid % 8;   // whole XCD rounds (slot order as the LDS engine's)
-                if (getenv("SPE_LDS_DEBUG") && !t->d_lds_dbg) {
-                    if (int r = dev_alloc(t->allocs, &t->d_lds_dbg, 16)) return r;
-                    HIP_TRY(hipMemset(t->d_lds_dbg, 0, 16 * sizeof(unsigned long long)));
-                }
-                k_sssp_l2<<<std::max(1, grid), LDS_T, l2e_bytes(g->hg.nc), s>>>(s0, s1, t->d_slots, t->blk0, g->dev,
-                                                                               t->md, t->tb, t->l2s, t->d_lds_dbg);
-                if (t->d_lds_dbg) {
-                    unsigned long long h[16];
-                    HIP_TRY(hipStreamSynchronize(s));
-                    HIP_TRY(hipMemcpy(h, t->d_lds_dbg, sizeof(h), hipMemcpyDeviceToHost));
-                    const double nsrc = (double)std::max(1ull, h[10]);
-                    fprintf(stderr, "spe-l2 sources %llu rounds/src %.1f levels/src %.1f us/src: init %.1f push %.1f "
-                            "parent %.1f lat %.1f tree-build %.1f tree-pass %.1f rows %.1f\n", h[10], h[8] / nsrc,
-                            h[9] / nsrc, h[0] / nsrc / 100.0, h[1] / nsrc / 100.0, h[2] / nsrc / 100.0,
-                            h[3] / nsrc / 100.0, h[4] / nsrc / 100.0, h[5] / nsrc / 100.0, h[6] / nsrc / 100.0);
-                }
-            }
-            if (t->md.prefer) {
-                LaunchTimer lt(t, s, SPE_K_DIRECT);
-                k_direct_overlay<<<(groups * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(
-                    groups, sb0, t->d_srcv, t->d_vertex_slot, g->dev, t->tb);
-            }
         } else if (t->engine == SPE_ENGINE_LDS) {
             {
                 LaunchTimer lt(t, s, SPE_K_LDS);

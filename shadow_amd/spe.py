@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(_HERE, "libspe.so")
 SPE_OK = 0
 SPE_SELF_ROW = 0
 SPE_SELF_RULE = 1
-SPE_ENGINE_AUTO, SPE_ENGINE_BATCH, SPE_ENGINE_LDS, SPE_ENGINE_L2 = 0, 1, 2, 3
+SPE_ENGINE_AUTO, SPE_ENGINE_BATCH, SPE_ENGINE_LDS = 0, 1, 2
 WAVE = 64
 
 
@@ -62,11 +62,11 @@ class Entry(C.Structure):
                 ("hops", C.c_int32)]
 
 
-KERNELS = ["init", "seed", "heavy", "relax", "rows", "direct", "lds", "fw", "l2"]
+KERNELS = ["init", "seed", "heavy", "relax", "rows", "direct", "lds", "fw"]
 
 
 class KernelProfile(C.Structure):
-    _fields_ = [("ms", C.c_double * len(KERNELS)), ("launches", C.c_int64 * len(KERNELS))]
+    _fields_ = [("ms", C.c_double * 8), ("launches", C.c_int64 * 8)]
 
 
 class BuildStats(C.Structure):

@@ -22,14 +22,13 @@ def golden_dir():
     return GOLDEN
 
 
-@pytest.fixture(params=["1", "2", "3"], ids=["batch", "lds", "l2"], autouse=True)
+@pytest.fixture(params=["1", "2"], ids=["batch", "lds"], autouse=True)
 def engine_env(request, monkeypatch):
-    """Every GPU test runs on all three path engines (SPE_ENGINE: 1 = 64-lane
-    batch relaxation, 2 = LDS-resident per-source rows, 3 = per-source rows with
-    L2-resident distances; 2 and 3 fall back to batch when the graph does not
-    fit).  CPU tests run once."""
+    """Every GPU test runs on both path engines (SPE_ENGINE: 1 = 64-lane batch
+    relaxation, 2 = LDS-resident per-source rows; the LDS engine falls back to
+    batch when the graph does not fit).  CPU tests run once."""
     if request.node.get_closest_marker("gpu") is None or request.node.get_closest_marker("engine_fixed"):
-        if request.param != "1":
+        if request.param == "2":
             pytest.skip("engine-independent test (CPU, or picks its engine itself)")
         return
     monkeypatch.setenv("SPE_ENGINE", request.param)
