@@ -1928,6 +1928,22 @@ int spe_graph_info_get(const spe_graph* g, spe_graph_info* out) {
     return SPE_OK;
 }
 
+int spe_order_sources(const spe_graph* g, const int32_t* attached, int32_t n_attached, int32_t* order_out) {
+    if (!g || (n_attached > 0 && (!attached || !order_out))) return fail(SPE_EINVAL, "NULL argument");
+    if (n_attached < 0) return fail(SPE_EINVAL, "negative n_attached");
+    const spe::HostGraph& h = g->hg;
+    std::vector<std::pair<int64_t, int32_t>> key((size_t)n_attached);
+    for (int32_t i = 0; i < n_attached; ++i) {
+        const int32_t v = attached[i];
+        if (v < 0 || v >= h.n) return fail(SPE_EINVAL, "attached vertex out of range");
+        const int32_t c = h.core_id[v] >= 0 ? h.core_id[v] : h.anchor_core[v];
+        key[(size_t)i] = {c, v};
+    }
+    std::sort(key.begin(), key.end());
+    for (int32_t i = 0; i < n_attached; ++i) order_out[i] = key[(size_t)i].second;
+    return SPE_OK;
+}
+
 void spe_graph_free(spe_graph* g) {
     if (!g) return;
     (void)hipSetDevice(g->device);

@@ -798,6 +798,21 @@ int32_t topology_seal(Topology* top) {
             rc = SPE_ESTATE;
         } else {
             const double t0 = now_s();
+            /* slots are internal (queries resolve IP -> vertex -> slot): number them
+             * in the engine's source-clustering order (spe_order_sources) */
+            int32_t* ord = malloc(((size_t)A + 1) * sizeof(int32_t));
+            if (ord && spe_order_sources(top->graph, att, A, ord) == SPE_OK) {
+                pthread_rwlock_wrlock(&top->ip_lock);
+                for (int32_t i = 0; i < A; ++i) {
+                    top->attached[i] = ord[i];
+                    top->slot_of_vertex[ord[i]] = i;
+                }
+                pthread_rwlock_unlock(&top->ip_lock);
+                free(att);
+                att = ord;
+            } else {
+                free(ord);
+            }
             spe_table_opts o;
             memset(&o, 0, sizeof o);
             o.self_mode = SPE_SELF_ROW;
@@ -856,16 +871,19 @@ int32_t topology_seal(Topology* top) {
 static int pair_slots(Topology* top, uint32_t src, uint32_t dst, int32_t* s, int32_t* t) {
     pthread_rwlock_rdlock(&top->ip_lock);
     const int32_t sv = ip_get(top, src), dv = ip_get(top, dst);
-    *s = sv >= 0 ? top->slot_of_vertex[sv] : -1;
-    *t = dv >= 0 ? top->slot_of_vertex[dv] : -1;
     pthread_rwlock_unlock(&top->ip_lock);
-    if (*s < 0 || *t < 0) {
-        struct in_addr a = {*s < 0 ? src : dst};
+    if (sv < 0 || dv < 0) {
+        struct in_addr a = {sv < 0 ? src : dst};
         tlog(top, LOG_CRITICAL, "invalid vertex, address %s is not connected to topology", inet_ntoa(a));
         return 0;
     }
+    /* sealing numbers the slots (spe_order_sources): resolve them afterwards */
     if (topology_seal(top) != SPE_OK) return 0;
-    return 1;
+    pthread_rwlock_rdlock(&top->ip_lock);
+    *s = top->slot_of_vertex[sv];
+    *t = top->slot_of_vertex[dv];
+    pthread_rwlock_unlock(&top->ip_lock);
+    return *s >= 0 && *t >= 0;
 }
 
 double topology_getLatency(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {

@@ -76,6 +76,7 @@ class BuildStats(C.Structure):
 
 # every symbol include/spe.h declares (tests/test_abi.py checks the export table)
 EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_info_get", "spe_graph_free",
+           "spe_order_sources",
            "spe_table_create", "spe_table_build", "spe_table_build_blocks", "spe_table_profile_enable",
            "spe_table_profile_get", "spe_table_build_stats", "spe_table_layout_get",
            "spe_table_get", "spe_table_download", "spe_lookup_batch", "spe_table_min_latency",
@@ -104,6 +105,7 @@ def lib():
         L.spe_device_count.argtypes = [P]
         L.spe_graph_create.argtypes = [P, C.c_int32, P]
         L.spe_graph_info_get.argtypes = [P, P]
+        L.spe_order_sources.argtypes = [P, P, C.c_int32, P]
         L.spe_graph_free.argtypes = [P]
         L.spe_graph_free.restype = None
         L.spe_table_create.argtypes = [P, P, C.c_int32, P, P]
@@ -173,6 +175,13 @@ class Graph:
         _check(lib().spe_fw_apsp(self.h, C.c_void_p(d_dist), int(ld), C.c_void_p(d_next or None),
                                  C.c_void_p(stream or None), C.byref(sec)), "spe_fw_apsp")
         return float(sec.value)
+
+    def order_sources(self, attached) -> np.ndarray:
+        """spe_order_sources: a slot order clustering sources by relaxation anchor."""
+        a = np.ascontiguousarray(attached, dtype=np.int32)
+        out = np.empty_like(a)
+        _check(lib().spe_order_sources(self.h, a.ctypes.data, int(a.shape[0]), out.ctypes.data), "spe_order_sources")
+        return out
 
     def info(self) -> dict:
         i = GraphInfo()

@@ -103,3 +103,32 @@ def test_c4_sample_rows_full_size(spe):
     sample = np.arange(448, 576, 17)
     ora = Oracle(top).rows(A[sample], A)
     compare({k: v[sample - 448] for k, v in rows.items()}, ora, label="C4")
+
+
+def test_order_sources_clusters_by_anchor_and_keeps_rows(spe):
+    """spe_order_sources: a permutation of the attached set, grouped by
+    relaxation anchor (pendants next to the other pendants of their anchor);
+    a table built in that slot order holds the same rows per vertex pair."""
+    top = graphs.gen_tiered(n_core=300, n_stub=900, n_attached=500, seed=7)
+    att = graphs.tiered_attached(top, n_core=300, n_attached=500)
+    g = spe.Graph(top)
+    order = g.order_sources(att)
+    assert sorted(order.tolist()) == sorted(att.tolist())
+    nbr = {}
+    for a, b in zip(top.esrc.tolist(), top.edst.tolist()):
+        if a != b:
+            nbr.setdefault(a, set()).add(b)
+            nbr.setdefault(b, set()).add(a)
+    anchors = [next(iter(nbr[v])) if len(nbr[v]) == 1 else v for v in order.tolist()]
+    runs = sum(1 for i in range(1, len(anchors)) if anchors[i] != anchors[i - 1]) + 1
+    assert runs == len(set(anchors))   # every anchor's sources are contiguous
+    t1 = spe.PathTable(g, att)
+    t1.build()
+    a1 = t1.download()
+    t2 = spe.PathTable(g, order)
+    t2.build()
+    a2 = t2.download()
+    pos = {v: i for i, v in enumerate(order.tolist())}
+    p = np.array([pos[v] for v in att.tolist()])
+    for k in ("lat", "rel", "next", "hops", "ok"):
+        assert np.array_equal(a1[k], a2[k][np.ix_(p, p)]), k
