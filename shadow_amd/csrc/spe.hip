@@ -43,6 +43,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <queue>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -1932,15 +1934,70 @@ int spe_order_sources(const spe_graph* g, const int32_t* attached, int32_t n_att
     if (!g || (n_attached > 0 && (!attached || !order_out))) return fail(SPE_EINVAL, "NULL argument");
     if (n_attached < 0) return fail(SPE_EINVAL, "negative n_attached");
     const spe::HostGraph& h = g->hg;
-    std::vector<std::pair<int64_t, int32_t>> key((size_t)n_attached);
+    // relaxation vertex of every source (a pruned pendant's anchor, else itself)
+    std::vector<int32_t> rv((size_t)n_attached);
+    std::vector<int32_t> distinct;
     for (int32_t i = 0; i < n_attached; ++i) {
         const int32_t v = attached[i];
         if (v < 0 || v >= h.n) return fail(SPE_EINVAL, "attached vertex out of range");
-        const int32_t c = h.core_id[v] >= 0 ? h.core_id[v] : h.anchor_core[v];
-        key[(size_t)i] = {c, v};
+        rv[(size_t)i] = h.core_id[v] >= 0 ? h.core_id[v] : h.anchor_core[v];
+        if (rv[(size_t)i] >= 0) distinct.push_back(rv[(size_t)i]);
     }
-    std::sort(key.begin(), key.end());
-    for (int32_t i = 0; i < n_attached; ++i) order_out[i] = key[(size_t)i].second;
+    std::sort(distinct.begin(), distinct.end());
+    distinct.erase(std::unique(distinct.begin(), distinct.end()), distinct.end());
+    // Voronoi cells of ceil(A / 64) seeded-random centres over the relaxation
+    // graph (multi-source Dijkstra on the in-CSR): a 64-source block then holds
+    // sources that are close to one another, whose lanes advance in similar rounds
+    int32_t per_cell = WAVE;
+    if (getenv("SPE_ORDER_CELL")) per_cell = std::max(1, atoi(getenv("SPE_ORDER_CELL")));   // diagnostic
+    const size_t K = std::min(distinct.size(), (size_t)((n_attached + per_cell - 1) / per_cell));
+    std::vector<int32_t> cell((size_t)h.nc, INT32_MAX);
+    std::vector<double> dist((size_t)h.nc, INF);
+    if (K > 0 && !h.complete) {
+        std::vector<int32_t> c = distinct;
+        std::mt19937_64 rng(0x5eed);
+        std::shuffle(c.begin(), c.end(), rng);
+        using QE = std::pair<double, int32_t>;
+        std::priority_queue<QE, std::vector<QE>, std::greater<QE>> pq;
+        for (size_t i = 0; i < K; ++i) {
+            cell[(size_t)c[i]] = (int32_t)i;
+            dist[(size_t)c[i]] = 0.0;
+            pq.push({0.0, c[i]});
+        }
+        while (!pq.empty()) {
+            const QE e = pq.top();
+            pq.pop();
+            const int32_t x = e.second;
+            if (e.first > dist[(size_t)x]) continue;
+            for (int32_t k = h.iptr[(size_t)x]; k < h.iptr[(size_t)x + 1]; ++k) {
+                const int32_t u = h.icol[(size_t)k];
+                const double du = e.first + h.iw[(size_t)k];
+                if (du < dist[(size_t)u]) {
+                    dist[(size_t)u] = du;
+                    cell[(size_t)u] = cell[(size_t)x];
+                    pq.push({du, u});
+                }
+            }
+        }
+    }
+    struct Key {
+        int32_t cell;
+        double d;
+        int32_t r, v;
+    };
+    std::vector<Key> key((size_t)n_attached);
+    for (int32_t i = 0; i < n_attached; ++i) {
+        const int32_t r = rv[(size_t)i];
+        key[(size_t)i] = r >= 0 ? Key{cell[(size_t)r], dist[(size_t)r], r, attached[i]}
+                                : Key{INT32_MAX, INF, INT32_MAX, attached[i]};
+    }
+    std::sort(key.begin(), key.end(), [](const Key& a, const Key& b) {
+        if (a.cell != b.cell) return a.cell < b.cell;
+        if (a.d != b.d) return a.d < b.d;
+        if (a.r != b.r) return a.r < b.r;
+        return a.v < b.v;
+    });
+    for (int32_t i = 0; i < n_attached; ++i) order_out[i] = key[(size_t)i].v;
     return SPE_OK;
 }
 
