@@ -284,7 +284,9 @@ def bench_full_table(args, rank, world, local, dist):
     from shadow_amd import spe
     top, att, desc = workload(args.config)
     g = spe.Graph(top, device=local)
-    att = g.order_sources(att)   # slot numbering is the caller's: cluster sources by anchor
+    t_ord = time.perf_counter()
+    att = g.order_sources(att)   # slot numbering is the caller's: clustered sources (host side)
+    t_ord = time.perf_counter() - t_ord
     info = g.info()
     A = int(att.shape[0])
     nblk = (A + 63) // 64
@@ -345,7 +347,7 @@ def bench_full_table(args, rank, world, local, dist):
                 "value": round(t_all, 3), "unit": "s", "higher_is_better": False, "n_gpus": world,
                 "dtype": "f64", "data": "synthetic",
                 "config": {"workload": desc, "n": info["n_vertices"], "relax_vertices": info["n_relax_vertices"],
-                           "m_dir_relax": info["n_relax_entries"], "attached": A, "slot_order": "spe_order_sources",
+                           "m_dir_relax": info["n_relax_entries"], "attached": A, "slot_order": "spe_order_sources", "slot_order_ms": round(1e3 * t_ord, 1),
                            "shares": shares, "share_built": [b0, b1] if shares != world else "all",
                            "table_bytes_per_gpu": int(elems * 22)},
                 "build_s": round(t_build, 3), "sources_per_s_per_gpu": round(srcs / max(t_build, 1e-9) / (1 if shares != world else world), 1),
@@ -402,7 +404,9 @@ def main():
     from shadow_amd import spe
     top, att, desc = workload(args.config)
     g = spe.Graph(top, device=local)
-    att = g.order_sources(att)   # slot numbering is the caller's: cluster sources by anchor
+    t_ord = time.perf_counter()
+    att = g.order_sources(att)   # slot numbering is the caller's: clustered sources (host side)
+    t_ord = time.perf_counter() - t_ord
     info = g.info()
     t = spe.PathTable(g, att, groups=args.groups, engine=args.engine)
     A = t.A
@@ -492,7 +496,7 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "sources/s", "n_gpus": world, "steps": steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * el / steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": desc, "n": n, "m_dir": m_dir, "attached": A, "slot_order": "spe_order_sources",
+            "config": {"workload": desc, "n": n, "m_dir": m_dir, "attached": A, "slot_order": "spe_order_sources", "slot_order_ms": round(1e3 * t_ord, 1),
                        "sources_per_step_per_gpu": bps * 64, "groups_per_launch": args.groups or "auto",
                        "parallelism": f"source blocks sharded over {world} GPU(s), no data-path collective"},
             "full_table_time_s": round(A / value, 3),
