@@ -3,9 +3,11 @@
 
 Workload (default, config C3 of BASELINE.json / SURVEY.md §8d): synthetic
 Barabasi-Albert n=50,000, m=3, seed 3, latency U(1,100) ms, loss U(0,0.01),
-every vertex attached (A = 50,000 sources x 50,000 targets).  A step = one batch
-of `--blocks-per-step` 64-source blocks: full rows (latency, reliability, next
-hop, hops) written into the HBM-resident table.  Ranks take disjoint source
+every vertex attached (A = 50,000 sources x 50,000 targets; slots in the
+engine's clustered order, spe_order_sources).  A step = one build launch of the
+table's groups per launch (24 at C3: 1,536 sources) or `--blocks-per-step`
+64-source blocks: full rows (latency, reliability, next hop, hops) written into
+the HBM-resident table.  Ranks take disjoint source
 blocks (weak scaling: fixed rows per GPU per step, no collective on the data
 path).  Rank 0 prints one JSON line.
 
@@ -364,7 +366,8 @@ def main():
     ap.add_argument("--steps", type=int, default=0, help="0 = one full table at N=1")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3")
-    ap.add_argument("--blocks-per-step", type=int, default=16)
+    ap.add_argument("--blocks-per-step", type=int, default=0,
+                    help="64-source blocks per step; 0 = one build launch (the table's groups per launch)")
     ap.add_argument("--groups", type=int, default=0)
     ap.add_argument("--engine", type=int, default=0, help="0 auto, 1 batch (64-lane HBM state), 2 LDS-resident rows")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -411,7 +414,9 @@ def main():
     t = spe.PathTable(g, att, groups=args.groups, engine=args.engine)
     A = t.A
     nblk = t.nblocks
-    bps = max(1, args.blocks_per_step)
+    lay = t.layout()
+    bps = args.blocks_per_step if args.blocks_per_step > 0 else (
+        lay["groups_per_launch"] if lay["engine"] == spe.SPE_ENGINE_BATCH else 16)
     nwin = math.ceil(nblk / bps)
     steps = args.steps if args.steps > 0 else nwin
 
@@ -497,7 +502,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(1e3 * el / steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": desc, "n": n, "m_dir": m_dir, "attached": A, "slot_order": "spe_order_sources", "slot_order_ms": round(1e3 * t_ord, 1),
-                       "sources_per_step_per_gpu": bps * 64, "groups_per_launch": args.groups or "auto",
+                       "sources_per_step_per_gpu": bps * 64, "groups_per_launch": lay["groups_per_launch"],
                        "parallelism": f"source blocks sharded over {world} GPU(s), no data-path collective"},
             "full_table_time_s": round(A / value, 3),
             "relax_rounds_per_step": round(it_total / max(1, steps), 1),

@@ -137,6 +137,8 @@ typedef struct spe_table_layout {
     void* latrel;                   /* device pointers: double[2] {latency, reliability} */
     void* next_hop;
     void* hops;
+    int32_t groups_per_launch;      /* 64-source blocks one build launch covers */
+    int32_t engine;                 /* the engine the table runs on (SPE_ENGINE_BATCH / _LDS) */
 } spe_table_layout;
 
 typedef struct spe_entry {
