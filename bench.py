@@ -391,12 +391,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, gloo
+    # instead of RCCL (RCCL refuses two ranks on one device); never for numbers
+    rehearse = os.environ.get("SPE_BENCH_REHEARSE_ONE_GPU") == "1"
+    if rehearse:
+        local = 0
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     if args.full_table:
         bench_full_table(args, rank, world, local, dist)
