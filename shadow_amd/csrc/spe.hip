@@ -1676,6 +1676,16 @@ struct spe_table {
     int32_t* h_counts = nullptr;
     unsigned long long* d_min = nullptr;
     hipStream_t stream = nullptr;
+    // batch engine: the rows of batch i (rows_stream) overlap batch i+1's
+    // relaxation (stream) on the other state / source buffer
+    bool overlap = false;
+    State st_buf[2]{};
+    int32_t* srcv_buf[2] = {nullptr, nullptr};
+    int32_t* srcc_buf[2] = {nullptr, nullptr};
+    hipStream_t rows_stream = nullptr;
+    hipEvent_t ev_relaxed = nullptr;
+    hipEvent_t ev_rows[2] = {nullptr, nullptr};
+    bool rows_pending[2] = {false, false};
     spe_build_stats stats{};
     std::vector<void*> allocs;
     // profiling: one event pair per launch, resolved after each batch's sync
@@ -2206,9 +2216,13 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     const size_t GL = G * (WAVE / t->lanes);   // lane groups per batch
     if (!t->md.complete && t->engine == SPE_ENGINE_BATCH) {
         const size_t se = G * n * WAVE;
-        TRY(dev_alloc(t->allocs, &t->st.D, se));
-        TRY(dev_alloc(t->allocs, &t->st.P, se));
-        TRY(dev_alloc(t->allocs, &t->st.RT, se));
+        t->overlap = !getenv("SPE_NO_OVERLAP");
+        for (int i = 0; i < (t->overlap ? 2 : 1); ++i) {
+            TRY(dev_alloc(t->allocs, &t->st_buf[i].D, se));
+            TRY(dev_alloc(t->allocs, &t->st_buf[i].P, se));
+            TRY(dev_alloc(t->allocs, &t->st_buf[i].RT, se));
+        }
+        t->st = t->st_buf[0];
         const size_t nrel = std::max<size_t>(1, g->hg.icol.size());
         TRY(dev_alloc(t->allocs, &t->inflag[0], GL * nrel));
         TRY(dev_alloc(t->allocs, &t->inflag[1], GL * nrel));
@@ -2223,14 +2237,24 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         t->max_iters = 4 * n + 64;
         TRY(dev_alloc(t->allocs, &t->counts, (size_t)t->max_iters + 2));
     }
-    TRY(dev_alloc(t->allocs, &t->d_srcv, G * WAVE));
-    TRY(dev_alloc(t->allocs, &t->d_srcc, G * WAVE));
+    for (int i = 0; i < (t->overlap ? 2 : 1); ++i) {
+        TRY(dev_alloc(t->allocs, &t->srcv_buf[i], G * WAVE));
+        TRY(dev_alloc(t->allocs, &t->srcc_buf[i], G * WAVE));
+    }
+    t->d_srcv = t->srcv_buf[0];
+    t->d_srcc = t->srcc_buf[0];
     TRY(dev_alloc(t->allocs, &t->d_min, 1));
 #undef TRY
     HIP_TRY(hipHostMalloc((void**)&t->h_srcv, 2 * G * WAVE * sizeof(int32_t), hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void**)&t->h_counts, std::max<size_t>(64, (size_t)t->max_iters + 2) * sizeof(int32_t),
                           hipHostMallocDefault));
     HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+    if (t->overlap) {
+        HIP_TRY(hipStreamCreateWithFlags(&t->rows_stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&t->ev_relaxed, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&t->ev_rows[0], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&t->ev_rows[1], hipEventDisableTiming));
+    }
     *out = t;
     return SPE_OK;
 }
@@ -2261,16 +2285,23 @@ struct LaunchTimer {
     }
 };
 
-static int resolve_profile(spe_table* t) {
+// all = false: only records whose end event has completed (the rows stream may
+// still run); the pool is recycled once nothing is pending.
+static int resolve_profile(spe_table* t, bool all = true) {
+    std::vector<spe_table::Rec> keep;
     for (auto& r : t->pending) {
+        if (!all && hipEventQuery(r.b) != hipSuccess) {
+            keep.push_back(r);
+            continue;
+        }
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
         t->kp.ms[r.kind] += ms;
         t->kp.launches[r.kind] += 1;
         if (t->trace) fprintf(stderr, "spe-trace %d %.4f\n", r.kind, ms);
     }
-    t->pending.clear();
-    t->ev_next = 0;
+    t->pending.swap(keep);
+    if (t->pending.empty()) t->ev_next = 0;
     return SPE_OK;
 }
 
@@ -2396,9 +2427,18 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
     const auto t0 = std::chrono::steady_clock::now();
     const spe_graph* g = t->g;
     t->stats = spe_build_stats{};
+    const bool ovl = t->overlap && !t->md.complete && t->engine == SPE_ENGINE_BATCH;
+    hipStream_t rs = ovl ? t->rows_stream : s;
+    int buf = 0;
     for (int32_t b = block_begin; b < block_end; b += t->groups) {
         const int32_t groups = std::min(t->groups, block_end - b);
         HIP_TRY(hipStreamSynchronize(s));   // h_srcv is reused per batch
+        if (ovl) {   // this batch's buffers: free once the rows two batches back are written
+            t->st = t->st_buf[buf];
+            t->d_srcv = t->srcv_buf[buf];
+            t->d_srcc = t->srcc_buf[buf];
+            if (t->rows_pending[buf]) HIP_TRY(hipStreamWaitEvent(s, t->ev_rows[buf], 0));
+        }
         for (int32_t gi = 0; gi < groups; ++gi)
             for (int32_t l = 0; l < WAVE; ++l) {
                 const int32_t slot = (b + gi) * WAVE + l;
@@ -2448,19 +2488,39 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
         } else {
             int r = relax_to_convergence(t, groups, s);
             if (r) return r;
+            if (ovl) {
+                HIP_TRY(hipEventRecord(t->ev_relaxed, s));
+                HIP_TRY(hipStreamWaitEvent(rs, t->ev_relaxed, 0));
+            }
             {
-                LaunchTimer lt(t, s, SPE_K_ROWS);
-                launch_rows_sssp(t, row_grid, groups, sb0, s);
+                LaunchTimer lt(t, rs, SPE_K_ROWS);
+                launch_rows_sssp(t, row_grid, groups, sb0, rs);
             }
             if (t->md.prefer) {
-                LaunchTimer lt(t, s, SPE_K_DIRECT);
-                k_direct_overlay<<<(groups * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(
+                LaunchTimer lt(t, rs, SPE_K_DIRECT);
+                k_direct_overlay<<<(groups * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, rs>>>(
                     groups, sb0, t->d_srcv, t->d_vertex_slot, g->dev, t->tb);
+            }
+            if (ovl) {
+                HIP_TRY(hipEventRecord(t->ev_rows[buf], rs));
+                t->rows_pending[buf] = true;
+                buf ^= 1;
             }
         }
         HIP_TRY(hipGetLastError());
         if (t->prof) {
             HIP_TRY(hipStreamSynchronize(s));
+            int r = resolve_profile(t, !ovl);
+            if (r) return r;
+        }
+    }
+    if (ovl) {
+        HIP_TRY(hipStreamSynchronize(rs));
+        t->rows_pending[0] = t->rows_pending[1] = false;
+        t->st = t->st_buf[0];
+        t->d_srcv = t->srcv_buf[0];
+        t->d_srcc = t->srcc_buf[0];
+        if (t->prof) {
             int r = resolve_profile(t);
             if (r) return r;
         }
@@ -2816,6 +2876,10 @@ void spe_table_free(spe_table* t) {
     if (t->h_counts) (void)hipHostFree(t->h_counts);
     for (hipEvent_t e : t->ev_pool) (void)hipEventDestroy(e);
     if (t->stream) (void)hipStreamDestroy(t->stream);
+    if (t->rows_stream) (void)hipStreamDestroy(t->rows_stream);
+    if (t->ev_relaxed) (void)hipEventDestroy(t->ev_relaxed);
+    for (hipEvent_t e : t->ev_rows)
+        if (e) (void)hipEventDestroy(e);
     delete t;
 }
 
