@@ -691,6 +691,17 @@ __device__ __forceinline__ bool direct_entry(const DevGraph& G, int32_t s, int32
     return true;
 }
 
+// per-target constants of the row passes (host-built, SlotInfo[A]): one 32-B
+// uniform load per target instead of a chain of dependent graph lookups
+struct alignas(16) SlotInfo {
+    int32_t t;      // attached vertex (original id)
+    int32_t c;      // relaxation vertex the row reads: t itself or its pendant anchor
+    int32_t kt;     // full in-CSR entry of t's pendant edge, -1 if t is a relaxation vertex
+    int32_t fast;   // 1: t's vertex factor is absent or 1.0 (no path-order re-fold for it)
+    double pw;      // latency of the pendant edge (relaxation weight), 0 otherwise
+    double pa;      // 1 - p of the pendant edge (get_eid edge), 1 otherwise
+};
+
 // Path-order sum 0.0 + a_1 + a_2 + ... of the auxiliary edge attribute along the
 // row's path to core vertex c (then the pendant target edge kt, if any), as the
 // offline completion tool sums a path's jitters (compute-topology-paths.py:27-33).
@@ -735,7 +746,7 @@ __device__ double aux_fold(const DevGraph& G, const State& st, int32_t g, int32_
 template <int L>
 __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, int32_t sb0,
                                                      const int32_t* __restrict__ srcv,
-                                                     const int32_t* __restrict__ slot_vertex, DevGraph G,
+                                                     const SlotInfo* __restrict__ slots, DevGraph G,
                                                      RowMode md, State st, Table tb) {
     const int32_t lane = threadIdx.x & (WAVE - 1);
     const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
@@ -743,7 +754,8 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
     for (int64_t it = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it < items; it += nwaves) {
         const int32_t b = (int32_t)(it / tb.A);
         const int32_t jt = (int32_t)(it - (int64_t)b * tb.A);
-        const int32_t t = slot_vertex[jt];
+        const SlotInfo si = slots[jt];
+        const int32_t t = si.t;
         const int32_t g = b * (WAVE / L) + lane / L, j = lane % L;
         const int32_t s = srcv[b * WAVE + lane];
         double Lt = -1.0, R = -1.0, AX = -1.0;
@@ -756,9 +768,8 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
             } else {
                 // a pruned pendant target is one edge past its anchor: Dijkstra's
                 // d[t] = d[c] + w, parent c (its only candidate)
-                const int32_t tc = G.core_id[t];
-                const int32_t c = tc >= 0 ? tc : G.anchor_core[t];
-                const int32_t kt = tc >= 0 ? -1 : G.fiptr[t];
+                const int32_t c = si.c;
+                const int32_t kt = si.kt;
                 const size_t rt = sidx<L>(g, n, c, j);
                 const double dc = st.D[rt];
                 if (dc < INF) {
@@ -766,13 +777,12 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
                     double d = dc;
                     Route rr = rc;
                     if (kt >= 0) {
-                        d = dc + G.fiw[kt];
-                        rr.r = rc.r * G.fia[kt];
+                        d = dc + si.pw;
+                        rr.r = rc.r * si.pa;
                         rr.h = rc.h + 1;
                         rr.f = (rc.h == 0) ? t : rc.f;   // c is the source itself
                     }
-                    const double ft = G.vfac[t];
-                    const bool fast = (!has_attr(ft) || ft == 1.0) && !md.multi_rep;
+                    const bool fast = si.fast && !md.multi_rep;
                     if (fast) {
                         Lt = d;
                         R = rr.r;
@@ -781,6 +791,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
                         // the target, or multigraph get_eid latencies).  Edge i of the path
                         // (1 = leaves the source) is found by walking back from t.
                         const double fs = G.vfac[s];
+                        const double ft = G.vfac[t];
                         double l = 0.0, r = 1.0;
                         if (has_attr(fs)) r *= fs;
                         if (has_attr(ft)) r *= ft;
@@ -925,16 +936,6 @@ __host__ __device__ constexpr size_t lds_bytes(int32_t nc) {
     return lds_align((size_t)nc * 8) + lds_align((size_t)nc * 4) + lds_hs_bytes(nc) +
            2 * lds_align((size_t)((nc + 31) / 32) * 4);
 }
-
-// per-target constants of the row passes (host-built, SlotInfo[A])
-struct alignas(16) SlotInfo {
-    int32_t t;      // attached vertex (original id)
-    int32_t c;      // relaxation vertex the row reads: t itself or its pendant anchor
-    int32_t kt;     // full in-CSR entry of t's pendant edge, -1 if t is a relaxation vertex
-    int32_t pad;
-    double pw;      // latency of the pendant edge (relaxation weight), 0 otherwise
-    double pa;      // 1 - p of the pendant edge (get_eid edge), 1 otherwise
-};
 
 // per-workgroup global scratch: the parent entries, kept for pass 5's rare
 // path walks once the LDS parent array holds first hops
@@ -1655,7 +1656,7 @@ struct spe_table {
     bool built = false;
     Table tb{};
     int32_t* d_slot_vertex = nullptr;
-    SlotInfo* d_slots = nullptr;   // LDS engine: per-target constants
+    SlotInfo* d_slots = nullptr;   // row passes (both engines): per-target constants
     LdsScratch lsc{};              // LDS engine: per-workgroup parent-entry scratch
     int32_t lds_grid = 0;          // LDS engine: workgroups per launch (scratch is sized for it)
     int32_t* d_rank = nullptr;     // owner replay: position of each slot in the source-run order
@@ -2182,14 +2183,15 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     t->d_slot_vertex = const_cast<int32_t*>(tmp);
     TRY(dev_upload(t->allocs, vslot, &tmp));
     t->d_vertex_slot = const_cast<int32_t*>(tmp);
-    if (!t->md.complete && t->engine == SPE_ENGINE_LDS) {
+    if (!t->md.complete) {
         const spe::HostGraph& h = g->hg;
         std::vector<SlotInfo> si(n_attached);
         for (int32_t j = 0; j < n_attached; ++j) {
             const int32_t v = attached[j];
             SlotInfo& x = si[j];
             x.t = v;
-            x.pad = 0;
+            const double ft = h.vfac[v];
+            x.fast = (std::isnan(ft) || ft == 1.0) ? 1 : 0;
             if (h.core_id[v] >= 0) {
                 x.c = h.core_id[v];
                 x.kt = -1;
@@ -2205,6 +2207,9 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         const SlotInfo* tsi = nullptr;
         TRY(dev_upload(t->allocs, si, &tsi));
         t->d_slots = const_cast<SlotInfo*>(tsi);
+    }
+    if (!t->md.complete && t->engine == SPE_ENGINE_LDS) {
+        const spe::HostGraph& h = g->hg;
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device);
         const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, LDS_MAX_BYTES / lds_bytes(h.nc)));
@@ -2394,7 +2399,7 @@ static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
 
 static void launch_rows_sssp(spe_table* t, int grid, int32_t blocks, int32_t sb0, hipStream_t s) {
     const spe_graph* g = t->g;
-#define ROWS(LL) k_rows_sssp<LL><<<grid, BLOCK, 0, s>>>(g->hg.nc, blocks, sb0, t->d_srcv, t->d_slot_vertex, g->dev, \
+#define ROWS(LL) k_rows_sssp<LL><<<grid, BLOCK, 0, s>>>(g->hg.nc, blocks, sb0, t->d_srcv, t->d_slots, g->dev, \
                                                          t->md, t->st, t->tb)
     switch (t->lanes) {
         case 16: ROWS(16); break;
