@@ -743,7 +743,7 @@ __device__ double aux_fold(const DevGraph& G, const State& st, int32_t g, int32_
 
 // State -> table rows.  One wave per (64-source block of the batch, target
 // slot): lane l = source b*64 + l, i.e. lane group b*(64/L) + l/L, lane l%L.
-template <int L>
+template <int L, bool AUX>
 __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, int32_t sb0,
                                                      const int32_t* __restrict__ srcv,
                                                      const SlotInfo* __restrict__ slots, DevGraph G,
@@ -751,97 +751,133 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
     const int32_t lane = threadIdx.x & (WAVE - 1);
     const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
     const int64_t items = (int64_t)blocks * tb.A;
-    for (int64_t it = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it < items; it += nwaves) {
-        const int32_t b = (int32_t)(it / tb.A);
-        const int32_t jt = (int32_t)(it - (int64_t)b * tb.A);
-        const SlotInfo si = slots[jt];
-        const int32_t t = si.t;
-        const int32_t g = b * (WAVE / L) + lane / L, j = lane % L;
-        const int32_t s = srcv[b * WAVE + lane];
-        double Lt = -1.0, R = -1.0, AX = -1.0;
-        int32_t N = -1, H = 0, PV = -1;
-        if (s >= 0) {
-            if (t == s) {
-                self_entry(G, md, s, Lt, R, N, H);
-                PV = (H == 2) ? N : (H > 0 ? s : -1);
-                AX = 0.0;
-            } else {
-                // a pruned pendant target is one edge past its anchor: Dijkstra's
-                // d[t] = d[c] + w, parent c (its only candidate)
-                const int32_t c = si.c;
-                const int32_t kt = si.kt;
-                const size_t rt = sidx<L>(g, n, c, j);
-                const double dc = st.D[rt];
-                if (dc < INF) {
-                    const Route rc = st.RT[rt];
-                    double d = dc;
-                    Route rr = rc;
-                    if (kt >= 0) {
-                        d = dc + si.pw;
-                        rr.r = rc.r * si.pa;
-                        rr.h = rc.h + 1;
-                        rr.f = (rc.h == 0) ? t : rc.f;   // c is the source itself
-                    }
-                    const bool fast = si.fast && !md.multi_rep;
-                    if (fast) {
-                        Lt = d;
-                        R = rr.r;
-                    } else {
-                        // path-order re-fold, shd-topology.c:1413-1493 (rare: vertex loss on
-                        // the target, or multigraph get_eid latencies).  Edge i of the path
-                        // (1 = leaves the source) is found by walking back from t.
-                        const double fs = G.vfac[s];
-                        const double ft = G.vfac[t];
-                        double l = 0.0, r = 1.0;
-                        if (has_attr(fs)) r *= fs;
-                        if (has_attr(ft)) r *= ft;
-                        const int32_t h = rr.h;
-                        for (int32_t i = 1; i <= h; ++i) {
-                            int32_t back = h - i;   // edges to step over from the end
-                            double ew, ea;
-                            if (kt >= 0 && back == 0) {
-                                ew = G.fiwrep[kt];
-                                ea = G.fia[kt];
-                            } else {
-                                int32_t x = c;
-                                if (kt >= 0) back -= 1;
-                                for (int32_t q = 0; q < back; ++q) x = G.icol[st.P[sidx<L>(g, n, x, j)]];
-                                const int32_t k = st.P[sidx<L>(g, n, x, j)];
-                                if (k >= 0) {
-                                    ew = G.iwrep[k];
-                                    ea = G.ia[k];
-                                } else {   // -2: the pendant source's edge into its anchor
-                                    ew = G.fiwrep[G.fiptr[s]];
-                                    ea = G.fia[G.fiptr[s]];
-                                }
-                            }
-                            l += ew;
-                            r *= ea;
-                        }
-                        Lt = l;
-                        R = r;
-                    }
-                    if (Lt == 0) Lt = 1;   // shd-topology.c:1833-1837
-                    if (tb.aux) AX = aux_fold<L>(G, st, g, n, j, s, c, kt);
-                    N = rr.f;
-                    H = rr.h;
-                    if (tb.prev) {
+    // Two items per trip: every load both need (slot constants, source, the
+    // target row's distance and route) is issued before either one's stores,
+    // so a trip waits for two memory round trips, not four.
+    struct In {
+        int32_t b, jt, s;
+        SlotInfo si;
+        double dc;
+        Route rc;
+    };
+    for (int64_t it0 = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it0 < items; it0 += 2 * nwaves) {
+        In in[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int64_t it = it0 + q * nwaves;
+            In& x = in[q];
+            x.b = -1;
+            if (it < items) {
+                x.b = (int32_t)(it / tb.A);
+                x.jt = (int32_t)(it - (int64_t)x.b * tb.A);
+                x.si = slots[x.jt];
+                x.s = srcv[x.b * WAVE + lane];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            In& x = in[q];
+            x.dc = INF;
+            if (x.b >= 0 && x.s >= 0 && x.si.t != x.s) {
+                const int32_t g = x.b * (WAVE / L) + lane / L, j = lane % L;
+                const size_t rt = sidx<L>(g, n, x.si.c, j);
+                x.dc = st.D[rt];
+                x.rc = st.RT[rt];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const In& x = in[q];
+            if (x.b < 0) continue;
+            const int32_t b = x.b, jt = x.jt, s = x.s;
+            const SlotInfo& si = x.si;
+            const int32_t t = si.t;
+            const int32_t g = b * (WAVE / L) + lane / L, j = lane % L;
+            double Lt = -1.0, R = -1.0, AX = -1.0;
+            int32_t N = -1, H = 0, PV = -1;
+            if (s >= 0) {
+                if (t == s) {
+                    self_entry(G, md, s, Lt, R, N, H);
+                    PV = (H == 2) ? N : (H > 0 ? s : -1);
+                    AX = 0.0;
+                } else {
+                    // a pruned pendant target is one edge past its anchor: Dijkstra's
+                    // d[t] = d[c] + w, parent c (its only candidate)
+                    const int32_t c = si.c;
+                    const int32_t kt = si.kt;
+                    const size_t rt = sidx<L>(g, n, c, j);
+                    const double dc = x.dc;
+                    if (dc < INF) {
+                        const Route rc = x.rc;
+                        double d = dc;
+                        Route rr = rc;
                         if (kt >= 0) {
-                            PV = G.corev[c];
+                            d = dc + si.pw;
+                            rr.r = rc.r * si.pa;
+                            rr.h = rc.h + 1;
+                            rr.f = (rc.h == 0) ? t : rc.f;   // c is the source itself
+                        }
+                        const bool fast = si.fast && !md.multi_rep;
+                        if (fast) {
+                            Lt = d;
+                            R = rr.r;
                         } else {
-                            const int32_t pk = st.P[rt];
-                            PV = pk >= 0 ? G.corev[G.icol[pk]] : s;   // -2: parent is the pendant source
+                            // path-order re-fold, shd-topology.c:1413-1493 (rare: vertex loss on
+                            // the target, or multigraph get_eid latencies).  Edge i of the path
+                            // (1 = leaves the source) is found by walking back from t.
+                            const double fs = G.vfac[s];
+                            const double ft = G.vfac[t];
+                            double l = 0.0, r = 1.0;
+                            if (has_attr(fs)) r *= fs;
+                            if (has_attr(ft)) r *= ft;
+                            const int32_t h = rr.h;
+                            for (int32_t i = 1; i <= h; ++i) {
+                                int32_t back = h - i;   // edges to step over from the end
+                                double ew, ea;
+                                if (kt >= 0 && back == 0) {
+                                    ew = G.fiwrep[kt];
+                                    ea = G.fia[kt];
+                                } else {
+                                    int32_t x = c;
+                                    if (kt >= 0) back -= 1;
+                                    for (int32_t q = 0; q < back; ++q) x = G.icol[st.P[sidx<L>(g, n, x, j)]];
+                                    const int32_t k = st.P[sidx<L>(g, n, x, j)];
+                                    if (k >= 0) {
+                                        ew = G.iwrep[k];
+                                        ea = G.ia[k];
+                                    } else {   // -2: the pendant source's edge into its anchor
+                                        ew = G.fiwrep[G.fiptr[s]];
+                                        ea = G.fia[G.fiptr[s]];
+                                    }
+                                }
+                                l += ew;
+                                r *= ea;
+                            }
+                            Lt = l;
+                            R = r;
+                        }
+                        if (Lt == 0) Lt = 1;   // shd-topology.c:1833-1837
+                        if constexpr (AUX) AX = aux_fold<L>(G, st, g, n, j, s, c, kt);
+                        N = rr.f;
+                        H = rr.h;
+                        if (tb.prev) {
+                            if (kt >= 0) {
+                                PV = G.corev[c];
+                            } else {
+                                const int32_t pk = st.P[rt];
+                                PV = pk >= 0 ? G.corev[G.icol[pk]] : s;   // -2: parent is the pendant source
+                            }
                         }
                     }
                 }
             }
+            const size_t o = tidx(sb0 + b, tb.A, jt, lane);
+            tb.lr[o] = make_double2(Lt, R);
+            tb.next[o] = N;
+            tb.hops[o] = (uint16_t)(H > 65535 ? 65535 : H);
+            if (tb.prev) tb.prev[o] = PV;
+            if constexpr (AUX) tb.aux[o] = AX;
         }
-        const size_t o = tidx(sb0 + b, tb.A, jt, lane);
-        tb.lr[o] = make_double2(Lt, R);
-        tb.next[o] = N;
-        tb.hops[o] = (uint16_t)(H > 65535 ? 65535 : H);
-        if (tb.prev) tb.prev[o] = PV;
-        if (tb.aux) tb.aux[o] = AX;
     }
 }
 
@@ -2399,8 +2435,15 @@ static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
 
 static void launch_rows_sssp(spe_table* t, int grid, int32_t blocks, int32_t sb0, hipStream_t s) {
     const spe_graph* g = t->g;
-#define ROWS(LL) k_rows_sssp<LL><<<grid, BLOCK, 0, s>>>(g->hg.nc, blocks, sb0, t->d_srcv, t->d_slots, g->dev, \
-                                                         t->md, t->st, t->tb)
+#define ROWS(LL)                                                                                              \
+    do {                                                                                                      \
+        if (t->tb.aux)                                                                                        \
+            k_rows_sssp<LL, true><<<grid, BLOCK, 0, s>>>(g->hg.nc, blocks, sb0, t->d_srcv, t->d_slots, g->dev, \
+                                                         t->md, t->st, t->tb);                                \
+        else                                                                                                  \
+            k_rows_sssp<LL, false><<<grid, BLOCK, 0, s>>>(g->hg.nc, blocks, sb0, t->d_srcv, t->d_slots,       \
+                                                          g->dev, t->md, t->st, t->tb);                       \
+    } while (0)
     switch (t->lanes) {
         case 16: ROWS(16); break;
         case 32: ROWS(32); break;
