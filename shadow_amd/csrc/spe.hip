@@ -198,41 +198,55 @@ __device__ __forceinline__ double sub_get_d(double x, int32_t src) {
 
 // ----------------------------------------------------------------- kernels
 
+// One lane group per blockIdx.y; threads stride over its [n][L] block with a
+// stride that is a multiple of L, so each thread keeps one lane (one source)
+// and resolves that source's constants once.  Stores only: D, P per element,
+// the route record on the source's own (and pruned source's anchor) row.
 template <int L>
 __global__ __launch_bounds__(BLOCK) void k_init_state(int32_t n, int32_t groups, const int32_t* __restrict__ srcv,
                                                       const double* __restrict__ vfac, DevGraph G, State st) {
-    const size_t total = (size_t)groups * n * L;
-    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < total; i += (size_t)gridDim.x * BLOCK) {
-        const int32_t j = (int32_t)(i % L);
-        const size_t gv = i / L;
-        const int32_t g = (int32_t)(gv / n);
-        const int32_t v = (int32_t)(gv - (size_t)g * n);
-        const int32_t s = srcv[g * L + j];   // original id, -1 = padding lane
-        st.P[i] = -1;
-        st.D[i] = INF;
-        if (s < 0) continue;
+    static_assert(BLOCK % L == 0, "the stride must keep the lane");
+    const int32_t g = blockIdx.y;
+    const int64_t per = (int64_t)n * L;
+    const int32_t j = threadIdx.x & (L - 1);
+    const int32_t s = srcv[g * L + j];   // original id, -1 = padding lane
+    int32_t sc = -1, anc = -1, kx = -1;
+    double r0 = 1.0;
+    if (s >= 0) {
         const double fs = vfac[s];
-        const double r0 = has_attr(fs) ? 1.0 * fs : 1.0;  // (1 * (1 - p_src)), shd-topology.c:1428-1430
-        const int32_t sc = G.core_id[s];
+        r0 = has_attr(fs) ? 1.0 * fs : 1.0;  // (1 * (1 - p_src)), shd-topology.c:1428-1430
+        sc = G.core_id[s];
+        if (sc < 0) {
+            anc = G.anchor_core[s];
+            kx = G.fiptr[s];
+        }
+    }
+    const size_t base = (size_t)g * (size_t)per;
+    for (int64_t x = (int64_t)blockIdx.x * BLOCK + threadIdx.x; x < per; x += (int64_t)gridDim.x * BLOCK) {
+        const int32_t v = (int32_t)(x / L);
+        const size_t i = base + (size_t)x;
+        double d = INF;
+        int32_t p = -1;
         if (v == sc) {
-            st.D[i] = 0.0;
+            d = 0.0;
             Route rt;
             rt.r = r0;
             rt.h = 0;
             rt.f = -1;
             st.RT[i] = rt;
-        } else if (sc < 0 && v == G.anchor_core[s]) {
+        } else if (v == anc) {
             // pruned pendant source: Dijkstra's first step s -> anchor, fixed (every
             // path leaves through it); P = -2 marks "parent is the pendant source"
-            const int32_t kx = G.fiptr[s];
-            st.D[i] = 0.0 + G.fiw[kx];
-            st.P[i] = -2;
+            d = 0.0 + G.fiw[kx];
+            p = -2;
             Route rt;
             rt.r = r0 * G.fia[kx];
             rt.h = 1;
             rt.f = G.corev[v];
             st.RT[i] = rt;
         }
+        st.D[i] = d;
+        st.P[i] = p;
     }
 }
 
@@ -743,6 +757,9 @@ __device__ double aux_fold(const DevGraph& G, const State& st, int32_t g, int32_
 
 // State -> table rows.  One wave per (64-source block of the batch, target
 // slot): lane l = source b*64 + l, i.e. lane group b*(64/L) + l/L, lane l%L.
+#ifndef ROWS_ITEMS
+#define ROWS_ITEMS 2
+#endif
 template <int L, bool AUX>
 __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, int32_t sb0,
                                                      const int32_t* __restrict__ srcv,
@@ -760,10 +777,11 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
         double dc;
         Route rc;
     };
-    for (int64_t it0 = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it0 < items; it0 += 2 * nwaves) {
-        In in[2];
+    constexpr int NI = ROWS_ITEMS;
+    for (int64_t it0 = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it0 < items; it0 += NI * nwaves) {
+        In in[NI];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < NI; ++q) {
             const int64_t it = it0 + q * nwaves;
             In& x = in[q];
             x.b = -1;
@@ -775,7 +793,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
             }
         }
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < NI; ++q) {
             In& x = in[q];
             x.dc = INF;
             if (x.b >= 0 && x.s >= 0 && x.si.t != x.s) {
@@ -786,7 +804,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
             }
         }
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < NI; ++q) {
             const In& x = in[q];
             if (x.b < 0) continue;
             const int32_t b = x.b, jt = x.jt, s = x.s;
@@ -2370,8 +2388,8 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     }
     {
         LaunchTimer lt(t, s, SPE_K_INIT);
-        k_init_state<L><<<grid_for(total * L, BLOCK, 8192), BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev.vfac, g->dev,
-                                                                            t->st);
+        const dim3 ig(grid_for((int64_t)n * L, BLOCK, std::max(8, 16384 / std::max(1, (int)groups))), groups);
+        k_init_state<L><<<ig, BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev.vfac, g->dev, t->st);
     }
     {
         LaunchTimer lt(t, s, SPE_K_SEED);
