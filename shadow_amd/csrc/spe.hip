@@ -154,6 +154,8 @@ struct State {
     Route* RT;        // route record
 };
 
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+
 struct Table {
     double2* lr;      // {latency, reliability}: one 16-B record, so a lookup is one HBM line
     int32_t* next;
@@ -890,9 +892,13 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
                 }
             }
             const size_t o = tidx(sb0 + b, tb.A, jt, lane);
-            tb.lr[o] = make_double2(Lt, R);
-            tb.next[o] = N;
-            tb.hops[o] = (uint16_t)(H > 65535 ? 65535 : H);
+            // the table is written once and not read during the build: stream it
+            dvec2 e;
+            e.x = Lt;
+            e.y = R;
+            __builtin_nontemporal_store(e, reinterpret_cast<dvec2*>(tb.lr + o));
+            __builtin_nontemporal_store(N, tb.next + o);
+            __builtin_nontemporal_store((uint16_t)(H > 65535 ? 65535 : H), tb.hops + o);
             if (tb.prev) tb.prev[o] = PV;
             if constexpr (AUX) tb.aux[o] = AX;
         }
@@ -1492,7 +1498,6 @@ __global__ __launch_bounds__(BLOCK) void k_owner_replay(int32_t A, const int32_t
     }
 }
 
-typedef double dvec2 __attribute__((ext_vector_type(2)));
 
 template <int NT>
 __global__ __launch_bounds__(BLOCK) void k_lookup(const int2* __restrict__ pairs, int64_t q, int32_t blk0,
