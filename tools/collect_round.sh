@@ -2,8 +2,8 @@
 set -e
 R=${ROUND:-r01}
 O=gpurun_out/$R
-for C in c1 c1all c3 c2 c2fw c4 c4_full c5 complete; do
-  cp $O/bench_$C.log profiles/${R}_bench_$C.log
+for C in c1 c1all c3 c2 c2fw c4 c4_full c4_steps c5 complete; do
+  [ -f $O/bench_$C.log ] && cp $O/bench_$C.log profiles/${R}_bench_$C.log
   if [ -d $O/kt_$C ]; then
     f=$(find $O/kt_$C -name '*kernel_stats.csv' | head -1)
     if [ -n "$f" ]; then cp "$f" profiles/${R}_rocprof_kernel_stats_$C.csv; fi

@@ -29,6 +29,8 @@ timeout -k 10 300 python -u bench.py --config c4 --full-table --shares 8 --share
 tail -1 $O/bench_c4.log
 timeout -k 10 300 python -u bench.py --config c4 --full-table > $O/bench_c4_full.log 2>&1 || { tail -20 $O/bench_c4_full.log; exit 1; }
 tail -1 $O/bench_c4_full.log
+timeout -k 10 200 python -u bench.py --config c4 --steps 20 --warmup 2 --no-cpu-baseline > $O/bench_c4_steps.log 2>&1 || { tail -20 $O/bench_c4_steps.log; exit 1; }
+timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d $O/kt_c4 -o run --output-format csv -- python bench.py --config c4 --steps 20 --warmup 2 --no-cpu-baseline > $O/kt_c4.log 2>&1
 timeout -k 10 200 python -u bench.py --config c5 --steps 10 --warmup 2 > $O/bench_c5.log 2>&1 || { tail -20 $O/bench_c5.log; exit 1; }
 tail -1 $O/bench_c5.log
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $O/kt_c5 -o run --output-format csv -- python bench.py --config c5 --steps 4 --warmup 1 > $O/kt_c5.log 2>&1
