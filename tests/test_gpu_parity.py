@@ -247,3 +247,29 @@ def test_min_latency_ignores_padding_lanes(spe):
     ref = Oracle(top).rows(A, A)
     ok = ref["kind"] != 0
     assert t.min_latency() == ref["lat"][ok].min() > 0
+
+
+@pytest.mark.engine_fixed
+def test_multibatch_rows_overlap_matches_serial_and_oracle(spe, monkeypatch):
+    """Batch engine, 15 source blocks one group per batch: batch i's rows run on
+    the second stream while batch i+1 relaxes (two state / source buffers,
+    event-ordered reuse).  With profiling on (records of the rows stream are
+    resolved once complete) and with the overlap off (SPE_NO_OVERLAP), the
+    table must be identical to the oracle's."""
+    top = graphs.gen_random_small(900, 2600, 46)
+    A = np.arange(top.n, dtype=np.int32)
+    ora = Oracle(top).rows(A, A)
+    g = spe.Graph(top)
+    t = spe.PathTable(g, A, groups=1, engine=spe.SPE_ENGINE_BATCH)
+    t.profile(True)
+    t.build()
+    kp = t.kernel_profile()
+    out = t.download()
+    compare(out, ora, label="overlap")
+    assert kp["rows"]["launches"] == 15 and kp["relax"]["launches"] > 0
+    monkeypatch.setenv("SPE_NO_OVERLAP", "1")
+    t2 = spe.PathTable(g, A, groups=2, engine=spe.SPE_ENGINE_BATCH)
+    t2.build()
+    out2 = t2.download()
+    for k in ("lat", "rel", "next", "hops"):
+        np.testing.assert_array_equal(out2[k], out[k])
