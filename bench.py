@@ -5,7 +5,7 @@ Workload (default, config C3 of BASELINE.json / SURVEY.md §8d): synthetic
 Barabasi-Albert n=50,000, m=3, seed 3, latency U(1,100) ms, loss U(0,0.01),
 every vertex attached (A = 50,000 sources x 50,000 targets; slots in the
 engine's clustered order, spe_order_sources).  A step = one build launch of the
-table's groups per launch (24 at C3: 1,536 sources) or `--blocks-per-step`
+table's groups per launch (48 at C3: 3,072 sources) or `--blocks-per-step`
 64-source blocks: full rows (latency, reliability, next hop, hops) written into
 the HBM-resident table.  Ranks take disjoint source
 blocks (weak scaling: fixed rows per GPU per step, no collective on the data

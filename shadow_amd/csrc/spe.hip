@@ -2150,14 +2150,15 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     t->md.self_mode = o.self_mode;
     t->md.multi_rep = g->hg.multi_rep;
     t->md.directed = g->hg.directed;
-    // groups per launch: ~1.2M (group, vertex) rows per relaxation round keep every
-    // CU busy through a round's tail (measured: C3 50k -> 24, C4's 20k core -> 60:
-    // +3 % / +14 % over a fixed 16); state per group = n * 64 * 28 B, kept within 4 GB
+    // groups per launch: ~2.4M (group, vertex) rows per relaxation round keep every
+    // CU busy through a round's tail (measured: C3 50k -> 48, +12 % over a fixed 16,
+    // +2 % over 24; C4's 20k core -> 64, +2 % over 60); state per group = n * 64 * 28 B, within
+    // 6 GB (held twice: the rows of one batch overlap the next batch's relaxation)
     int32_t groups = o.groups_per_launch;
     if (groups <= 0) {
         const double per_group = (double)n * WAVE * 28.0;
-        const double want = std::round(1.2e6 / std::max(1, n));
-        groups = (int32_t)std::max(1.0, std::min({64.0, want, 4.0e9 / per_group}));
+        const double want = std::round(2.4e6 / std::max(1, n));
+        groups = (int32_t)std::max(1.0, std::min({64.0, want, 6.0e9 / per_group}));
     }
     t->groups = std::max(1, std::min(groups, std::max(1, t->blk1 - t->blk0)));
     // sources per lane group (shared frontier); 64/L groups per 64-source block
