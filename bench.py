@@ -4,12 +4,13 @@
 Workload (default, config C3 of BASELINE.json / SURVEY.md §8d): synthetic
 Barabasi-Albert n=50,000, m=3, seed 3, latency U(1,100) ms, loss U(0,0.01),
 every vertex attached (A = 50,000 sources x 50,000 targets; slots in the
-engine's clustered order, spe_order_sources).  A step = one build launch of the
-table's groups per launch (48 at C3: 3,072 sources) or `--blocks-per-step`
-64-source blocks: full rows (latency, reliability, next hop, hops) written into
-the HBM-resident table.  Ranks take disjoint source
-blocks (weak scaling: fixed rows per GPU per step, no collective on the data
-path).  Rank 0 prints one JSON line.
+engine's clustered order, spe_order_sources).  A step = one WHOLE path table:
+every source row (latency, reliability, next hop, hops) written into the
+HBM-resident table.  With N GPUs (one rank each) the sources are dealt
+round-robin in chunks of one build launch and the latency/reliability records
+of every chunk are all-gathered over RCCL, overlapped with the next chunk's
+build, so each step ends with the whole table replicated on every GPU (strong
+scaling: fixed work per step).  Rank 0 prints one JSON line.
 
 Run: python bench.py [--gpus N --steps K --warmup W]
      torchrun --nproc-per-node N bench.py --gpus N ...
@@ -18,7 +19,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import platform
 import subprocess
@@ -72,20 +72,25 @@ def workload(name: str):
 
 
 def cpu_baseline(top, att, seconds: float, seed: int = 6):
-    """Oracle (C restatement of igraph Dijkstra + Shadow row rules, -O2, 1 core)
-    timed on a bounded sample of this workload's sources."""
+    """Oracle (C restatement of igraph Dijkstra + Shadow row rules, -O2) timed on a
+    bounded sample of this workload's sources: 1 core (the reference serialises
+    its Dijkstra runs under graphLock, shd-topology.c:1732-1766), then all cores
+    (OpenMP over sources: a bound the reference cannot reach).  Sources are drawn
+    in a seeded random order, cycling when the sample outlasts A (C1)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Oracle
     o = Oracle(top)
-    rng = np.random.default_rng(seed)
-    order = rng.permutation(att.shape[0])
+    A = att.shape[0]
+    order = np.random.default_rng(seed).permutation(A)
+
+    def take(start, k):
+        return att[order[np.arange(start, start + k) % A]]
+
     done, t0, dj = 0, time.perf_counter(), 0.0
-    chunk = 8
-    while time.perf_counter() - t0 < seconds and done < att.shape[0]:
-        src = att[order[done:done + chunk]]
-        r = o.rows(src, att, nthreads=1, want_dijkstra_time=True)
+    while time.perf_counter() - t0 < seconds:
+        r = o.rows(take(done, 8), att, nthreads=1, want_dijkstra_time=True)
         dj += r["dijkstra_seconds"]
-        done += src.shape[0]
+        done += 8
     el = time.perf_counter() - t0
     model = ""
     try:
@@ -95,20 +100,19 @@ def cpu_baseline(top, att, seconds: float, seed: int = 6):
                 break
     except OSError:
         pass
-    # BASELINE.md's "optimistic, all cores" (OpenMP over sources; the reference
-    # serialises Dijkstra under graphLock, so this is a bound it cannot reach)
     nt = min(16, os.cpu_count() or 1)
     done_all, t1 = 0, time.perf_counter()
-    while time.perf_counter() - t1 < seconds / 4 and done + done_all < att.shape[0]:
-        src = att[order[done + done_all:done + done_all + 8 * nt]]
-        o.rows(src, att, nthreads=nt)
-        done_all += src.shape[0]
+    while time.perf_counter() - t1 < seconds / 4:
+        o.rows(take(done + done_all, 8 * nt), att, nthreads=nt)
+        done_all += 8 * nt
     el_all = time.perf_counter() - t1
-    return {"value": done / el, "unit": "sources/s", "cores": 1, "kind": "port",
-            "sample": f"{done} seeded-random sources (seed {seed}) x {att.shape[0]} targets, full row build, "
-                      f"{el:.1f} s; Dijkstra-only {done / max(dj, 1e-9):.1f} sources/s",
-            "optimistic_all_cores": {"value": round(done_all / max(el_all, 1e-9), 1), "threads": nt,
-                                     "sample": f"{done_all} further sources"},
+    dij = (f"Dijkstra-only {done / dj:.1f} sources/s" if dj > 0
+           else "no Dijkstra runs: every pair is DIRECT (complete graph, shd-topology.c:2002-2008)")
+    return {"value": round(done / el, 1), "unit": "sources/s", "cores": 1, "kind": "port",
+            "sample": f"{done} seeded-random source rows (seed {seed}, cycling over A = {A}) x {A} targets, full "
+                      f"row build, {el:.1f} s; {dij}",
+            "optimistic_all_cores": {"value": round(done_all / el_all, 1), "threads": nt,
+                                     "sample": f"{done_all} source rows, {el_all:.1f} s"},
             "cpu_model": model, "host_nproc": os.cpu_count()}
 
 
@@ -276,12 +280,36 @@ def bench_fw(args):
     print(json.dumps(line), flush=True)
 
 
-def bench_full_table(args, rank, world, local, dist):
-    """Whole path-table precompute (BASELINE north star: C4 on 8 GPUs in < 10 s).
-    Rank r owns the contiguous source-block range r of `shares` (= world, or more to
-    emulate one rank of a larger job on fewer GPUs); with --gather and world > 1 the
-    latency/reliability records are then all-gathered over RCCL into a full
-    replicated table on every GPU (one contiguous SB64 span per rank)."""
+def relax_bytes(info, A, lds: bool, direct: bool):
+    """SURVEY §8d algorithmic bytes per source, priced on the graph the engine
+    relaxes (pendants pruned: n_relax_vertices / n_relax_entries) -- the relaxation
+    stage B_relax = 12 m + 28 n + 8, the row stage 22 A; the LDS engine's one
+    fused kernel does both; a DIRECT (complete) row is 38 B per pair."""
+    n, m = info["n_relax_vertices"], info["n_relax_entries"]
+    b_relax = 12.0 * m + 28.0 * n + 8.0
+    b_rows = 22.0 * A
+    if lds:
+        b_relax += b_rows
+    if direct:
+        b_relax = 38.0 * A
+    return b_relax, b_rows
+
+
+def auto_groups(info) -> int:
+    """spe_table_create's default groups per launch (spe.hip): ~2.4M (group,
+    vertex) rows per relaxation round, capped at 64 groups and 6 GB of state."""
+    n = max(1, info["n_relax_vertices"])
+    return int(max(1.0, min(64.0, round(2.4e6 / n), 6.0e9 / (n * 64 * 28.0))))
+
+
+def bench_table(args, rank, world, local, dist):
+    """The default measurement: a step is one WHOLE path table (every source
+    row) of the config -- BASELINE's "full path-table time".  At N > 1 (one rank
+    per GPU, torchrun) the source blocks are dealt round-robin in chunks of one
+    build launch, and every chunk's {latency, reliability} records are
+    all-gathered over RCCL into the replicated table on every GPU, overlapped with
+    the next chunk's build; the step ends when every rank holds the whole table
+    (strong scaling: the total work per step is fixed)."""
     import torch
     from shadow_amd import spe
     top, att, desc = workload(args.config)
@@ -292,94 +320,163 @@ def bench_full_table(args, rank, world, local, dist):
     info = g.info()
     A = int(att.shape[0])
     nblk = (A + 63) // 64
-    shares = max(world, args.shares)
-    share = rank if shares == world else args.share_index
-    cb = (nblk + shares - 1) // shares
-    b0, b1 = min(nblk, share * cb), min(nblk, (share + 1) * cb)
-    elems = cb * A * 64
     dev = torch.device("cuda", local)
-    bufs = [torch.empty((elems, 2), dtype=torch.float64, device=dev),   # {latency, reliability}
-            torch.empty(elems, dtype=torch.int32, device=dev), torch.empty(elems, dtype=torch.int16, device=dev)]
-    t = None
-    if b1 > b0:   # (a rank past the last block owns nothing but still joins the gather)
-        t = spe.PathTable(g, att, blocks=(b0, b1), ext=[b.data_ptr() for b in bufs], groups=args.groups)
-    if t is not None:   # warm-up: one batch (kernel code objects, first-touch of the state)
-        t.build_blocks(b0, min(b1, b0 + 1))
+    # the engine's groups per launch (auto rule: ~2.4M (group, vertex) rows per
+    # round) bounds the chunk: one chunk = one build launch
+    probe = spe.PathTable(g, att[:64], engine=args.engine)   # the engine AUTO picks for this graph
+    lds_engine = probe.layout()["engine"] == spe.SPE_ENGINE_LDS
+    probe.close()
+    # one chunk = one build launch: the LDS engine covers every block in one launch,
+    # the batch engine `groups` blocks (auto rule: ~2.4M (group, vertex) rows per round)
+    gpl = nblk if lds_engine else (args.groups if args.groups > 0 else auto_groups(info))
+    from shadow_amd import dist as sd
+    shares = max(world, args.shares)
+    emulated = shares != world   # one rank of a `shares`-GPU job: its chunks only, no gather
+    rounds, G = sd.chunk_plan(nblk, shares, gpl)
+    mine = sd.rank_chunks(nblk, shares, args.share_index if emulated else rank, rounds, G)
+    padded = rounds * shares * G
+    elems = padded * A * 64
+    gather = world > 1 and not args.no_gather
+    # the table in caller-owned HBM (spe_table_opts.ext_*): every rank holds the
+    # whole record span (its own chunks built in place, the others' gathered in)
+    lr = torch.empty((elems, 2), dtype=torch.float64, device=dev)
+    nx = torch.empty(elems, dtype=torch.int32, device=dev)
+    hp = torch.empty(elems, dtype=torch.int16, device=dev)
+    t = spe.PathTable(g, att, blocks=(0, nblk), ext=[lr.data_ptr(), nx.data_ptr(), hp.data_ptr()], groups=G,
+                      engine=args.engine)
+    chunk_elems = G * A * 64
+
+    def one_table():
+        works, tb, tg, its = [], 0.0, 0.0, 0
+        for k, c, b0, b1 in mine:
+            t0 = time.perf_counter()
+            if b1 > b0:
+                its += t.build_blocks(b0, b1)["iterations"]
+            tb += time.perf_counter() - t0
+            if gather:   # overlaps the next round's build (RCCL runs on its own stream)
+                w = sd.allgather_round(lr, k, world, rank, chunk_elems, dist, async_op=True)
+                if w is not None:
+                    works.append(w)
+        t1 = time.perf_counter()
+        for w in works:
+            w.wait()
+        torch.cuda.synchronize(dev)
+        tg += time.perf_counter() - t1
+        return tb, tg, its
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        one_table()
+    if not args.no_profile:
+        t.profile(True)
+    steps = args.steps if args.steps > 0 else 3
     torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
+    barrier()
     t0 = time.perf_counter()
-    if t is not None:
-        t.build()
+    tb_sum = tg_sum = 0.0
+    it_total = 0
+    for _ in range(steps):
+        tb, tg, its = one_table()
+        tb_sum += tb
+        tg_sum += tg
+        it_total += its
     torch.cuda.synchronize(dev)
-    t_build = time.perf_counter() - t0
-    if dist is not None:
-        dist.barrier()
-    t_all = time.perf_counter() - t0
-    gather = None
-    if args.gather and dist is not None:
-        full_lr = torch.empty((world * elems, 2), dtype=torch.float64, device=dev)
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        tg = time.perf_counter()
-        dist.all_gather_into_tensor(full_lr, bufs[0])
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        t_gather = time.perf_counter() - tg
-        t_all = time.perf_counter() - t0
-        gather = {"bytes_per_gpu_received": int(2 * (world - 1) * elems * 8), "seconds": round(t_gather, 3),
-                  "GBps_per_gpu": round(2 * (world - 1) * elems * 8 / t_gather / 1e9, 1)}
-    x = torch.tensor([t_build, t_all], dtype=torch.float64, device=dev)
+    barrier()
+    el = time.perf_counter() - t0
+    kp = t.kernel_profile() if not args.no_profile else None
+    x = torch.tensor([el, tb_sum, tg_sum], dtype=torch.float64, device=dev)
     if dist is not None:
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
-    t_build, t_all = float(x[0]), float(x[1])
+    el, tb_sum, tg_sum = (float(v) for v in x.tolist())
+    built = sum(min(A, b1 * 64) - b0 * 64 for _, _, b0, b1 in mine if b1 > b0)
+    total = built if emulated else A
+    value = total * steps / el
+    lds = kp is not None and kp["lds"]["launches"] > 0
+    direct = kp is not None and kp["direct"]["launches"] > 0 and kp["relax"]["launches"] == 0 and not lds
+    b_relax, b_rows = relax_bytes(info, A, lds, direct)
+    roof, extra = None, {}
+    if kp is not None:
+        kname = "k_sssp_lds" if lds else ("k_rows_direct" if direct else "k_relax")
+        rl = kp["lds" if lds else ("direct" if direct else "relax")]
+        relax_s = rl["ms"] / 1e3
+        done = built * steps   # this rank's sources (the profile is this rank's launches)
+        ach = b_relax * done / relax_s / 1e9 if relax_s > 0 else 0.0
+        roof = {"bound": "hbm", "kernel": kname + (" (SSSP + rows, LDS-resident state)" if lds else
+                                                   (" (DIRECT rows)" if direct else " (SSSP stage)")),
+                "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": pmc_traffic(args, kname), "launches": rl["launches"],
+                "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
+                "algorithmic_bytes_per_source": b_relax,
+                "bytes_basis": "relaxation graph: 12 m_relax + 28 n_relax + 8 (SURVEY 8d B_s minus the row stage)"}
+        rw = kp["rows"]
+        rows_s = rw["ms"] / 1e3
+        extra["roofline_rows"] = {"kernel": "k_rows_sssp", "achieved": round(b_rows * done / rows_s / 1e9, 1)
+                                  if rows_s > 0 else 0.0, "unit": "GB/s", "launches": rw["launches"],
+                                  "launch_avg_us": round(1e3 * rw["ms"] / max(1, rw["launches"]), 2),
+                                  "algorithmic_bytes_per_source": b_rows}
+        extra["kernel_ms"] = {k: round(v["ms"], 3) for k, v in kp.items()}
+        extra["kernel_launches"] = {k: v["launches"] for k, v in kp.items()}
+        extra["engine"] = "lds" if lds else ("direct" if direct else "batch")
+        # the whole build against the full-graph SURVEY bytes (what BASELINE's B_s prices)
+        m_full = int(np.count_nonzero(top.esrc != top.edst)) * (1 if top.directed else 2)
+        b_full = 12.0 * m_full + 28.0 * top.n + 22.0 * A + 8.0
+        extra["roofline_full_graph_pricing"] = {
+            "achieved": round(b_full * built / (tb_sum / steps) / 1e9, 1), "unit": "GB/s",
+            "frac": round(b_full * built / (tb_sum / steps) / 1e9 / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes_per_source": b_full,
+            "note": "SURVEY 8d B_s = 12 m_dir + 28 n + 22 A + 8 over the FULL graph, per GPU build time; the "
+                    "engine relaxes the pruned graph, so this overstates the kernel's achieved bandwidth"}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not emulated:
+        cpu = cpu_baseline(top, att, args.cpu_seconds)
     if rank == 0:
-        srcs = min(A, b1 * 64) - b0 * 64 if shares != world else A
-        # SURVEY §8d per-source algorithmic bytes on the FULL graph (the reference's
-        # Dijkstra scans every vertex and edge; pendant pruning is this engine's saving)
-        m_dir_full = int(np.count_nonzero(top.esrc != top.edst)) * (1 if top.directed else 2)
-        b_s = 12.0 * m_dir_full + 28.0 * top.n + 22.0 * A + 8.0
-        per_gpu_s = t_build
-        ach = b_s * srcs / (1 if shares != world else world) / max(per_gpu_s, 1e-9) / 1e9
-        roof_full = {"bound": "hbm", "kernel": "whole build (relax + rows), per GPU", "achieved": round(ach, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                     "algorithmic_bytes_per_source": b_s, "traffic": None,
-                     "note": "SURVEY 8d B_s = 12 m_dir + 28 n + 22 A + 8 over the full graph"}
-        line = {"metric": "full path-table precompute time (north star: C4 on 8 GPUs < 10 s)",
-                "value": round(t_all, 3), "unit": "s", "higher_is_better": False, "n_gpus": world,
-                "dtype": "f64", "data": "synthetic",
-                "config": {"workload": desc, "n": info["n_vertices"], "relax_vertices": info["n_relax_vertices"],
-                           "m_dir_relax": info["n_relax_entries"], "attached": A, "slot_order": "spe_order_sources", "slot_order_ms": round(1e3 * t_ord, 1),
-                           "shares": shares, "share_built": [b0, b1] if shares != world else "all",
-                           "table_bytes_per_gpu": int(elems * 22)},
-                "build_s": round(t_build, 3), "sources_per_s_per_gpu": round(srcs / max(t_build, 1e-9) / (1 if shares != world else world), 1),
-                "roofline": roof_full,
-                "gather": gather,
-                "note": ("emulated: this run built ONE share of a %d-way split (weak-scaling equivalent of one rank); "
-                         "no all-gather measured" % shares) if shares != world else None}
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "sources/s", "n_gpus": world, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * el / steps, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": desc, "n": info["n_vertices"], "n_relax": info["n_relax_vertices"],
+                       "m_relax": info["n_relax_entries"], "attached": A, "slot_order": "spe_order_sources",
+                       "slot_order_ms": round(1e3 * t_ord, 1),
+                       "step": "one whole path table (every source row)" + (
+                           f"; emulated share {args.share_index} of {shares} (no gather)" if emulated else ""),
+                       "chunk_blocks": G, "rounds": rounds,
+                       "parallelism": (f"source chunks round-robin over {world} GPUs, RCCL all-gather of the "
+                                       f"latency/reliability records overlapped with the next chunk's build"
+                                       if gather else f"{world} GPU(s), no collective")},
+            "full_table_time_s": round(el / steps, 4) if not emulated else None,
+            "build_s_per_step": round(tb_sum / steps, 4),
+            "gather_wait_s_per_step": round(tg_sum / steps, 4) if gather else None,
+            "gather_bytes_per_gpu_per_step": int((world - 1) * rounds * chunk_elems * 16) if gather else None,
+            "relax_rounds_per_step": round(it_total / max(1, steps), 1),
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        line.update(extra)
+        if cpu:
+            line["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)
         print(json.dumps(line), flush=True)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=0, help="0 = one full table at N=1")
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=0, help="whole tables timed (0 = 3)")
+    ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3")
-    ap.add_argument("--blocks-per-step", type=int, default=0,
-                    help="64-source blocks per step; 0 = one build launch (the table's groups per launch)")
-    ap.add_argument("--groups", type=int, default=0)
+    ap.add_argument("--groups", type=int, default=0, help="64-source blocks per build launch (0 = auto)")
     ap.add_argument("--engine", type=int, default=0, help="0 auto, 1 batch (64-lane HBM state), 2 LDS-resident rows")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
+    ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the all-gather (build only)")
     ap.add_argument("--queries", type=int, default=100_000_000, help="c5: lookups per step")
     ap.add_argument("--pois", type=int, default=10000, help="complete: POIs")
     ap.add_argument("--pmc-json", default=None, help="per-dispatch HBM bytes from tools/pmc_to_json.py")
-    ap.add_argument("--full-table", action="store_true", help="time one whole path-table precompute")
-    ap.add_argument("--gather", action="store_true", help="--full-table: RCCL all-gather of latency/reliability")
-    ap.add_argument("--shares", type=int, default=1, help="--full-table: split into this many source shares")
-    ap.add_argument("--share-index", type=int, default=0, help="--full-table: the share this run builds")
+    ap.add_argument("--full-table", action="store_true", help="(the default; kept for old command lines)")
+    ap.add_argument("--shares", type=int, default=1, help="emulate one rank of a job with this many GPUs")
+    ap.add_argument("--share-index", type=int, default=0, help="--shares: the rank whose chunks this run builds")
     args = ap.parse_args()
     if args.config == "c5":
         return bench_lookup(args)
@@ -405,122 +502,7 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    if args.full_table:
-        bench_full_table(args, rank, world, local, dist)
-        if dist is not None:
-            dist.destroy_process_group()
-        return
-
-    from shadow_amd import spe
-    top, att, desc = workload(args.config)
-    g = spe.Graph(top, device=local)
-    t_ord = time.perf_counter()
-    att = g.order_sources(att)   # slot numbering is the caller's: clustered sources (host side)
-    t_ord = time.perf_counter() - t_ord
-    info = g.info()
-    t = spe.PathTable(g, att, groups=args.groups, engine=args.engine)
-    A = t.A
-    nblk = t.nblocks
-    lay = t.layout()
-    bps = args.blocks_per_step if args.blocks_per_step > 0 else (
-        lay["groups_per_launch"] if lay["engine"] == spe.SPE_ENGINE_BATCH else 16)
-    nwin = math.ceil(nblk / bps)
-    steps = args.steps if args.steps > 0 else nwin
-
-    def window(k: int):
-        w = (k * world + rank) % nwin
-        return w * bps, min(nblk, (w + 1) * bps)
-
-    def sources_in(b0, b1):
-        return min(A, b1 * 64) - b0 * 64
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    for k in range(args.warmup):
-        t.build_blocks(*window(k))
-    if not args.no_profile:
-        t.profile(True)
-    it_total, fr_total, done = 0, 0, 0
-    barrier()
-    t0 = time.perf_counter()
-    for k in range(steps):
-        b0, b1 = window(args.warmup + k)
-        st = t.build_blocks(b0, b1)
-        it_total += st["iterations"]
-        fr_total += st["active_rounds"]
-        done += sources_in(b0, b1)
-    barrier()
-    el = time.perf_counter() - t0
-    kp = t.kernel_profile() if not args.no_profile else None
-
-    total_sources = done
-    if dist is not None:
-        import torch
-        x = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(x, op=dist.ReduceOp.MAX)
-        el = float(x.item())
-        y = torch.tensor([done], dtype=torch.float64, device="cuda")
-        dist.all_reduce(y)
-        total_sources = int(y.item())
-
-    value = total_sources / el
-    n, m_dir = info["n_vertices"], info["n_relax_entries"]
-    # SURVEY §8d per-source algorithmic bytes, split by stage
-    b_relax = 12.0 * m_dir + 28.0 * n + 8.0
-    b_rows = 22.0 * A
-    roof = None
-    extra = {}
-    lds = kp is not None and kp["lds"]["launches"] > 0
-    direct = kp is not None and kp["direct"]["launches"] > 0 and kp["relax"]["launches"] == 0 and not lds
-    if lds:   # one fused kernel: relaxation in LDS + row writes
-        b_relax += b_rows
-    if direct:   # complete graph: every row is DIRECT, 38 B per pair
-        b_relax = 38.0 * A
-    if kp is not None:
-        kname = "k_sssp_lds" if lds else ("k_rows_direct" if direct else "k_relax")
-        rl = kp["lds" if lds else ("direct" if direct else "relax")]
-        relax_s = rl["ms"] / 1e3
-        ach = b_relax * done / relax_s / 1e9 if relax_s > 0 else 0.0
-        traffic = pmc_traffic(args, kname)
-        roof = {"bound": "hbm", "kernel": kname + (" (SSSP + rows, LDS-resident state)" if lds else
-                                                   (" (DIRECT rows)" if direct else " (SSSP stage)")),
-                "achieved": round(ach, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "launches": rl["launches"], "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
-                "algorithmic_bytes_per_source": b_relax}
-        rw = kp["rows"]
-        rows_s = rw["ms"] / 1e3
-        extra["roofline_rows"] = {"kernel": "k_rows_sssp", "achieved": round(b_rows * done / rows_s / 1e9, 1)
-                                  if rows_s > 0 else 0.0, "unit": "GB/s", "launches": rw["launches"],
-                                  "launch_avg_us": round(1e3 * rw["ms"] / max(1, rw["launches"]), 2),
-                                  "algorithmic_bytes_per_source": b_rows}
-        extra["kernel_ms"] = {k: round(v["ms"], 3) for k, v in kp.items()}
-        extra["kernel_launches"] = {k: v["launches"] for k, v in kp.items()}
-        extra["pipeline_frac_of_hbm"] = round((b_relax + (0 if lds else b_rows)) * value / 1e9 / HBM_PEAK_GBS, 4)
-        extra["engine"] = "lds" if lds else ("direct" if direct else "batch")
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(top, att, args.cpu_seconds)
-    if rank == 0:
-        line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "sources/s", "n_gpus": world, "steps": steps,
-            "warmup": args.warmup, "ms_per_step": round(1e3 * el / steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": desc, "n": n, "m_dir": m_dir, "attached": A, "slot_order": "spe_order_sources", "slot_order_ms": round(1e3 * t_ord, 1),
-                       "sources_per_step_per_gpu": bps * 64, "groups_per_launch": lay["groups_per_launch"],
-                       "parallelism": f"source blocks sharded over {world} GPU(s), no data-path collective"},
-            "full_table_time_s": round(A / value, 3),
-            "relax_rounds_per_step": round(it_total / max(1, steps), 1),
-            "active_rounds_per_step": round(fr_total / max(1, steps), 1),
-            "roofline": roof, "cpu_baseline": cpu,
-        }
-        line.update(extra)
-        if cpu:
-            line["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)
-        print(json.dumps(line), flush=True)
+    bench_table(args, rank, world, local, dist)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -10,9 +10,13 @@
  *   master:  topology_free                               shd-master.c:100
  * Here the three per-packet calls are topology_getPathInfo (one table read);
  * every 64th packet is re-asked through the three separate getters, which must
- * agree bit for bit.
+ * agree bit for bit.  With late_hosts > 0 the main thread attaches that many
+ * more hosts AFTER the table is sealed while the workers are querying (a
+ * replacement table is built and swapped in under them), and the workers also
+ * address the late hosts once attached.  At the end the packet counters of
+ * every cached path must add up to the number of counted packets exactly.
  *
- *   shd_topology_demo <graph.graphml> <hosts> <packets> [threads] [seed]
+ *   shd_topology_demo <graph.graphml> <hosts> <packets> [threads] [seed] [late_hosts]
  * prints one JSON line; exit 0 ok, 1 disagreement, 2 setup failure. */
 #include <arpa/inet.h>
 #include <pthread.h>
@@ -37,10 +41,10 @@ static spe_in_addr_t host_addr(int32_t i) { return htonl((11u << 24) | (uint32_t
 
 typedef struct {
     Topology* top;
-    int32_t hosts;
+    int32_t hosts;         /* hosts addressed: the first ones plus the late ones */
     int64_t packets;
     unsigned seed;
-    int64_t routable, mismatches;
+    int64_t routable, mismatches, skipped;
     double latency_sum;
 } Worker;
 
@@ -49,6 +53,10 @@ static void* worker_run(void* arg) {
     for (int64_t p = 0; p < w->packets; ++p) {
         const spe_in_addr_t s = host_addr(rand_r(&w->seed) % w->hosts);
         const spe_in_addr_t d = host_addr(rand_r(&w->seed) % w->hosts);
+        if (topology_attached_vertex(w->top, s) < 0 || topology_attached_vertex(w->top, d) < 0) {
+            ++w->skipped;   /* a late host not attached yet */
+            continue;
+        }
         double lat = 0.0, rel = 0.0;
         const int32_t ok = topology_getPathInfo(w->top, s, d, &lat, &rel);
         if (ok) {
@@ -68,14 +76,15 @@ static void* worker_run(void* arg) {
 
 int main(int argc, char** argv) {
     if (argc < 4) {
-        fprintf(stderr, "usage: %s <graph.graphml> <hosts> <packets> [threads] [seed]\n", argv[0]);
+        fprintf(stderr, "usage: %s <graph.graphml> <hosts> <packets> [threads] [seed] [late_hosts]\n", argv[0]);
         return 2;
     }
     const int32_t hosts = atoi(argv[2]);
     const int64_t packets = atoll(argv[3]);
     const int32_t threads = argc > 4 ? atoi(argv[4]) : 4;
     unsigned seed = argc > 5 ? (unsigned)atoi(argv[5]) : 1u;
-    if (hosts < 1 || packets < 0 || threads < 1) return 2;
+    const int32_t late = argc > 6 ? atoi(argv[6]) : 0;
+    if (hosts < 1 || packets < 0 || threads < 1 || late < 0) return 2;
 
     const double t0 = now_s();
     Topology* top = topology_new(argv[1]);
@@ -113,32 +122,53 @@ int main(int argc, char** argv) {
     pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
     for (int32_t k = 0; k < threads; ++k) {
         ws[k].top = top;
-        ws[k].hosts = hosts;
+        ws[k].hosts = hosts + late;
         ws[k].packets = packets / threads + (k < packets % threads ? 1 : 0);
         ws[k].seed = seed + 7919u * (unsigned)(k + 1);
         pthread_create(&th[k], NULL, worker_run, &ws[k]);
     }
-    int64_t routable = 0, mismatches = 0;
+    for (int32_t i = 0; i < late; ++i) {   /* attach after seal, under concurrent readers */
+        uint64_t bw_down = 0, bw_up = 0;
+        topology_attach(top, host_addr(hosts + i), next_double, &seed, NULL, NULL, NULL, NULL, NULL, &bw_down,
+                        &bw_up);
+    }
+    int64_t routable = 0, mismatches = 0, skipped = 0;
     double latency_sum = 0.0;
     for (int32_t k = 0; k < threads; ++k) {
         pthread_join(th[k], NULL);
         routable += ws[k].routable;
         mismatches += ws[k].mismatches;
+        skipped += ws[k].skipped;
         latency_sum += ws[k].latency_sum;
     }
     const double t4 = now_s();
+    /* every counted packet sits on exactly one cached path: one per unordered
+     * vertex pair (undirected graphs), asked through one representative host each */
+    const int32_t nh = hosts + late, nv = topology_vertex_count(top);
+    int32_t* rep = (int32_t*)malloc((size_t)nv * sizeof(int32_t));
+    for (int32_t v = 0; v < nv; ++v) rep[v] = -1;
+    for (int32_t i = 0; i < nh; ++i) {
+        const int32_t v = topology_attached_vertex(top, host_addr(i));
+        if (v >= 0 && rep[v] < 0) rep[v] = i;
+    }
+    uint64_t counted = 0;
+    for (int32_t a = 0; a < nv; ++a)
+        for (int32_t b = a; b < nv && rep[a] >= 0; ++b)
+            if (rep[b] >= 0) counted += topology_path_packet_count(top, host_addr(rep[a]), host_addr(rep[b]));
+    free(rep);
     /* the counters are per (src, dst) pair and atomic: re-count one pair */
     const uint64_t c00 = topology_path_packet_count(top, host_addr(0), host_addr(0));
     const double min_lat = topology_min_path_latency(top);
     printf("{\"graph\": \"%s\", \"vertices\": %d, \"hosts\": %d, \"attached_vertices\": %d, "
            "\"load_s\": %.4f, \"attach_s\": %.4f, \"seal_s\": %.4f, \"packets\": %lld, \"threads\": %d, "
            "\"packets_per_s\": %.1f, \"routable\": %lld, \"latency_sum\": %.6f, \"min_path_latency\": %.6f, "
-           "\"count_pair_0_0\": %llu, \"mismatches\": %lld}\n",
+           "\"count_pair_0_0\": %llu, \"late_hosts\": %d, \"skipped\": %lld, \"counted\": %llu, "
+           "\"mismatches\": %lld}\n",
            argv[1], topology_vertex_count(top), hosts, distinct, t1 - t0, t2 - t1, t3 - t2, (long long)packets,
            threads, packets > 0 ? (double)packets / (t4 - t3) : 0.0, (long long)routable, latency_sum, min_lat,
-           (unsigned long long)c00, (long long)mismatches);
+           (unsigned long long)c00, late, (long long)skipped, (unsigned long long)counted, (long long)mismatches);
     free(th);
     free(ws);
     topology_free(top);
-    return mismatches == 0 ? 0 : 1;
+    return (mismatches == 0 && counted == (uint64_t)routable) ? 0 : 1;
 }

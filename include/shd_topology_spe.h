@@ -42,9 +42,13 @@ typedef void (*topology_min_latency_fn)(double min_latency_ms, void* ctx);
 typedef void (*topology_log_fn)(int level, const char* text, void* ctx);
 
 /* GraphML file -> validated topology on `device`; NULL on any validation
- * failure (shd-topology.c:2485-2490).  The file is read synchronously. */
+ * failure (shd-topology.c:2485-2490).  The file is read synchronously.
+ * topology_new builds on device SHADOW_SPE_DEVICE (default 0). */
 Topology* topology_new(const char* graphPath);
 Topology* topology_new_on_device(const char* graphPath, int32_t device);
+/* The ingest and validation of topology_new alone (no device work): 1 when the
+ * reference would accept the file, else 0. */
+int32_t topology_check_graphml(const char* graphPath);
 void topology_free(Topology* top);
 
 /* Hint-matched attachment (shd-topology.c:2077-2413).  Hints may be NULL. */
@@ -64,16 +68,48 @@ void topology_incrementPathPacketCounter(Topology* top, spe_in_addr_t srcAddress
 int32_t topology_getPathInfo(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress, double* latency,
                              double* reliability);
 
-/* engine hooks */
+/* engine hooks (callbacks run on the calling thread, some inside the topology's
+ * locks: they must not call back into the topology) */
 void topology_set_log_callback(Topology* top, topology_log_fn fn, void* ctx);
+/* levels above `level` are not formatted (default 3, message; 4 enables the
+ * per-path info lines of a source's first query and the cached-path dump at
+ * topology_free, 5 the per-target debug lines) */
+void topology_set_log_level(Topology* top, int32_t level);
 void topology_set_min_latency_callback(Topology* top, topology_min_latency_fn fn, void* ctx);
-/* Build the path table now (otherwise done once, on the first query). */
+
+/* What a query answers.  The reference lazily caches one Path per vertex pair,
+ * first writer wins, and answers (s, t) with the cached (t, s) path when t's
+ * Dijkstra ran first (shd-topology.c:1292-1321, 1952-2034), so its answers
+ * depend on query order.  Both modes keep that cache's bookkeeping (which Path
+ * each query hits, its packetCount, the dump at topology_free):
+ *   TOPOLOGY_ANSWER_ROWS       (default) the source row of s: tree_s(s -> t),
+ *                              independent of query order;
+ *   TOPOLOGY_ANSWER_REFERENCE  the cached Path's values, exactly as the
+ *                              reference would return them for this query
+ *                              order (also: -1 for a query whose Dijkstra row
+ *                              fails, quirk B5; minimumPathLatency over stored
+ *                              Paths, reported to the callback as it changes).
+ * The environment variable SHADOW_SPE_PATH_CACHE=reference selects the second
+ * at topology_new. */
+#define TOPOLOGY_ANSWER_ROWS 0
+#define TOPOLOGY_ANSWER_REFERENCE 1
+int32_t topology_set_answer_mode(Topology* top, int32_t mode);
+
+/* Build the path table now (otherwise done on the first query).  Hosts may
+ * attach after sealing: the published table keeps answering the pairs it holds
+ * while the first query that needs a new vertex builds a replacement, which is
+ * swapped in atomically (readers never see a freed or half-built table; packet
+ * counts and cache state are per vertex pair and carry over). */
 int32_t topology_seal(Topology* top);
 /* introspection used by tests */
 int32_t topology_vertex_count(const Topology* top);
 int32_t topology_attached_vertex(const Topology* top, spe_in_addr_t address);   /* -1 if unknown */
+/* packetCount of the cached Path the query (src, dst) hits (exact, every pair) */
 uint64_t topology_path_packet_count(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
 double topology_min_path_latency(Topology* top);
+/* number of Paths the reference's cache would hold now (the lines the dump at
+ * topology_free prints at log level 4) */
+int64_t topology_cached_path_count(Topology* top);
 
 #ifdef __cplusplus
 }

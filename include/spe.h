@@ -121,7 +121,29 @@ typedef struct spe_table_opts {
                                      * (compute-topology-paths.py:27-33).  SSSP rows on the batch
                                      * engine only (force_sssp for complete / preferdirect graphs);
                                      * (s,s) = 0, unroutable = -1. */
+    /* Multi-device build in ONE process (Shadow is single-process, shd-master.c:390-394).
+     * n_devices > 1: device i builds the contiguous share i of the 64-source blocks
+     * (spe_device_shares) on its own host thread and stream, into a replica of the
+     * {latency, reliability} records on that device; spe_table_build then all-gathers
+     * the records (RCCL ncclAllGather over xGMI, communicators from ncclCommInitAll)
+     * so that every device holds the whole table.  Next hop / hops stay with the
+     * building device.  devices[0] is the table's home (lookups, layout).  Not
+     * combinable with block ranges, external storage, owner replay or want_aux; the
+     * on-disk cache and spe_table_build_blocks are single-device only. */
+    const int32_t* devices;         /* n_devices device indices (NULL: the graph's device) */
+    int32_t n_devices;              /* 0 or 1: single device */
+    int32_t gather;                 /* SPE_GATHER_* */
 } spe_table_opts;
+
+#define SPE_GATHER_AUTO 0           /* RCCL when the devices are distinct and librccl loads, else PEER */
+#define SPE_GATHER_RCCL 1           /* ncclAllGather, in place, one communicator per device */
+#define SPE_GATHER_PEER 2           /* hipMemcpyPeerAsync from every share's owner to every other device */
+
+/* The multi-device share of device i: 64-source blocks [block_begin[i], block_end[i])
+ * of the ceil(n_attached / 64) blocks, contiguous, every share padded to the same
+ * ceil(blocks / n_devices) (the all-gather's equal counts; a share past the end is
+ * empty).  Host-only. */
+int spe_device_shares(int32_t n_attached, int32_t n_devices, int32_t* block_begin, int32_t* block_end);
 
 /* Where a table keeps its rows.  Element (s_slot, t_slot) of a field lives at
  *   ((s_slot / 64 - block_begin) * n_attached + t_slot) * 64 + s_slot % 64
@@ -139,6 +161,10 @@ typedef struct spe_table_layout {
     void* hops;
     int32_t groups_per_launch;      /* 64-source blocks one build launch covers */
     int32_t engine;                 /* the engine the table runs on (SPE_ENGINE_BATCH / _LDS) */
+    int32_t n_devices;              /* > 1: a multi-device table; latrel is the home device's
+                                     * replica of ALL blocks (padded to n_devices equal shares),
+                                     * next_hop / hops are NULL (they stay with each share's device) */
+    int32_t device;                 /* the device latrel lives on */
 } spe_table_layout;
 
 typedef struct spe_entry {
@@ -152,7 +178,10 @@ typedef struct spe_build_stats {
     int64_t iterations;             /* relaxation rounds summed over launches */
     int64_t active_rounds;          /* relaxation rounds in which some distance/route changed */
     int64_t launches;
-    double seconds;                 /* wall time of the last spe_table_build */
+    double seconds;                 /* wall time of the last spe_table_build (incl. the gather) */
+    double gather_seconds;          /* multi-device: the all-gather of the records */
+    int32_t n_devices;
+    int32_t gather;                 /* the SPE_GATHER_* mode used */
 } spe_build_stats;
 
 const char* spe_last_error(void);
@@ -176,6 +205,18 @@ int spe_order_sources(const spe_graph* g, const int32_t* attached, int32_t n_att
  * value.  Replaces nothing in shd-topology.c (which only validates jitter,
  * :1090-1100); it serves the offline completion tool (compute-topology-paths.py). */
 int spe_graph_set_edge_aux(spe_graph* g, const double* edge_aux);
+/* Host-side rule evaluation (no GPU work; thread-safe), for a caller that keeps
+ * the reference's lazy path cache semantics (the topology shim):
+ *   spe_graph_self_path  _topology_computeShortestPathToSelf  shd-topology.c:1530-1638:
+ *                        the first minimum-latency edge of v's OUT incidence list,
+ *                        taken twice: latency 2w, reliability r*r, no vertex loss,
+ *                        next_hop = the edge's other endpoint, hops = 2; latency -1 /
+ *                        hops 0 when v has no incident edge;
+ *   spe_graph_adjacent   _topology_verticesAreAdjacent        shd-topology.c:1233-1249:
+ *                        *out = 1 when an edge from -> to exists (either direction
+ *                        for undirected graphs; a self-loop for from == to). */
+int spe_graph_self_path(const spe_graph* g, int32_t v, spe_entry* out);
+int spe_graph_adjacent(const spe_graph* g, int32_t from, int32_t to, int32_t* out);
 void spe_graph_free(spe_graph* g);
 
 /* attached[i] = vertex of source/target slot i (unique vertices). */

@@ -33,11 +33,12 @@ def _stale(out, srcs):
 
 
 def build_spe(force: bool = False) -> str:
-    srcs = [os.path.join(CSRC, f) for f in ("spe.hip", "spe_graph_prep.cpp", "spe_internal.h")]
+    srcs = [os.path.join(CSRC, f) for f in ("spe.hip", "spe_graph_prep.cpp", "spe_multi.cpp", "spe_internal.h")]
     srcs.append(os.path.join(ROOT, "include", "spe.h"))
     if force or _stale(LIB_SPE, srcs):
         _run([HIPCC, *HIP_FLAGS, "-shared", "-o", LIB_SPE,
-              os.path.join(CSRC, "spe.hip"), os.path.join(CSRC, "spe_graph_prep.cpp")])
+              os.path.join(CSRC, "spe.hip"), os.path.join(CSRC, "spe_graph_prep.cpp"),
+              os.path.join(CSRC, "spe_multi.cpp"), "-ldl", "-lpthread"])
     return LIB_SPE
 
 

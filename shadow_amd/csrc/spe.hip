@@ -1692,6 +1692,7 @@ struct spe_graph {
     spe::HostGraph hg;
     uint64_t key = 0;              // hash of the graph description (table cache key)
     int32_t device = 0;
+    std::vector<double> aux_edge;  // spe_graph_set_edge_aux values per edge (re-uploaded by clones)
     DevGraph dev{};
     HeavyPlan hp{};
     const uint8_t* d_heavy = nullptr;
@@ -1712,7 +1713,9 @@ struct spe_table {
     int32_t occ = 0;               // diagnostic: forced waves/SIMD of k_relax (0 = compiler's choice)
     RowMode md{};
     bool ext = false;
-    bool built = false;
+    bool built = false;              // every owned block holds its rows
+    std::vector<uint8_t> blk_built;  // per owned block (spe_table_build_blocks builds ranges)
+    spe::MultiDev* multi = nullptr;  // a multi-device table: everything below is unused
     Table tb{};
     int32_t* d_slot_vertex = nullptr;
     SlotInfo* d_slots = nullptr;   // row passes (both engines): per-target constants
@@ -1806,6 +1809,10 @@ int grid_for(int64_t work_items, int64_t per_block, int cap = 8192) {
 
 }  // namespace
 
+static int graph_upload(spe_graph* g);
+
+int spe::set_error(int code, const std::string& msg) { return fail(code, msg); }
+
 extern "C" {
 
 const char* spe_last_error(void) { return g_err.c_str(); }
@@ -1850,20 +1857,36 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
         g->key = f.h;
     }
     spe::prune_pendants(&g->hg, getenv("SPE_NO_PRUNE") == nullptr);
+    r = graph_upload(g);
+    if (r) {
+        spe_graph_free(g);
+        return r;
+    }
+    *out = g;
+    return SPE_OK;
+}
+
+}  // extern "C"
+
+// Device copy of a prepared host graph (spe_graph_create, and the other devices
+// of a multi-device table).  On failure the caller frees g.
+static int graph_upload(spe_graph* g) {
+    int r = SPE_OK;
     const spe::HostGraph& h = g->hg;
     DevGraph& d = g->dev;
     d.n = h.nc;
     d.n_full = h.n;
     d.nrel = (int32_t)h.icol.size();
+#ifdef SPE_DIAGNOSTICS   // experiments only: SPE_ABLATE bit 0 skips route records (inexact rows)
     d.ablate = getenv("SPE_ABLATE") ? atoi(getenv("SPE_ABLATE")) : 0;
+#else
+    d.ablate = 0;
+#endif
 #define UPBASE d
 #define UP(field, src)                                   \
     do {                                                 \
         r = dev_upload(g->allocs, src, &UPBASE.field);   \
-        if (r) {                                         \
-            spe_graph_free(g);                           \
-            return r;                                    \
-        }                                                \
+        if (r) return r;                                 \
     } while (0)
     UP(iptr, h.iptr);
     UP(icol, h.icol);
@@ -1872,10 +1895,7 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
         for (int32_t v = 0; v < h.nc; ++v)
             for (int32_t k = h.iptr[v]; k < h.iptr[v + 1]; ++k) irow[k] = v;
         r = dev_upload(g->allocs, irow, &d.irow);
-        if (r) {
-            spe_graph_free(g);
-            return r;
-        }
+        if (r) return r;
     }
     UP(iw, h.iw);
     UP(ia, h.ia);
@@ -1950,24 +1970,46 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
         UP(heavy_seg0, heavy_seg0);
 #undef UPBASE
         r = dev_upload(g->allocs, heavy, &g->d_heavy);
-        if (r) {
-            spe_graph_free(g);
-            return r;
-        }
+        if (r) return r;
         d.heavy = g->d_heavy;
         const std::vector<int32_t>& oc = h.directed ? h.ocol : h.icol;
         std::vector<uint8_t> oheavy(oc.size());
         for (size_t k = 0; k < oc.size(); ++k) oheavy[k] = heavy[oc[k]];
         r = dev_upload(g->allocs, oheavy, &d.oheavy);
-        if (r) {
-            spe_graph_free(g);
-            return r;
-        }
+        if (r) return r;
     }
 #undef UP
-    *out = g;
+    if (!g->aux_edge.empty()) {   // the auxiliary attribute, if set (spe_graph_set_edge_aux)
+        std::vector<double> ia(h.ieid.size()), fa(h.fieid.size());
+        for (size_t k = 0; k < ia.size(); ++k) ia[k] = g->aux_edge[h.ieid[k]];
+        for (size_t k = 0; k < fa.size(); ++k) fa[k] = g->aux_edge[h.fieid[k]];
+        if (ia.empty()) ia.push_back(0.0);
+        if (fa.empty()) fa.push_back(0.0);
+        if ((r = dev_upload(g->allocs, ia, &g->dev.iaux))) return r;
+        if ((r = dev_upload(g->allocs, fa, &g->dev.fiaux))) return r;
+    }
     return SPE_OK;
 }
+
+int spe::graph_clone(const spe_graph* g, int32_t device, spe_graph** out) {
+    *out = nullptr;
+    int r = check_device(device);
+    if (r) return r;
+    auto* c = new spe_graph();
+    c->hg = g->hg;
+    c->key = g->key;
+    c->device = device;
+    c->aux_edge = g->aux_edge;
+    r = graph_upload(c);
+    if (r) {
+        spe_graph_free(c);
+        return r;
+    }
+    *out = c;
+    return SPE_OK;
+}
+
+extern "C" {
 
 int spe_graph_set_edge_aux(spe_graph* g, const double* edge_aux) {
     if (!g || (!edge_aux && g->hg.m > 0)) return fail(SPE_EINVAL, "NULL argument");
@@ -1975,6 +2017,7 @@ int spe_graph_set_edge_aux(spe_graph* g, const double* edge_aux) {
     const spe::HostGraph& h = g->hg;
     for (int64_t e = 0; e < h.m; ++e)
         if (!std::isfinite(edge_aux[e])) return fail(SPE_EINVAL, "edge " + std::to_string(e) + " aux value is not finite");
+    g->aux_edge.assign(edge_aux, edge_aux + h.m);
     std::vector<double> ia(h.ieid.size()), fa(h.fieid.size());
     for (size_t k = 0; k < ia.size(); ++k) ia[k] = edge_aux[h.ieid[k]];
     for (size_t k = 0; k < fa.size(); ++k) fa[k] = edge_aux[h.fieid[k]];
@@ -1997,6 +2040,35 @@ int spe_graph_info_get(const spe_graph* g, spe_graph_info* out) {
     out->parallel_latency_differs = g->hg.multi_rep;
     out->weight_floor_ok = g->hg.weight_floor_ok;
     out->device = g->device;
+    return SPE_OK;
+}
+
+int spe_graph_self_path(const spe_graph* g, int32_t v, spe_entry* out) {
+    if (!g || !out) return fail(SPE_EINVAL, "NULL argument");
+    const spe::HostGraph& h = g->hg;
+    if (v < 0 || v >= h.n) return fail(SPE_EINVAL, "vertex out of range");
+    if (h.self_other[(size_t)v] < 0) {
+        *out = spe_entry{-1.0, -1.0, -1, 0};
+    } else {
+        *out = spe_entry{h.self_w2[(size_t)v], h.self_a2[(size_t)v], h.self_other[(size_t)v], 2};
+    }
+    return SPE_OK;
+}
+
+int spe_graph_adjacent(const spe_graph* g, int32_t from, int32_t to, int32_t* out) {
+    if (!g || !out) return fail(SPE_EINVAL, "NULL argument");
+    const spe::HostGraph& h = g->hg;
+    if (from < 0 || from >= h.n || to < 0 || to >= h.n) return fail(SPE_EINVAL, "vertex out of range");
+    if (from == to) {   // self-loops are kept out of the CSRs (get_eid(v, v): loop_eid)
+        *out = h.loop_eid[(size_t)from] >= 0 ? 1 : 0;
+        return SPE_OK;
+    }
+    // the out-CSR of a directed graph (never pruned), the full original-id in-CSR
+    // of an undirected one (symmetric: search the list of `to` for `from`)
+    const std::vector<int32_t>& ptr = h.directed ? h.optr : h.fiptr;
+    const std::vector<int32_t>& col = h.directed ? h.ocol : h.ficol;
+    const int32_t row = h.directed ? from : to, key = h.directed ? to : from;
+    *out = std::binary_search(col.begin() + ptr[(size_t)row], col.begin() + ptr[(size_t)row + 1], key) ? 1 : 0;
     return SPE_OK;
 }
 
@@ -2092,20 +2164,26 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         if (vslot[v] >= 0) return fail(SPE_EINVAL, "attached vertices must be unique");
         vslot[v] = i;
     }
+    spe_table_opts o{};
+    if (opts) o = *opts;
+    const int32_t nblk_all = (n_attached + WAVE - 1) / WAVE;
+    // every argument check before the first allocation (nothing to unwind)
+    if (o.block_begin != 0 || o.block_end != 0) {
+        if (o.block_begin < 0 || o.block_end > nblk_all || o.block_begin > o.block_end)
+            return fail(SPE_EINVAL, "block range out of bounds");
+    }
+    if (o.owner_rank && (o.block_begin != 0 || (o.block_end != 0 && o.block_end != nblk_all)))
+        return fail(SPE_EUNSUPPORTED, "owner replay needs a table that owns every source block");
+    if ((o.ext_latrel || o.ext_next_hop || o.ext_hops) && !(o.ext_latrel && o.ext_next_hop && o.ext_hops))
+        return fail(SPE_EINVAL, "external storage needs all three fields");
+    if (o.devices && o.n_devices < 1) return fail(SPE_EINVAL, "n_devices must be >= 1 with a device list");
     auto* t = new spe_table();
     t->g = g;
     t->A = n_attached;
     t->attached.assign(attached, attached + n_attached);
-    const int32_t nblk_all = (n_attached + WAVE - 1) / WAVE;
     t->blk0 = 0;
     t->blk1 = nblk_all;
-    spe_table_opts o{};
-    if (opts) o = *opts;
     if (o.block_begin != 0 || o.block_end != 0) {
-        if (o.block_begin < 0 || o.block_end > nblk_all || o.block_begin > o.block_end) {
-            delete t;
-            return fail(SPE_EINVAL, "block range out of bounds");
-        }
         t->blk0 = o.block_begin;
         t->blk1 = o.block_end;
     }
@@ -2128,6 +2206,15 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         f.val(aux);
         if (has_owner) f.add(o.owner_rank, (size_t)n_attached * sizeof(int32_t));
         t->key = f.h;
+    }
+    if (o.devices) {   // one process, several devices (spe_multi.cpp)
+        int r = spe::multi_create(g, attached, n_attached, o, &t->multi);
+        if (r) {
+            delete t;
+            return r;
+        }
+        *out = t;
+        return SPE_OK;
     }
     t->md.complete = g->hg.complete && !force;
     t->md.prefer = g->hg.prefer_direct && !force;
@@ -2189,8 +2276,13 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         if (t->engine == SPE_ENGINE_LDS && !t->md.complete) {
             // no HBM state: one launch covers every owned block (unless asked otherwise)
             if (o.groups_per_launch <= 0) t->groups = std::max(1, t->blk1 - t->blk0);
-            HIP_TRY(hipFuncSetAttribute((const void*)k_sssp_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds_bytes(g->hg.nc)));
+            const hipError_t fe = hipFuncSetAttribute((const void*)k_sssp_lds,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      (int)lds_bytes(g->hg.nc));
+            if (fe != hipSuccess) {
+                delete t;
+                return fail(SPE_EHIP, std::string("hipFuncSetAttribute(k_sssp_lds): ") + hipGetErrorString(fe));
+            }
         }
     }
     t->infl = lanes == 64 ? 8 : 4;
@@ -2211,10 +2303,6 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         }                       \
     } while (0)
     if (o.ext_latrel || o.ext_next_hop || o.ext_hops) {
-        if (!(o.ext_latrel && o.ext_next_hop && o.ext_hops)) {
-            delete t;
-            return fail(SPE_EINVAL, "external storage needs all three fields");
-        }
         t->ext = true;
         t->built = o.ext_filled != 0;
         t->tb.lr = (double2*)o.ext_latrel;
@@ -2225,11 +2313,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         TRY(dev_alloc(t->allocs, &t->tb.next, elems));
         TRY(dev_alloc(t->allocs, &t->tb.hops, elems));
     }
-    if (o.owner_rank) {   // owner replay needs every source row in this table
-        if (t->blk0 != 0 || t->blk1 != nblk_all) {
-            delete t;
-            return fail(SPE_EUNSUPPORTED, "owner replay needs a table that owns every source block");
-        }
+    if (o.owner_rank) {   // owner replay needs every source row in this table (checked above)
         std::vector<int32_t> rk(o.owner_rank, o.owner_rank + n_attached);
         const int32_t* tmpr = nullptr;
         TRY(dev_upload(t->allocs, rk, &tmpr));
@@ -2310,16 +2394,27 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     t->d_srcc = t->srcc_buf[0];
     TRY(dev_alloc(t->allocs, &t->d_min, 1));
 #undef TRY
-    HIP_TRY(hipHostMalloc((void**)&t->h_srcv, 2 * G * WAVE * sizeof(int32_t), hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void**)&t->h_counts, std::max<size_t>(64, (size_t)t->max_iters + 2) * sizeof(int32_t),
-                          hipHostMallocDefault));
-    HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+    // every failure from here on releases what was allocated (spe_table_free)
+#define HTRY(expr)                                                                         \
+    do {                                                                                   \
+        const hipError_t _e = (expr);                                                      \
+        if (_e != hipSuccess) {                                                            \
+            spe_table_free(t);                                                             \
+            return fail(SPE_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
+        }                                                                                  \
+    } while (0)
+    HTRY(hipHostMalloc((void**)&t->h_srcv, 2 * G * WAVE * sizeof(int32_t), hipHostMallocDefault));
+    HTRY(hipHostMalloc((void**)&t->h_counts, std::max<size_t>(64, (size_t)t->max_iters + 2) * sizeof(int32_t),
+                       hipHostMallocDefault));
+    HTRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
     if (t->overlap) {
-        HIP_TRY(hipStreamCreateWithFlags(&t->rows_stream, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&t->ev_relaxed, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&t->ev_rows[0], hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&t->ev_rows[1], hipEventDisableTiming));
+        HTRY(hipStreamCreateWithFlags(&t->rows_stream, hipStreamNonBlocking));
+        HTRY(hipEventCreateWithFlags(&t->ev_relaxed, hipEventDisableTiming));
+        HTRY(hipEventCreateWithFlags(&t->ev_rows[0], hipEventDisableTiming));
+        HTRY(hipEventCreateWithFlags(&t->ev_rows[1], hipEventDisableTiming));
     }
+#undef HTRY
+    t->blk_built.assign((size_t)(t->blk1 - t->blk0), t->built ? 1 : 0);
     *out = t;
     return SPE_OK;
 }
@@ -2479,6 +2574,11 @@ static void launch_rows_sssp(spe_table* t, int grid, int32_t blocks, int32_t sb0
 
 int spe_table_build(spe_table* t, void* stream) {
     if (!t) return fail(SPE_EINVAL, "NULL table");
+    if (t->multi) {
+        const int r = spe::multi_build(t->multi, &t->stats);
+        t->built = r == SPE_OK && spe::multi_built(t->multi);
+        return r;
+    }
     int r = spe_table_build_blocks(t, t->blk0, t->blk1, stream);
     if (r || !t->d_rank || t->md.complete) return r;
     hipStream_t s = stream ? (hipStream_t)stream : t->stream;
@@ -2492,6 +2592,7 @@ int spe_table_build(spe_table* t, void* stream) {
 
 int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end, void* stream) {
     if (!t) return fail(SPE_EINVAL, "NULL table");
+    if (t->multi) return fail(SPE_EUNSUPPORTED, "a multi-device table builds whole (spe_table_build)");
     if (block_begin < t->blk0 || block_end > t->blk1 || block_begin > block_end)
         return fail(SPE_EINVAL, "block range not owned by this table");
     HIP_TRY(hipSetDevice(t->g->device));
@@ -2599,12 +2700,15 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
     }
     HIP_TRY(hipStreamSynchronize(s));
     t->stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    t->built = true;
+    t->stats.n_devices = 1;
+    for (int32_t b = block_begin; b < block_end; ++b) t->blk_built[(size_t)(b - t->blk0)] = 1;
+    t->built = std::all_of(t->blk_built.begin(), t->blk_built.end(), [](uint8_t x) { return x != 0; });
     return SPE_OK;
 }
 
 int spe_table_profile_enable(spe_table* t, int32_t enable) {
     if (!t) return fail(SPE_EINVAL, "NULL table");
+    if (t->multi) return spe::multi_profile_enable(t->multi, enable);
     t->prof = enable != 0;
     t->kp = spe_kernel_profile{};
     t->pending.clear();
@@ -2614,6 +2718,7 @@ int spe_table_profile_enable(spe_table* t, int32_t enable) {
 
 int spe_table_profile_get(const spe_table* t, spe_kernel_profile* out) {
     if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
+    if (t->multi) return spe::multi_profile_get(t->multi, out);
     *out = t->kp;
     return SPE_OK;
 }
@@ -2626,6 +2731,9 @@ int spe_table_build_stats(const spe_table* t, spe_build_stats* out) {
 
 int spe_table_layout_get(const spe_table* t, spe_table_layout* out) {
     if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
+    if (t->multi) return spe::multi_layout(t->multi, out);
+    out->n_devices = 1;
+    out->device = t->g->device;
     out->n_attached = t->A;
     out->block_begin = t->blk0;
     out->block_end = t->blk1;
@@ -2640,10 +2748,14 @@ int spe_table_layout_get(const spe_table* t, spe_table_layout* out) {
 
 int spe_table_get(const spe_table* t, int32_t s_slot, int32_t t_slot, spe_entry* out) {
     if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
-    if (!t->built) return fail(SPE_ESTATE, "table not built");
+    if (t->multi) {
+        if (!t->built) return fail(SPE_ESTATE, "table not built");
+        return spe::multi_get(t->multi, s_slot, t_slot, out);
+    }
     if (s_slot < 0 || s_slot >= t->A || t_slot < 0 || t_slot >= t->A) return fail(SPE_EINVAL, "slot out of range");
     const int32_t sb = s_slot / WAVE;
     if (sb < t->blk0 || sb >= t->blk1) return fail(SPE_EINVAL, "source row not owned by this table");
+    if (!t->blk_built[(size_t)(sb - t->blk0)]) return fail(SPE_ESTATE, "source row not built");
     HIP_TRY(hipSetDevice(t->g->device));
     const size_t o = ((size_t)(sb - t->blk0) * t->A + t_slot) * WAVE + (s_slot % WAVE);
     uint16_t h = 0;
@@ -2699,9 +2811,10 @@ __global__ __launch_bounds__(256) void k_sb64_rows(int32_t A, const double2* __r
 static int download_rows(const spe_table* t, int32_t row_begin, int32_t row_end, double* latency,
                          double* reliability, int32_t* next_hop, int32_t* hops, double* aux) {
     if (!t) return fail(SPE_EINVAL, "NULL table");
-    if (!t->built) return fail(SPE_ESTATE, "table not built");
     if (row_begin < t->blk0 * WAVE || row_end > std::min(t->A, t->blk1 * WAVE) || row_begin > row_end)
         return fail(SPE_EINVAL, "row range not owned by this table");
+    for (int32_t b = row_begin / WAVE; b < (row_end + WAVE - 1) / WAVE; ++b)
+        if (!t->blk_built[(size_t)(b - t->blk0)]) return fail(SPE_ESTATE, "rows not built");
     if (row_begin == row_end) return SPE_OK;
     HIP_TRY(hipSetDevice(t->g->device));
     const int32_t A = t->A;
@@ -2749,11 +2862,16 @@ static int download_rows(const spe_table* t, int32_t row_begin, int32_t row_end,
 
 int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, double* latency,
                        double* reliability, int32_t* next_hop, int32_t* hops) {
+    if (t && t->multi) {
+        if (!t->built) return fail(SPE_ESTATE, "table not built");
+        return spe::multi_download(t->multi, row_begin, row_end, latency, reliability, next_hop, hops);
+    }
     return download_rows(t, row_begin, row_end, latency, reliability, next_hop, hops, nullptr);
 }
 
 int spe_table_download_aux(const spe_table* t, int32_t row_begin, int32_t row_end, double* aux) {
     if (!t || !aux) return fail(SPE_EINVAL, "NULL argument");
+    if (t->multi) return fail(SPE_EUNSUPPORTED, "multi-device tables have no aux field");
     if (!t->tb.aux) return fail(SPE_ESTATE, "table was created without want_aux");
     return download_rows(t, row_begin, row_end, nullptr, nullptr, nullptr, nullptr, aux);
 }
@@ -2763,6 +2881,7 @@ int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, doub
     if (!t || (q > 0 && (!d_pairs || !d_latency || !d_reliability || !d_ok))) return fail(SPE_EINVAL, "bad arguments");
     if (!t->built) return fail(SPE_ESTATE, "table not built");
     if (q == 0) return SPE_OK;
+    if (t->multi) return spe::multi_lookup(t->multi, d_pairs, q, d_latency, d_reliability, d_ok, stream);
     HIP_TRY(hipSetDevice(t->g->device));
     hipStream_t s = stream ? (hipStream_t)stream : t->stream;
     k_lookup<1><<<grid_for(q, BLOCK, 16384), BLOCK, 0, s>>>((const int2*)d_pairs, q, t->blk0, t->blk1, t->tb,
@@ -2771,6 +2890,24 @@ int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, doub
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return SPE_OK;
 }
+
+}  // extern "C"
+
+int spe::lookup_on_replica(int32_t device, const void* latrel, int32_t A, int32_t nblk, const int32_t* d_pairs,
+                           int64_t q, double* d_latency, double* d_reliability, uint8_t* d_ok, void* stream) {
+    HIP_TRY(hipSetDevice(device));
+    Table tb{};
+    tb.lr = (double2*)latrel;
+    tb.A = A;
+    hipStream_t s = (hipStream_t)stream;
+    k_lookup<1><<<grid_for(q, BLOCK, 16384), BLOCK, 0, s>>>((const int2*)d_pairs, q, 0, nblk, tb, d_latency,
+                                                           d_reliability, d_ok);
+    HIP_TRY(hipGetLastError());
+    if (!stream) HIP_TRY(hipStreamSynchronize(s));
+    return SPE_OK;
+}
+
+extern "C" {
 
 int spe_fw_apsp(spe_graph* g, double* d_dist, int64_t ld, int32_t* d_next, void* stream, double* seconds) {
     if (!g || !d_dist) return fail(SPE_EINVAL, "NULL argument");
@@ -2807,7 +2944,8 @@ int spe_fw_apsp(spe_graph* g, double* d_dist, int64_t ld, int32_t* d_next, void*
 
 int spe_table_min_latency(const spe_table* t, double* out) {
     if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
-    if (!t->built) return fail(SPE_ESTATE, "table not built");
+    if (!t->built) return fail(SPE_ESTATE, "table not built (every owned block)");
+    if (t->multi) return spe::multi_min_latency(t->multi, out);
     HIP_TRY(hipSetDevice(t->g->device));
     const unsigned long long init = 0x7FF0000000000000ull;  // +inf
     HIP_TRY(hipMemcpyAsync(t->d_min, &init, sizeof(init), hipMemcpyHostToDevice, t->stream));
@@ -2863,8 +3001,9 @@ int spe_table_key(const spe_table* t, uint64_t* key) {
 
 int spe_table_save(const spe_table* t, const char* path) {
     if (t && t->tb.aux) return fail(SPE_EUNSUPPORTED, "the table cache does not hold want_aux rows");
+    if (t && t->multi) return fail(SPE_EUNSUPPORTED, "the table cache holds single-device tables");
     if (!t || !path) return fail(SPE_EINVAL, "NULL argument");
-    if (!t->built) return fail(SPE_ESTATE, "table not built");
+    if (!t->built) return fail(SPE_ESTATE, "table not built (every owned block)");
     HIP_TRY(hipSetDevice(t->g->device));
     HIP_TRY(hipStreamSynchronize(t->stream));
     Field f[3];
@@ -2906,6 +3045,7 @@ int spe_table_save(const spe_table* t, const char* path) {
 
 int spe_table_load(spe_table* t, const char* path) {
     if (t && t->tb.aux) return fail(SPE_EUNSUPPORTED, "the table cache does not hold want_aux rows");
+    if (t && t->multi) return fail(SPE_EUNSUPPORTED, "the table cache holds single-device tables");
     if (!t || !path) return fail(SPE_EINVAL, "NULL argument");
     HIP_TRY(hipSetDevice(t->g->device));
     FILE* fp = fopen(path, "rb");
@@ -2935,12 +3075,20 @@ int spe_table_load(spe_table* t, const char* path) {
     }
     if (stage) (void)hipHostFree(stage);
     fclose(fp);
-    if (rc == SPE_OK) t->built = true;
+    if (rc == SPE_OK) {
+        t->built = true;
+        std::fill(t->blk_built.begin(), t->blk_built.end(), (uint8_t)1);
+    }
     return rc;
 }
 
 void spe_table_free(spe_table* t) {
     if (!t) return;
+    if (t->multi) {
+        spe::multi_free(t->multi);
+        delete t;
+        return;
+    }
     (void)hipSetDevice(t->g->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     for (void* p : t->allocs) (void)hipFree(p);

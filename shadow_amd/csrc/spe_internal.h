@@ -52,6 +52,32 @@ struct HostGraph {
 };
 
 int prepare_graph(const spe_graph_desc* d, HostGraph* hg, std::string* err);
+// spe_last_error's message for the calling thread; returns code
+int set_error(int code, const std::string& msg);
+// the prepared graph uploaded to another device (multi-device tables)
+int graph_clone(const spe_graph* g, int32_t device, spe_graph** out);
+// k_lookup over a caller-described SB64 {latency, reliability} span holding
+// blocks [0, nblk) of an A-target table on `device`
+int lookup_on_replica(int32_t device, const void* latrel, int32_t A, int32_t nblk, const int32_t* d_pairs,
+                      int64_t q, double* d_latency, double* d_reliability, uint8_t* d_ok, void* stream);
+
+// Multi-device tables (spe_multi.cpp): one part table per device over a
+// contiguous share of the 64-source blocks; the {latency, reliability}
+// records are then all-gathered so every device holds the whole table.
+struct MultiDev;
+int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_table_opts& o, MultiDev** out);
+void multi_free(MultiDev* m);
+int multi_build(MultiDev* m, spe_build_stats* stats);
+bool multi_built(const MultiDev* m);
+int multi_get(const MultiDev* m, int32_t s_slot, int32_t t_slot, spe_entry* out);
+int multi_download(const MultiDev* m, int32_t row_begin, int32_t row_end, double* latency, double* reliability,
+                   int32_t* next_hop, int32_t* hops);
+int multi_lookup(const MultiDev* m, const int32_t* d_pairs, int64_t q, double* d_latency, double* d_reliability,
+                 uint8_t* d_ok, void* stream);
+int multi_min_latency(const MultiDev* m, double* out);
+int multi_layout(const MultiDev* m, spe_table_layout* out);
+int multi_profile_enable(MultiDev* m, int32_t enable);
+int multi_profile_get(const MultiDev* m, spe_kernel_profile* out);
 // Restrict the relaxation CSR to the core (no-op for directed graphs or when
 // `enable` is false); keeps the full CSR in hg->f*.
 void prune_pendants(HostGraph* hg, bool enable);

@@ -1,0 +1,365 @@
+// spe_multi.cpp -- multi-device path tables in one process.
+//
+// Shadow runs as ONE process (shd-master.c:390-394: "For now we only have one
+// slave"), so the drop-in cannot rely on one rank per GPU: the library itself
+// drives every device of the node.  A multi-device table is one part table per
+// device, each over a contiguous share of the 64-source blocks (the sources are
+// independent rows: no exchange during the build), built concurrently from one
+// host thread per device on that device's own stream.  The parts write their
+// {latency, reliability} records straight into a full-size replica on their own
+// device (at their share's offset), and one all-gather then fills every replica:
+//   RCCL  ncclCommInitAll over the device list + ncclGroupStart / ncclAllGather
+//         (in place: each device's send buffer is its own share of its replica)
+//         / ncclGroupEnd -- RCCL's collective over the xGMI links;
+//   PEER  hipMemcpyPeerAsync of every share to every other device (also the path
+//         for a device list that repeats a GPU, which RCCL refuses).
+// Next hop and hop count stay with the device that built them.  RCCL is loaded
+// with dlopen on first use, so single-device users never load it.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "spe_internal.h"
+
+namespace spe {
+
+namespace {
+
+constexpr int32_t kWave = 64;
+
+struct Rccl {
+    bool tried = false;
+    bool ok = false;
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+Rccl& rccl() {
+    static Rccl r;
+    if (r.tried) return r;
+    r.tried = true;
+    // the process's RCCL if one is loaded already (e.g. by PyTorch), else ROCm's
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+    if (!h) return r;
+    r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
+    r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+    r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+    r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+    r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+    r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+    r.ok = r.comm_init_all && r.comm_destroy && r.all_gather && r.group_start && r.group_end && r.error_string;
+    return r;
+}
+
+int hip_fail(const char* what, hipError_t e) { return set_error(SPE_EHIP, std::string(what) + ": " + hipGetErrorString(e)); }
+
+}  // namespace
+
+struct MultiDev {
+    int32_t A = 0, nblk = 0, cb = 0, n = 0;
+    int32_t gather = SPE_GATHER_PEER;
+    std::vector<int32_t> devs;
+    std::vector<int32_t> b0, b1;           // share of each device
+    spe_graph* home = nullptr;             // the caller's graph (not owned)
+    std::vector<spe_graph*> graphs;        // per device: home, or a clone on that device
+    std::vector<spe_table*> parts;         // nullptr for an empty share
+    std::vector<void*> replica;            // full {lat, rel} span per device: n * cb blocks
+    std::vector<void*> next, hops;         // the device's own share
+    std::vector<hipStream_t> streams;
+    std::vector<ncclComm_t> comms;
+    bool built = false;
+    spe_build_stats stats{};
+
+    size_t blk_elems() const { return (size_t)A * kWave; }
+};
+
+int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_table_opts& o, MultiDev** out) {
+    *out = nullptr;
+    if (o.block_begin || o.block_end || o.ext_latrel || o.ext_next_hop || o.ext_hops || o.owner_rank || o.want_aux)
+        return set_error(SPE_EUNSUPPORTED, "a multi-device table owns every block and its own storage "
+                                           "(no block range, external storage, owner replay or want_aux)");
+    if (o.gather < SPE_GATHER_AUTO || o.gather > SPE_GATHER_PEER) return set_error(SPE_EINVAL, "unknown gather mode");
+    spe_graph_info gi;
+    spe_graph_info_get(g, &gi);
+    auto* m = new MultiDev();
+    m->home = g;
+    m->A = A;
+    m->n = o.n_devices;
+    m->devs.assign(o.devices, o.devices + o.n_devices);
+    m->nblk = (A + kWave - 1) / kWave;
+    m->b0.resize(m->n);
+    m->b1.resize(m->n);
+    spe_device_shares(A, m->n, m->b0.data(), m->b1.data());
+    m->cb = (m->nblk + m->n - 1) / m->n;
+    bool distinct = true;
+    for (int i = 0; i < m->n; ++i)
+        for (int j = 0; j < i; ++j) distinct &= m->devs[i] != m->devs[j];
+    if (o.gather == SPE_GATHER_RCCL && !distinct) {
+        delete m;
+        return set_error(SPE_EUNSUPPORTED, "RCCL needs distinct devices (a repeated device: use SPE_GATHER_PEER)");
+    }
+    m->gather = o.gather == SPE_GATHER_PEER || !distinct ? SPE_GATHER_PEER
+                : (rccl().ok ? SPE_GATHER_RCCL : (o.gather == SPE_GATHER_RCCL ? -1 : SPE_GATHER_PEER));
+    if (m->gather < 0) {
+        delete m;
+        return set_error(SPE_EUNSUPPORTED, "librccl.so.1 could not be loaded");
+    }
+    m->graphs.assign(m->n, nullptr);
+    m->parts.assign(m->n, nullptr);
+    m->replica.assign(m->n, nullptr);
+    m->next.assign(m->n, nullptr);
+    m->hops.assign(m->n, nullptr);
+    m->streams.assign(m->n, nullptr);
+    int r = SPE_OK;
+    const size_t rep_bytes = (size_t)m->n * m->cb * m->blk_elems() * 2 * sizeof(double);
+    const size_t own = (size_t)m->cb * m->blk_elems();
+    for (int d = 0; d < m->n && !r; ++d) {
+        if (m->devs[d] == gi.device) {
+            m->graphs[d] = g;
+        } else if ((r = graph_clone(g, m->devs[d], &m->graphs[d]))) {
+            break;
+        }
+        hipError_t e = hipSetDevice(m->devs[d]);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->streams[d], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMalloc(&m->replica[d], rep_bytes);
+        if (e == hipSuccess) e = hipMalloc(&m->next[d], std::max<size_t>(1, own) * sizeof(int32_t));
+        if (e == hipSuccess) e = hipMalloc(&m->hops[d], std::max<size_t>(1, own) * sizeof(uint16_t));
+        if (e != hipSuccess) {
+            r = hip_fail("multi-device table storage", e);
+            break;
+        }
+        if (m->b1[d] <= m->b0[d]) continue;   // an empty share (more devices than blocks)
+        spe_table_opts po = o;
+        po.devices = nullptr;
+        po.n_devices = 0;
+        po.block_begin = m->b0[d];
+        po.block_end = m->b1[d];
+        po.ext_latrel = (char*)m->replica[d] + (size_t)m->b0[d] * m->blk_elems() * 2 * sizeof(double);
+        po.ext_next_hop = m->next[d];
+        po.ext_hops = m->hops[d];
+        po.ext_filled = 0;
+        r = spe_table_create(m->graphs[d], attached, A, &po, &m->parts[d]);
+    }
+    if (!r && m->gather == SPE_GATHER_RCCL) {
+        m->comms.assign(m->n, nullptr);
+        const ncclResult_t nr = rccl().comm_init_all(m->comms.data(), m->n, m->devs.data());
+        if (nr != ncclSuccess) {
+            m->comms.clear();
+            r = set_error(SPE_EHIP, std::string("ncclCommInitAll: ") + rccl().error_string(nr));
+        }
+    }
+    if (r) {
+        multi_free(m);
+        return r;
+    }
+    *out = m;
+    return SPE_OK;
+}
+
+void multi_free(MultiDev* m) {
+    if (!m) return;
+    for (ncclComm_t c : m->comms)
+        if (c) rccl().comm_destroy(c);
+    for (int d = 0; d < m->n; ++d) {
+        if (m->parts[d]) spe_table_free(m->parts[d]);
+        (void)hipSetDevice(m->devs[d]);
+        if (m->streams[d]) (void)hipStreamSynchronize(m->streams[d]);
+        if (m->replica[d]) (void)hipFree(m->replica[d]);
+        if (m->next[d]) (void)hipFree(m->next[d]);
+        if (m->hops[d]) (void)hipFree(m->hops[d]);
+        if (m->streams[d]) (void)hipStreamDestroy(m->streams[d]);
+        if (m->graphs[d] && m->graphs[d] != m->home) spe_graph_free(m->graphs[d]);
+    }
+    delete m;
+}
+
+static int gather_records(MultiDev* m) {
+    const size_t share_bytes = (size_t)m->cb * m->blk_elems() * 2 * sizeof(double);
+    if (m->gather == SPE_GATHER_RCCL) {
+        Rccl& R = rccl();
+        R.group_start();
+        ncclResult_t nr = ncclSuccess;
+        for (int d = 0; d < m->n && nr == ncclSuccess; ++d) {
+            if (hipSetDevice(m->devs[d]) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
+            const void* send = (const char*)m->replica[d] + (size_t)d * share_bytes;
+            nr = R.all_gather(send, m->replica[d], (size_t)m->cb * m->blk_elems() * 2, ncclDouble, m->comms[d],
+                              m->streams[d]);
+        }
+        const ncclResult_t ne = R.group_end();
+        if (nr != ncclSuccess || ne != ncclSuccess)
+            return set_error(SPE_EHIP, std::string("ncclAllGather: ") + R.error_string(nr != ncclSuccess ? nr : ne));
+    } else {
+        for (int e = 0; e < m->n; ++e) {   // device e pulls every other share
+            if (hipSetDevice(m->devs[e]) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
+            for (int d = 0; d < m->n; ++d) {
+                if (d == e || m->b1[d] <= m->b0[d]) continue;
+                const size_t off = (size_t)m->b0[d] * m->blk_elems() * 2 * sizeof(double);
+                const size_t bytes = (size_t)(m->b1[d] - m->b0[d]) * m->blk_elems() * 2 * sizeof(double);
+                const hipError_t he = hipMemcpyPeerAsync((char*)m->replica[e] + off, m->devs[e],
+                                                         (const char*)m->replica[d] + off, m->devs[d], bytes,
+                                                         m->streams[e]);
+                if (he != hipSuccess) return hip_fail("hipMemcpyPeerAsync", he);
+            }
+        }
+    }
+    for (int d = 0; d < m->n; ++d) {
+        if (hipSetDevice(m->devs[d]) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
+        const hipError_t he = hipStreamSynchronize(m->streams[d]);
+        if (he != hipSuccess) return hip_fail("gather sync", he);
+    }
+    return SPE_OK;
+}
+
+int multi_build(MultiDev* m, spe_build_stats* stats) {
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<int> rc(m->n, SPE_OK);
+    std::vector<std::string> err(m->n);
+    std::vector<std::thread> th;
+    for (int d = 0; d < m->n; ++d) {
+        if (!m->parts[d]) continue;
+        th.emplace_back([m, d, &rc, &err]() {
+            rc[d] = spe_table_build(m->parts[d], nullptr);
+            if (rc[d]) err[d] = spe_last_error();
+        });
+    }
+    for (auto& x : th) x.join();
+    for (int d = 0; d < m->n; ++d)
+        if (rc[d]) return set_error(rc[d], "device " + std::to_string(m->devs[d]) + ": " + err[d]);
+    const auto t1 = std::chrono::steady_clock::now();
+    if (int r = gather_records(m)) return r;
+    const auto t2 = std::chrono::steady_clock::now();
+    spe_build_stats s{};
+    for (int d = 0; d < m->n; ++d) {
+        if (!m->parts[d]) continue;
+        spe_build_stats p{};
+        spe_table_build_stats(m->parts[d], &p);
+        s.iterations += p.iterations;
+        s.active_rounds += p.active_rounds;
+        s.launches += p.launches;
+    }
+    s.seconds = std::chrono::duration<double>(t2 - t0).count();
+    s.gather_seconds = std::chrono::duration<double>(t2 - t1).count();
+    s.n_devices = m->n;
+    s.gather = m->gather;
+    m->stats = s;
+    if (stats) *stats = s;
+    m->built = true;
+    return SPE_OK;
+}
+
+bool multi_built(const MultiDev* m) { return m->built; }
+
+static int owner_of(const MultiDev* m, int32_t s_slot) {
+    const int32_t b = s_slot / kWave;
+    for (int d = 0; d < m->n; ++d)
+        if (b >= m->b0[d] && b < m->b1[d]) return d;
+    return -1;
+}
+
+int multi_get(const MultiDev* m, int32_t s_slot, int32_t t_slot, spe_entry* out) {
+    if (s_slot < 0 || s_slot >= m->A || t_slot < 0 || t_slot >= m->A) return set_error(SPE_EINVAL, "slot out of range");
+    return spe_table_get(m->parts[owner_of(m, s_slot)], s_slot, t_slot, out);
+}
+
+int multi_download(const MultiDev* m, int32_t row_begin, int32_t row_end, double* latency, double* reliability,
+                   int32_t* next_hop, int32_t* hops) {
+    if (row_begin < 0 || row_end > m->A || row_begin > row_end) return set_error(SPE_EINVAL, "row range out of bounds");
+    for (int32_t r0 = row_begin; r0 < row_end;) {
+        const int d = owner_of(m, r0);
+        const int32_t r1 = std::min(row_end, m->b1[d] * kWave);
+        const size_t off = (size_t)(r0 - row_begin) * m->A;
+        int rc = spe_table_download(m->parts[d], r0, r1, latency ? latency + off : nullptr,
+                                    reliability ? reliability + off : nullptr, next_hop ? next_hop + off : nullptr,
+                                    hops ? hops + off : nullptr);
+        if (rc) return rc;
+        r0 = r1;
+    }
+    return SPE_OK;
+}
+
+int multi_lookup(const MultiDev* m, const int32_t* d_pairs, int64_t q, double* d_latency, double* d_reliability,
+                 uint8_t* d_ok, void* stream) {
+    return lookup_on_replica(m->devs[0], m->replica[0], m->A, m->nblk, d_pairs, q, d_latency, d_reliability, d_ok,
+                             stream);
+}
+
+int multi_min_latency(const MultiDev* m, double* out) {
+    double best = 0.0;
+    for (int d = 0; d < m->n; ++d) {
+        if (!m->parts[d]) continue;
+        double v = 0.0;
+        if (int r = spe_table_min_latency(m->parts[d], &v)) return r;
+        if (v > 0 && (best == 0.0 || v < best)) best = v;   // 0 = the reference's "unset"
+    }
+    *out = best;
+    return SPE_OK;
+}
+
+int multi_layout(const MultiDev* m, spe_table_layout* out) {
+    spe_table_layout p{};
+    for (int d = 0; d < m->n; ++d)
+        if (m->parts[d]) {
+            spe_table_layout_get(m->parts[d], &p);
+            break;
+        }
+    out->n_attached = m->A;
+    out->block_begin = 0;
+    out->block_end = m->nblk;
+    out->elems = (int64_t)m->n * m->cb * m->A * kWave;
+    out->latrel = m->replica[0];
+    out->next_hop = nullptr;
+    out->hops = nullptr;
+    out->groups_per_launch = p.groups_per_launch;
+    out->engine = p.engine;
+    out->n_devices = m->n;
+    out->device = m->devs[0];
+    return SPE_OK;
+}
+
+int multi_profile_enable(MultiDev* m, int32_t enable) {
+    for (spe_table* p : m->parts)
+        if (p)
+            if (int r = spe_table_profile_enable(p, enable)) return r;
+    return SPE_OK;
+}
+
+int multi_profile_get(const MultiDev* m, spe_kernel_profile* out) {
+    *out = spe_kernel_profile{};
+    for (spe_table* p : m->parts) {
+        if (!p) continue;
+        spe_kernel_profile k{};
+        spe_table_profile_get(p, &k);
+        for (int i = 0; i < SPE_K_COUNT; ++i) {
+            out->ms[i] = std::max(out->ms[i], k.ms[i]);   // the parts run concurrently: the slowest
+            out->launches[i] += k.launches[i];
+        }
+    }
+    return SPE_OK;
+}
+
+}  // namespace spe
+
+extern "C" int spe_device_shares(int32_t n_attached, int32_t n_devices, int32_t* block_begin, int32_t* block_end) {
+    if (n_attached < 0 || n_devices < 1 || !block_begin || !block_end)
+        return spe::set_error(SPE_EINVAL, "spe_device_shares: bad arguments");
+    const int32_t nblk = (n_attached + 63) / 64;
+    const int32_t cb = (nblk + n_devices - 1) / n_devices;
+    for (int32_t d = 0; d < n_devices; ++d) {
+        block_begin[d] = std::min(nblk, d * cb);
+        block_end[d] = std::min(nblk, (d + 1) * cb);
+    }
+    return SPE_OK;
+}

@@ -1,11 +1,15 @@
-"""Multi-GPU sharding of the path table.
+"""Multi-GPU sharding of the path table, one process per GPU.
 
-Source rows are independent, so ranks own disjoint, contiguous runs of 64-row
-source blocks and compute them with no communication.  When a replicated table
-is wanted, every rank's SB64 block run is one contiguous span of each field, so
-one all_gather_into_tensor per field (RCCL over xGMI; gloo on CPU in tests)
-assembles the full table in place.  Equal shard sizes: the block count is
-padded to a multiple of the world size (padding blocks hold unroutable rows).
+Source rows are independent, so ranks compute disjoint sets of 64-row source
+blocks with no communication.  Two layouts:
+  * contiguous shares (rank_block_range): one run of blocks per rank, one
+    all_gather_into_tensor per field at the end (also what the in-library
+    multi-device table does, spe_device_shares);
+  * round-robin chunks (chunk_plan / rank_chunks, bench.py): the blocks are
+    dealt in rounds of world x G, one build launch per rank per round, and each
+    round's records are all-gathered IN PLACE (they are contiguous in the SB64
+    table) while the next round builds -- the gather hides behind the build.
+Equal shard sizes: the block count is padded (padding blocks are never read).
 """
 from __future__ import annotations
 
@@ -88,3 +92,36 @@ def allgather_table(shard: Dict, world: int, dist):
             dist.all_gather_into_tensor(out, xb)
         full[name] = out.view(x.dtype).reshape((-1,) + tuple(x.shape[1:]))
     return full
+
+
+def chunk_plan(nblk: int, world: int, groups: int) -> Tuple[int, int]:
+    """(rounds, G): rounds of world x G blocks, G <= groups (one build launch),
+    balanced so the padding is at most world x rounds - 1 blocks."""
+    rounds = max(1, math.ceil(nblk / (world * max(1, groups))))
+    return rounds, math.ceil(nblk / (world * rounds))
+
+
+def rank_chunks(nblk: int, world: int, rank: int, rounds: int, G: int):
+    """[(round, chunk, b0, b1)] of `rank`: chunk c = round * world + rank covers
+    blocks [c * G, (c + 1) * G) clipped to nblk (may be empty)."""
+    out = []
+    for k in range(rounds):
+        c = k * world + rank
+        out.append((k, c, min(nblk, c * G), min(nblk, (c + 1) * G)))
+    return out
+
+
+def allgather_round(lr, k: int, world: int, rank: int, chunk_elems: int, dist, async_op: bool = False):
+    """All-gather round k's records in place: rank r's chunk (k * world + r) sits
+    at element (k * world + r) * chunk_elems of `lr` on every rank, so the round
+    is one contiguous span (RCCL all_gather_into_tensor; gloo on CPU gathers a
+    list and copies back)."""
+    grp = lr[k * world * chunk_elems:(k + 1) * world * chunk_elems]
+    own = lr[(k * world + rank) * chunk_elems:(k * world + rank + 1) * chunk_elems]
+    if dist.get_backend() == "gloo":
+        parts = [p.clone() for p in grp.chunk(world)]
+        dist.all_gather(parts, own.clone())
+        for p, dst in zip(parts, grp.chunk(world)):
+            dst.copy_(p)
+        return None
+    return dist.all_gather_into_tensor(grp, own, async_op=async_op)

@@ -14,7 +14,8 @@ called at src/main/routing/shd-topology.c:371):
   * values are looked up by their exact igraph attribute name ("latency",
     "packetloss", ...: igraph_cattribute_has_attr / EAN / VAN with the
     canonical names, shd-topology.c:272-354); the reference's case-insensitive
-    prefix match (:178-267) only drives its type-check warnings.
+    prefix match (:178-267) drives its attribute TYPE checks, whose results
+    overwrite one another (check_attribute_types, :550-707).
 """
 from __future__ import annotations
 
@@ -66,6 +67,58 @@ def _attr_match(name: str, canonical: str) -> bool:
     return name == canonical
 
 
+def _attr_prefix(name: str, canonical: str) -> bool:
+    """g_ascii_strncasecmp(name, canonical, len(canonical)) == 0 (shd-topology.c:178-267)."""
+    return name is not None and name[:len(canonical)].lower() == canonical
+
+
+_VCHECK = [("id", "string"), ("ip", "string"), ("citycode", "string"), ("countrycode", "string"),
+           ("asn", "numeric"), ("type", "string"), ("bandwidthdown", "numeric"), ("bandwidthup", "numeric"),
+           ("packetloss", "numeric"), ("geocode", "string")]
+_ECHECK = [("latency", "numeric"), ("jitter", "numeric"), ("packetloss", "numeric")]
+
+
+def _igraph_type(attr_type: str) -> str:
+    t = (attr_type or "string").lower()
+    return "numeric" if t in ("int", "long", "float", "double") else ("boolean" if t == "boolean" else "string")
+
+
+def check_attribute_types(keys) -> bool:
+    """_topology_checkGraphAttributes (shd-topology.c:550-707) over the <key>
+    declarations in document order, `keys` = [(attr.name, attr.type, for)]:
+    every attribute whose name prefix-matches a known one gets a type check that
+    OVERWRITES the running result; the required-attribute checks (exact names)
+    can only clear it.  Hence only the last prefix-matched edge attribute's type
+    counts, plus the presence of "latency" and "packetloss"."""
+    def dom(f, d):
+        return f in (d, "all")
+    ok = True
+    for name, typ, f in keys:
+        if dom(f, "graph") and _attr_prefix(name, "preferdirectpaths"):
+            ok = _igraph_type(typ) == "string"
+    for name, typ, f in keys:
+        if not dom(f, "node"):
+            continue
+        for canon, want in _VCHECK:
+            if _attr_prefix(name, canon):
+                ok = _igraph_type(typ) == want
+                break
+    vnames = {n for n, _, f in keys if dom(f, "node")}
+    if "bandwidthdown" not in vnames or "bandwidthup" not in vnames:
+        ok = False
+    for name, typ, f in keys:
+        if not dom(f, "edge"):
+            continue
+        for canon, want in _ECHECK:
+            if _attr_prefix(name, canon):
+                ok = _igraph_type(typ) == want
+                break
+    enames = {n for n, _, f in keys if dom(f, "edge")}
+    if "latency" not in enames or "packetloss" not in enames:
+        ok = False
+    return ok
+
+
 def load_graphml(source: str, is_text: bool = False) -> Topology:
     """Parse a GraphML file (optionally .xz) or a GraphML string."""
     if is_text:
@@ -80,8 +133,10 @@ def load_graphml(source: str, is_text: bool = False) -> Topology:
         return el.tag.replace(GRAPHML_NS, "")
 
     keys = {}
+    key_list = []
     for k in root:
         if tag(k) == "key":
+            key_list.append((k.get("attr.name"), k.get("attr.type", "string"), k.get("for", "all")))
             default = None
             for d in k:
                 if tag(d) == "default":
@@ -138,10 +193,10 @@ def load_graphml(source: str, is_text: bool = False) -> Topology:
 
     n = len(index)
     m = len(edges)
+    if not check_attribute_types(key_list):
+        raise ValueError("topology validation failed because of problem with graph, vertex, or edge attributes")
     lat_k, lat_def = find_key("edge", "latency")
     loss_k, loss_def = find_key("edge", "packetloss")
-    if lat_k is None or loss_k is None:
-        raise ValueError("edges need latency and packetloss attributes")
     esrc = np.array([e[0] for e in edges], dtype=np.int32)
     edst = np.array([e[1] for e in edges], dtype=np.int32)
     elat = np.array([numeric(e[2].get(lat_k, lat_def)) for e in edges], dtype=np.float64)

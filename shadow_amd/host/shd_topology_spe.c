@@ -46,10 +46,39 @@ enum { VN_BWDOWN = 0, VN_BWUP, VN_PACKETLOSS, VN_ASN, VN_COUNT };
 static const char* VS_NAMES[VS_COUNT] = {"id", "ip", "citycode", "countrycode", "geocode", "type"};
 static const char* VN_NAMES[VN_COUNT] = {"bandwidthdown", "bandwidthup", "packetloss", "asn"};
 
+/* One record of the path-cache model per ORDERED vertex pair (x, y) that has an
+ * explicitly stored Path (a DIRECT or SELF store) or a packet count.  Rows stored
+ * by a source's Dijkstra run are implicit (run_seq); see "path cache model". */
+enum { K_NONE = 0, K_DIRECT, K_SELF };
 typedef struct {
-    uint64_t key;   /* (s_slot << 32 | t_slot) + 1, 0 = empty */
-    _Atomic uint64_t count;
-} PairCount;
+    uint64_t key;      /* ((uint64_t)x << 32 | y) + 1, 0 = empty */
+    uint64_t seq;      /* store sequence of an explicit entry, 0 = none */
+    uint64_t count;    /* Path.packetCount (shd-path.c:53-56) of entry (x, y) */
+    int32_t kind;      /* K_DIRECT / K_SELF when seq > 0 */
+} PairRec;
+
+#define NSHARD 64
+typedef struct {
+    pthread_mutex_t mu;
+    PairRec* tab;
+    size_t cap, size;
+} Shard;
+
+/* An immutable sealed table: published under state_lock, replaced whole (never
+ * modified) when hosts attach after sealing, and freed only after the writer
+ * lock has drained every reader that could hold it. */
+typedef struct {
+    int32_t A;
+    int32_t* slot_of_vertex;       /* [n] slot, -1 = not in this table */
+    int32_t* attached;             /* [A] slot -> vertex */
+    spe_table* table;
+    double* mlat;                  /* full host mirror [A][A], or NULL */
+    double* mrel;
+    _Atomic(double*)* blocks;      /* lazy mirror per 64-source block: lat[rows][A], rel[rows][A] */
+    _Atomic int64_t row_budget;    /* bytes left for lazy blocks; beyond it: spe_table_get */
+    pthread_mutex_t row_mu;
+    double min_latency;            /* over every routable entry */
+} Snap;
 
 struct _Topology {
     int32_t device;
@@ -57,6 +86,7 @@ struct _Topology {
     int64_t m;
     int32_t directed;
     int32_t prefer_direct;
+    int32_t complete;
     /* graph, edge list form (GraphML order) */
     int32_t *esrc, *edst;
     double *elat, *eloss;
@@ -64,38 +94,45 @@ struct _Topology {
     double* vnum[VN_COUNT];
     spe_graph* graph;
 
-    /* attachment: ip -> vertex (open addressing), vertex -> slot */
-    pthread_rwlock_t ip_lock;
+    /* state_lock guards the IP map, the attached set and the published snapshot;
+     * queries hold it shared for their whole duration, attach / publish exclusive */
+    pthread_rwlock_t state_lock;
     uint32_t* ip_keys;
     int32_t* ip_vals;
     uint8_t* ip_used;
     size_t ip_cap, ip_size;
-    int32_t* slot_of_vertex;
-    int32_t* attached;          /* slot -> vertex, in first-attach order */
+    uint8_t* is_attached;      /* [n] */
+    int32_t* attached;         /* vertices in first-attach order */
     int32_t n_attached;
+    Snap* snap;
 
-    /* sealed table (host mirror) */
-    pthread_mutex_t seal_lock;
-    _Atomic int sealed;
-    spe_table* table;
-    int32_t A;
-    double* lat;                /* [A][A] row-major */
-    double* rel;
-    double min_latency;
+    pthread_mutex_t seal_lock; /* one table build at a time */
     double build_seconds;
     int64_t build_rows;
 
-    /* per-pair packet counters (shd-path.c:53-56), lock-free insert */
-    PairCount* counts;
-    size_t counts_cap;
+    /* path cache model (shd-topology.c:1269-1371, 1952-2034): run_seq[v] = store
+     * sequence of v's first Dijkstra row run; explicit entries and packet counts
+     * in sharded maps; cache_mu serialises misses (the reference's store path) */
+    pthread_mutex_t cache_mu;
+    _Atomic uint64_t* run_seq;
+    _Atomic uint64_t seq;
+    _Atomic int64_t n_explicit;
+    Shard shards[NSHARD];
+    int32_t cache_mode;        /* TOPOLOGY_ANSWER_ROWS | TOPOLOGY_ANSWER_REFERENCE */
+    _Atomic uint64_t stored_min_bits;   /* minimumPathLatency over stored entries (reference mode) */
+    int64_t self_paths;
 
+    int32_t log_level;
     topology_log_fn log_fn;
     void* log_ctx;
     topology_min_latency_fn minlat_fn;
     void* minlat_ctx;
 };
 
+static int log_on(const Topology* top, int level) { return !top || level <= top->log_level; }
+
 static void tlog(Topology* top, int level, const char* fmt, ...) {
+    if (!log_on(top, level)) return;
     char buf[1024];
     va_list ap;
     va_start(ap, fmt);
@@ -107,13 +144,95 @@ static void tlog(Topology* top, int level, const char* fmt, ...) {
 
 /* ------------------------------------------------------------ GraphML */
 
+/* igraph attribute types of the GraphML reader: int/long/float/double -> numeric,
+ * boolean -> boolean, string (or no attr.type) -> string */
+enum { AT_STRING = 0, AT_NUMERIC, AT_BOOLEAN };
+
 typedef struct {
     char* id;
     char* name;
     int numeric;   /* attr.type int/long/float/double */
+    int atype;     /* AT_* */
     int for_;      /* 0 graph, 1 node, 2 edge, 3 all */
     char* def;
 } GKey;
+
+/* _topology_is{Graph,Vertex,Edge}AttributeKey (shd-topology.c:178-181, 235-238,
+ * 264-267): g_ascii_strncasecmp over the canonical name's length, i.e. the
+ * attribute name starts with the canonical one, case-insensitively */
+static int attr_prefix(const char* name, const char* canonical) {
+    return name && !strncasecmp(name, canonical, strlen(canonical));
+}
+
+static int key_in(const GKey* k, int domain) { return k->for_ == domain || k->for_ == 3; }
+
+static int has_exact(const GKey* keys, size_t nkeys, int domain, const char* name) {
+    for (size_t i = 0; i < nkeys; ++i)
+        if (key_in(&keys[i], domain) && keys[i].name && !strcmp(keys[i].name, name)) return 1;
+    return 0;
+}
+
+/* _topology_checkGraphAttributes, shd-topology.c:550-707.  Attributes are listed
+ * per domain in declaration order (igraph_cattribute_list).  Each one whose name
+ * prefix-matches a known attribute gets a type check whose result OVERWRITES
+ * isSuccess (:588, :605-623, :666-670) instead of AND-ing into it; the
+ * required-attribute checks (exact igraph names, :635-659, :675-690) can only
+ * clear it.  So a type error is forgiven when a later checked attribute passes,
+ * and only the last prefix-matched edge attribute's type counts in the end. */
+static int check_attribute_types(Topology* top, const GKey* keys, size_t nkeys);
+
+static const struct {
+    const char* name;
+    int type;
+} VCHECK[] = {{"id", AT_STRING},          {"ip", AT_STRING},        {"citycode", AT_STRING},
+              {"countrycode", AT_STRING}, {"asn", AT_NUMERIC},      {"type", AT_STRING},
+              {"bandwidthdown", AT_NUMERIC}, {"bandwidthup", AT_NUMERIC}, {"packetloss", AT_NUMERIC},
+              {"geocode", AT_STRING}},
+  ECHECK[] = {{"latency", AT_NUMERIC}, {"jitter", AT_NUMERIC}, {"packetloss", AT_NUMERIC}};
+
+static int type_ok(Topology* top, const GKey* k, int want) {   /* _topology_checkAttributeType */
+    if (k->atype == want) return 1;
+    tlog(top, LOG_WARNING, "attribute '%s' has an unexpected type (expected %s)", k->name,
+         want == AT_NUMERIC ? "NUMERIC" : "STRING");
+    return 0;
+}
+
+static int check_attribute_types(Topology* top, const GKey* keys, size_t nkeys) {
+    int isSuccess = 1;
+    for (size_t i = 0; i < nkeys; ++i) {   /* graph attributes */
+        if (!key_in(&keys[i], 0) || !keys[i].name) continue;
+        if (attr_prefix(keys[i].name, "preferdirectpaths")) isSuccess = type_ok(top, &keys[i], AT_STRING);
+        else tlog(top, LOG_WARNING, "graph attribute '%s' is unsupported and will be ignored", keys[i].name);
+    }
+    for (size_t i = 0; i < nkeys; ++i) {   /* vertex attributes: first matching name, in the reference's order */
+        if (!key_in(&keys[i], 1) || !keys[i].name) continue;
+        size_t a = 0;
+        while (a < sizeof VCHECK / sizeof VCHECK[0] && !attr_prefix(keys[i].name, VCHECK[a].name)) ++a;
+        if (a < sizeof VCHECK / sizeof VCHECK[0]) isSuccess = type_ok(top, &keys[i], VCHECK[a].type);
+        else tlog(top, LOG_INFO, "vertex attribute '%s' is unsupported and will be ignored", keys[i].name);
+    }
+    /* required vertex attributes ("id" is always defined: igraph stores the node ids) */
+    if (!has_exact(keys, nkeys, 1, "bandwidthdown") || !has_exact(keys, nkeys, 1, "bandwidthup")) {
+        tlog(top, LOG_WARNING, "the vertex attributes 'bandwidthdown' and 'bandwidthup' of type 'NUMERIC' are "
+                               "required but not provided");
+        isSuccess = 0;
+    }
+    for (size_t i = 0; i < nkeys; ++i) {   /* edge attributes */
+        if (!key_in(&keys[i], 2) || !keys[i].name) continue;
+        size_t a = 0;
+        while (a < sizeof ECHECK / sizeof ECHECK[0] && !attr_prefix(keys[i].name, ECHECK[a].name)) ++a;
+        if (a < sizeof ECHECK / sizeof ECHECK[0]) isSuccess = type_ok(top, &keys[i], ECHECK[a].type);
+        else tlog(top, LOG_INFO, "edge attribute '%s' is unsupported and will be ignored", keys[i].name);
+    }
+    if (!has_exact(keys, nkeys, 2, "latency") || !has_exact(keys, nkeys, 2, "packetloss")) {
+        tlog(top, LOG_WARNING, "the edge attributes 'latency' and 'packetloss' of type 'NUMERIC' are required but "
+                               "not provided");
+        isSuccess = 0;
+    }
+    if (isSuccess) tlog(top, LOG_MESSAGE, "successfully verified all graph, vertex, and edge attributes");
+    else tlog(top, LOG_WARNING, "we could not properly validate all graph, vertex, and edge attributes");
+    return isSuccess;
+}
 
 static char* xstrdup(const xmlChar* s) { return s ? strdup((const char*)s) : NULL; }
 
@@ -214,6 +333,8 @@ static int load_graphml(Topology* top, const char* path) {
             a = xmlGetProp(c, (const xmlChar*)"attr.type");
             k->numeric = a && (!xmlStrcmp(a, (const xmlChar*)"int") || !xmlStrcmp(a, (const xmlChar*)"long") ||
                                !xmlStrcmp(a, (const xmlChar*)"float") || !xmlStrcmp(a, (const xmlChar*)"double"));
+            k->atype = k->numeric ? AT_NUMERIC
+                                  : (a && !xmlStrcmp(a, (const xmlChar*)"boolean") ? AT_BOOLEAN : AT_STRING);
             xmlFree(a);
             a = xmlGetProp(c, (const xmlChar*)"for");
             k->for_ = key_for((const char*)a);
@@ -348,13 +469,10 @@ static int load_graphml(Topology* top, const char* path) {
         if (!strcmp(keys[i].name, "packetloss")) ek_loss = (int)i;
         if (!strcmp(keys[i].name, "jitter")) ek_jit = (int)i;
     }
-    /* required attributes are defined on the graph (shd-topology.c:634-690) */
-    if (vn_key[VN_BWDOWN] < 0 || vn_key[VN_BWUP] < 0) {
-        tlog(top, LOG_WARNING, "vertex attributes 'bandwidthdown' and 'bandwidthup' are required");
-        ok = 0;
-    }
-    if (ek_lat < 0 || ek_loss < 0) {
-        tlog(top, LOG_WARNING, "edge attributes 'latency' and 'packetloss' are required");
+    /* attribute names and types (shd-topology.c:550-707; the per-vertex and
+     * per-edge value checks below still need bandwidth / latency / loss values) */
+    if (!check_attribute_types(top, keys, nkeys)) {
+        tlog(top, LOG_CRITICAL, "topology validation failed because of problem with graph, vertex, or edge attributes");
         ok = 0;
     }
     size_t e = 0;
@@ -398,7 +516,11 @@ static int load_graphml(Topology* top, const char* path) {
     }
     /* _topology_checkGraphVerticesHelperHook, shd-topology.c:796-963 */
     for (int32_t v = 0; v < n && ok; ++v) {
-        if (!(top->vnum[VN_BWDOWN][v] > 0.0) || !(top->vnum[VN_BWUP][v] > 0.0)) {
+        if (!top->vnum[VN_BWDOWN] || !top->vnum[VN_BWUP]) {   /* :828-862 "is missing" */
+            tlog(top, LOG_WARNING, "required bandwidth attribute on vertex %d ('%s') is missing", v,
+                 top->vstr[VS_ID][v]);
+            ok = 0;
+        } else if (!(top->vnum[VN_BWDOWN][v] > 0.0) || !(top->vnum[VN_BWUP][v] > 0.0)) {
             tlog(top, LOG_WARNING, "required bandwidth attribute on vertex %d ('%s') is NAN or negative", v,
                  top->vstr[VS_ID][v]);
             ok = 0;
@@ -487,9 +609,24 @@ static int strongly_connected(const Topology* top) {
 
 /* --------------------------------------------------------- lifecycle */
 
+static void snap_free(Snap* s) {
+    if (!s) return;
+    if (s->table) spe_table_free(s->table);
+    if (s->blocks) {
+        for (int32_t b = 0; b < (s->A + 63) / 64; ++b) free(atomic_load(&s->blocks[b]));
+        free(s->blocks);
+    }
+    free(s->mlat);
+    free(s->mrel);
+    free(s->slot_of_vertex);
+    free(s->attached);
+    pthread_mutex_destroy(&s->row_mu);
+    free(s);
+}
+
 static void topo_release(Topology* top) {
     if (!top) return;
-    if (top->table) spe_table_free(top->table);
+    snap_free(top->snap);
     if (top->graph) spe_graph_free(top->graph);
     for (int a = 0; a < VS_COUNT; ++a)
         if (top->vstr[a]) {
@@ -499,10 +636,15 @@ static void topo_release(Topology* top) {
     for (int a = 0; a < VN_COUNT; ++a) free(top->vnum[a]);
     free(top->esrc); free(top->edst); free(top->elat); free(top->eloss);
     free(top->ip_keys); free(top->ip_vals); free(top->ip_used);
-    free(top->slot_of_vertex); free(top->attached);
-    free(top->lat); free(top->rel); free(top->counts);
-    pthread_rwlock_destroy(&top->ip_lock);
+    free(top->is_attached); free(top->attached);
+    free((void*)top->run_seq);
+    for (int i = 0; i < NSHARD; ++i) {
+        free(top->shards[i].tab);
+        pthread_mutex_destroy(&top->shards[i].mu);
+    }
+    pthread_rwlock_destroy(&top->state_lock);
     pthread_mutex_destroy(&top->seal_lock);
+    pthread_mutex_destroy(&top->cache_mu);
     free(top);
 }
 
@@ -510,8 +652,20 @@ Topology* topology_new_on_device(const char* graphPath, int32_t device) {
     if (!graphPath) return NULL;
     Topology* top = calloc(1, sizeof(Topology));
     top->device = device;
-    pthread_rwlock_init(&top->ip_lock, NULL);
+    top->log_level = LOG_MESSAGE;
+    {   /* writer preference: a table swap or an attach must not starve behind a
+         * steady stream of queries (glibc's default prefers readers) */
+        pthread_rwlockattr_t ra;
+        pthread_rwlockattr_init(&ra);
+        pthread_rwlockattr_setkind_np(&ra, PTHREAD_RWLOCK_PREFER_WRITER_NONRECURSIVE_NP);
+        pthread_rwlock_init(&top->state_lock, &ra);
+        pthread_rwlockattr_destroy(&ra);
+    }
     pthread_mutex_init(&top->seal_lock, NULL);
+    pthread_mutex_init(&top->cache_mu, NULL);
+    for (int i = 0; i < NSHARD; ++i) pthread_mutex_init(&top->shards[i].mu, NULL);
+    const char* mode = getenv("SHADOW_SPE_PATH_CACHE");
+    top->cache_mode = (mode && !strcasecmp(mode, "reference")) ? TOPOLOGY_ANSWER_REFERENCE : TOPOLOGY_ANSWER_ROWS;
     tlog(top, LOG_MESSAGE, "reading graphml topology graph at '%s'...", graphPath);
     if (!load_graphml(top, graphPath) || !strongly_connected(top)) {
         tlog(top, LOG_CRITICAL, "we failed to create the simulation topology because we were unable to "
@@ -536,6 +690,11 @@ Topology* topology_new_on_device(const char* graphPath, int32_t device) {
     }
     spe_graph_info info;
     spe_graph_info_get(top->graph, &info);
+    top->complete = info.complete;
+    if (!info.weight_floor_ok)   /* outside the bit-exactness argument */
+        tlog(top, LOG_WARNING, "some edge latency is below ulp(path latency)/2: a relaxation could leave a "
+                               "distance unchanged (fl(d + w) == d); routes are exact only when every "
+                               "fl(d + w) > d");
     tlog(top, LOG_MESSAGE, "topology graph is %s, %s, and strongly connected with 1 cluster. It does%s prefer "
                            "direct paths.", info.complete ? "complete" : "incomplete",
          top->directed ? "directed" : "undirected", top->prefer_direct ? "" : " not");
@@ -543,13 +702,30 @@ Topology* topology_new_on_device(const char* graphPath, int32_t device) {
     top->ip_keys = calloc(top->ip_cap, sizeof(uint32_t));
     top->ip_vals = calloc(top->ip_cap, sizeof(int32_t));
     top->ip_used = calloc(top->ip_cap, 1);
-    top->slot_of_vertex = malloc(((size_t)top->n + 1) * sizeof(int32_t));
-    for (int32_t v = 0; v < top->n; ++v) top->slot_of_vertex[v] = -1;
+    top->is_attached = calloc((size_t)top->n + 1, 1);
     top->attached = malloc(((size_t)top->n + 1) * sizeof(int32_t));
+    top->run_seq = calloc((size_t)top->n + 1, sizeof(uint64_t));
     return top;
 }
 
-Topology* topology_new(const char* graphPath) { return topology_new_on_device(graphPath, 0); }
+int32_t topology_check_graphml(const char* graphPath) {
+    if (!graphPath) return 0;
+    Topology* top = calloc(1, sizeof(Topology));
+    top->log_level = LOG_WARNING;
+    pthread_rwlock_init(&top->state_lock, NULL);
+    pthread_mutex_init(&top->seal_lock, NULL);
+    pthread_mutex_init(&top->cache_mu, NULL);
+    for (int i = 0; i < NSHARD; ++i) pthread_mutex_init(&top->shards[i].mu, NULL);
+    const int ok = load_graphml(top, graphPath) && strongly_connected(top);
+    topo_release(top);
+    return ok ? 1 : 0;
+}
+
+Topology* topology_new(const char* graphPath) {
+    /* SHADOW_SPE_DEVICE=<index>: the GPU to build on (default 0) */
+    const char* dev = getenv("SHADOW_SPE_DEVICE");
+    return topology_new_on_device(graphPath, dev && *dev ? atoi(dev) : 0);
+}
 
 void topology_set_log_callback(Topology* top, topology_log_fn fn, void* ctx) {
     if (!top) return;
@@ -557,10 +733,20 @@ void topology_set_log_callback(Topology* top, topology_log_fn fn, void* ctx) {
     top->log_ctx = ctx;
 }
 
+void topology_set_log_level(Topology* top, int32_t level) {
+    if (top) top->log_level = level;
+}
+
 void topology_set_min_latency_callback(Topology* top, topology_min_latency_fn fn, void* ctx) {
     if (!top) return;
     top->minlat_fn = fn;
     top->minlat_ctx = ctx;
+}
+
+int32_t topology_set_answer_mode(Topology* top, int32_t mode) {
+    if (!top || (mode != TOPOLOGY_ANSWER_ROWS && mode != TOPOLOGY_ANSWER_REFERENCE)) return SPE_EINVAL;
+    top->cache_mode = mode;
+    return SPE_OK;
 }
 
 int32_t topology_vertex_count(const Topology* top) { return top ? top->n : 0; }
@@ -621,14 +807,6 @@ static void ip_del(Topology* top, uint32_t ip) {
         }
         j = (j + 1) & (top->ip_cap - 1);
     }
-}
-
-int32_t topology_attached_vertex(const Topology* top, spe_in_addr_t address) {
-    if (!top) return -1;
-    pthread_rwlock_rdlock((pthread_rwlock_t*)&top->ip_lock);
-    const int32_t v = ip_get((Topology*)top, address);
-    pthread_rwlock_unlock((pthread_rwlock_t*)&top->ip_lock);
-    return v;
 }
 
 /* ---------------------------------------------------------- attachment */
@@ -750,14 +928,16 @@ void topology_attach(Topology* top, spe_in_addr_t address, topology_random_fn ra
         tlog(top, LOG_CRITICAL, "unable to find an attachment vertex");
         return;
     }
-    pthread_rwlock_wrlock(&top->ip_lock);
+    /* A new vertex only joins the attached set here; a sealed table stays
+     * published (it answers every pair it holds) until the next query that needs
+     * the new vertex builds and publishes a replacement. */
+    pthread_rwlock_wrlock(&top->state_lock);
     ip_put(top, address, v);
-    if (top->slot_of_vertex[v] < 0) {
-        top->slot_of_vertex[v] = top->n_attached;
+    if (!top->is_attached[v]) {
+        top->is_attached[v] = 1;
         top->attached[top->n_attached++] = v;
-        if (atomic_load(&top->sealed)) atomic_store(&top->sealed, 0);   /* A grew: rebuild on next query */
     }
-    pthread_rwlock_unlock(&top->ip_lock);
+    pthread_rwlock_unlock(&top->state_lock);
     if (bwUpOut) *bwUpOut = (uint64_t)top->vnum[VN_BWUP][v];
     if (bwDownOut) *bwDownOut = (uint64_t)top->vnum[VN_BWDOWN][v];
     struct in_addr a = {address};
@@ -766,9 +946,17 @@ void topology_attach(Topology* top, spe_in_addr_t address, topology_random_fn ra
 
 void topology_detach(Topology* top, spe_in_addr_t address) {
     if (!top) return;
-    pthread_rwlock_wrlock(&top->ip_lock);
+    pthread_rwlock_wrlock(&top->state_lock);
     ip_del(top, address);   /* the vertex stays in A, like the reference (:2415-2421) */
-    pthread_rwlock_unlock(&top->ip_lock);
+    pthread_rwlock_unlock(&top->state_lock);
+}
+
+int32_t topology_attached_vertex(const Topology* top, spe_in_addr_t address) {
+    if (!top) return -1;
+    pthread_rwlock_rdlock((pthread_rwlock_t*)&top->state_lock);
+    const int32_t v = ip_get((Topology*)top, address);
+    pthread_rwlock_unlock((pthread_rwlock_t*)&top->state_lock);
+    return v;
 }
 
 /* -------------------------------------------------------------- sealing */
@@ -779,201 +967,566 @@ static double now_s(void) {
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
+static int64_t env_bytes(const char* name, int64_t dflt) {
+    const char* s = getenv(name);
+    return (s && *s) ? (int64_t)strtoll(s, NULL, 10) : dflt;
+}
+
+/* Build a table over `att` (A vertices) and its host-side view. */
+static int snap_build(Topology* top, const int32_t* att_in, int32_t A, Snap** out) {
+    *out = NULL;
+    Snap* s = calloc(1, sizeof(Snap));
+    pthread_mutex_init(&s->row_mu, NULL);
+    s->A = A;
+    s->attached = malloc(((size_t)A + 1) * sizeof(int32_t));
+    s->slot_of_vertex = malloc(((size_t)top->n + 1) * sizeof(int32_t));
+    for (int32_t v = 0; v < top->n; ++v) s->slot_of_vertex[v] = -1;
+    /* slots are internal (queries resolve IP -> vertex -> slot): number them in
+     * the engine's source-clustering order (spe_order_sources) */
+    if (spe_order_sources(top->graph, att_in, A, s->attached) != SPE_OK)
+        memcpy(s->attached, att_in, (size_t)A * sizeof(int32_t));
+    for (int32_t i = 0; i < A; ++i) s->slot_of_vertex[s->attached[i]] = i;
+    spe_table_opts o;
+    memset(&o, 0, sizeof o);
+    o.self_mode = SPE_SELF_ROW;
+    /* SHADOW_SPE_DEVICES=0,1,...: build on several GPUs of this node (one share of
+     * the sources each, then an all-gather of the records, spe_table_opts.devices) */
+    int32_t devs[64];
+    int32_t ndev = 0;
+    const char* dl = getenv("SHADOW_SPE_DEVICES");
+    for (const char* p = dl; p && *p && ndev < 64;) {
+        char* end = NULL;
+        const long d = strtol(p, &end, 10);
+        if (end == p) break;
+        devs[ndev++] = (int32_t)d;
+        p = (*end == ',') ? end + 1 : end;
+    }
+    if (ndev > 1) {
+        o.devices = devs;
+        o.n_devices = ndev;
+    }
+    int rc = spe_table_create(top->graph, s->attached, A, &o, &s->table);
+    /* SHADOW_SPE_TABLE_CACHE=<dir>: reuse the rows of an earlier run on the same
+     * graph / hosts (keyed file), else build and save them */
+    const char* cdir = getenv("SHADOW_SPE_TABLE_CACHE");
+    char cpath[4096] = {0};
+    int loaded = 0;
+    if (rc == SPE_OK && cdir && *cdir && ndev <= 1) {   /* the cache holds single-device tables */
+        uint64_t key = 0;
+        spe_table_key(s->table, &key);
+        snprintf(cpath, sizeof cpath, "%s/spe-table-%016llx.bin", cdir, (unsigned long long)key);
+        loaded = spe_table_load(s->table, cpath) == SPE_OK;
+        tlog(top, LOG_MESSAGE, "path table cache %s: %s", loaded ? "hit" : "miss", cpath);
+    }
+    if (rc == SPE_OK && !loaded) {
+        rc = spe_table_build(s->table, NULL);
+        if (rc == SPE_OK && cpath[0] && spe_table_save(s->table, cpath) != SPE_OK)
+            tlog(top, LOG_WARNING, "could not save the path table cache: %s", spe_last_error());
+    }
+    /* host view: the whole table when it fits SHADOW_SPE_MIRROR_BYTES (default
+     * 8 GiB: A <= 23k), else 64-source blocks mirrored on first use within that
+     * budget, then single-entry device reads (spe_table_get) */
+    const int64_t budget = env_bytes("SHADOW_SPE_MIRROR_BYTES", (int64_t)8 << 30);
+    const int64_t full = (int64_t)A * A * 16;
+    if (rc == SPE_OK && full <= budget) {
+        s->mlat = malloc((size_t)A * A * sizeof(double));
+        s->mrel = malloc((size_t)A * A * sizeof(double));
+        if (!s->mlat || !s->mrel) rc = SPE_ENOMEM;
+        else rc = spe_table_download(s->table, 0, A, s->mlat, s->mrel, NULL, NULL);
+    } else if (rc == SPE_OK) {
+        s->blocks = calloc((size_t)(A + 63) / 64, sizeof(*s->blocks));
+        atomic_store(&s->row_budget, budget);
+        if (!s->blocks) rc = SPE_ENOMEM;
+    }
+    if (rc == SPE_OK) rc = spe_table_min_latency(s->table, &s->min_latency);
+    if (rc != SPE_OK) {
+        tlog(top, LOG_CRITICAL, "path table build failed: %s", spe_last_error());
+        snap_free(s);
+        return rc;
+    }
+    *out = s;
+    return SPE_OK;
+}
+
 int32_t topology_seal(Topology* top) {
     if (!top) return SPE_EINVAL;
-    if (atomic_load_explicit(&top->sealed, memory_order_acquire)) return SPE_OK;
     pthread_mutex_lock(&top->seal_lock);
+    pthread_rwlock_rdlock(&top->state_lock);
+    const int32_t A = top->n_attached;
+    const int fresh = top->snap && top->snap->A == A;   /* A only grows */
+    int32_t* att = fresh ? NULL : malloc(((size_t)A + 1) * sizeof(int32_t));
+    if (att) memcpy(att, top->attached, (size_t)A * sizeof(int32_t));
+    pthread_rwlock_unlock(&top->state_lock);
     int rc = SPE_OK;
-    if (!atomic_load(&top->sealed)) {
-        pthread_rwlock_rdlock(&top->ip_lock);
-        const int32_t A = top->n_attached;
-        int32_t* att = malloc(((size_t)A + 1) * sizeof(int32_t));
-        memcpy(att, top->attached, (size_t)A * sizeof(int32_t));
-        pthread_rwlock_unlock(&top->ip_lock);
-        if (top->table) {
-            spe_table_free(top->table);
-            top->table = NULL;
-        }
+    if (!fresh) {
+        Snap* s = NULL;
         if (A == 0) {
             rc = SPE_ESTATE;
         } else {
             const double t0 = now_s();
-            /* slots are internal (queries resolve IP -> vertex -> slot): number them
-             * in the engine's source-clustering order (spe_order_sources) */
-            int32_t* ord = malloc(((size_t)A + 1) * sizeof(int32_t));
-            if (ord && spe_order_sources(top->graph, att, A, ord) == SPE_OK) {
-                pthread_rwlock_wrlock(&top->ip_lock);
-                for (int32_t i = 0; i < A; ++i) {
-                    top->attached[i] = ord[i];
-                    top->slot_of_vertex[ord[i]] = i;
-                }
-                pthread_rwlock_unlock(&top->ip_lock);
-                free(att);
-                att = ord;
-            } else {
-                free(ord);
-            }
-            spe_table_opts o;
-            memset(&o, 0, sizeof o);
-            o.self_mode = SPE_SELF_ROW;
-            rc = spe_table_create(top->graph, att, A, &o, &top->table);
-            /* SHADOW_SPE_TABLE_CACHE=<dir>: reuse the rows of an earlier run on the
-             * same graph / hosts (keyed file), else build and save them */
-            const char* cdir = getenv("SHADOW_SPE_TABLE_CACHE");
-            char cpath[4096] = {0};
-            int loaded = 0;
-            if (rc == SPE_OK && cdir && *cdir) {
-                uint64_t key = 0;
-                spe_table_key(top->table, &key);
-                snprintf(cpath, sizeof cpath, "%s/spe-table-%016llx.bin", cdir, (unsigned long long)key);
-                loaded = spe_table_load(top->table, cpath) == SPE_OK;
-                tlog(top, LOG_MESSAGE, "path table cache %s: %s", loaded ? "hit" : "miss", cpath);
-            }
-            if (rc == SPE_OK && !loaded) {
-                rc = spe_table_build(top->table, NULL);
-                if (rc == SPE_OK && cpath[0] && spe_table_save(top->table, cpath) != SPE_OK)
-                    tlog(top, LOG_WARNING, "could not save the path table cache: %s", spe_last_error());
-            }
+            rc = snap_build(top, att, A, &s);   /* no lock held: queries on the old table go on */
             if (rc == SPE_OK) {
-                free(top->lat);
-                free(top->rel);
-                top->lat = malloc((size_t)A * A * sizeof(double));
-                top->rel = malloc((size_t)A * A * sizeof(double));
-                if (!top->lat || !top->rel) rc = SPE_ENOMEM;
-                else rc = spe_table_download(top->table, 0, A, top->lat, top->rel, NULL, NULL);
-            }
-            if (rc == SPE_OK) rc = spe_table_min_latency(top->table, &top->min_latency);
-            if (rc == SPE_OK) {
-                top->A = A;
                 top->build_seconds += now_s() - t0;
                 top->build_rows += A;
-                free(top->counts);
-                top->counts_cap = 1024;
-                while (top->counts_cap < (size_t)A * 4) top->counts_cap *= 2;
-                top->counts = calloc(top->counts_cap, sizeof(PairCount));
             }
         }
-        free(att);
         if (rc == SPE_OK) {
-            atomic_store_explicit(&top->sealed, 1, memory_order_release);
-            /* worker_updateMinTimeJump(minimumPathLatency), shd-topology.c:1359-1370: runs on the
+            pthread_rwlock_wrlock(&top->state_lock);   /* drains every reader of the old table */
+            Snap* old = top->snap;
+            top->snap = s;
+            pthread_rwlock_unlock(&top->state_lock);
+            snap_free(old);
+            /* worker_updateMinTimeJump(minimumPathLatency), shd-topology.c:1359-1370: on the
              * querying (worker) thread, as the reference requires */
-            if (top->minlat_fn && top->min_latency > 0) top->minlat_fn(top->min_latency, top->minlat_ctx);
-        } else {
-            tlog(top, LOG_CRITICAL, "path table build failed: %s", spe_last_error());
+            if (top->cache_mode == TOPOLOGY_ANSWER_ROWS && top->minlat_fn && s->min_latency > 0)
+                top->minlat_fn(s->min_latency, top->minlat_ctx);
         }
     }
+    free(att);
     pthread_mutex_unlock(&top->seal_lock);
     return rc;
 }
 
-/* slots of a pair, -1 when an address is not attached */
-static int pair_slots(Topology* top, uint32_t src, uint32_t dst, int32_t* s, int32_t* t) {
-    pthread_rwlock_rdlock(&top->ip_lock);
-    const int32_t sv = ip_get(top, src), dv = ip_get(top, dst);
-    pthread_rwlock_unlock(&top->ip_lock);
-    if (sv < 0 || dv < 0) {
-        struct in_addr a = {sv < 0 ? src : dst};
-        tlog(top, LOG_CRITICAL, "invalid vertex, address %s is not connected to topology", inet_ntoa(a));
-        return 0;
+/* Latency and reliability of table entry (s, t) of a published snapshot; the
+ * caller holds state_lock shared. */
+static void snap_value(Topology* top, Snap* sn, int32_t s, int32_t t, double* lat, double* rel) {
+    const int32_t A = sn->A;
+    if (sn->mlat) {
+        *lat = sn->mlat[(size_t)s * A + t];
+        *rel = sn->mrel[(size_t)s * A + t];
+        return;
     }
-    /* sealing numbers the slots (spe_order_sources): resolve them afterwards */
-    if (topology_seal(top) != SPE_OK) return 0;
-    pthread_rwlock_rdlock(&top->ip_lock);
-    *s = top->slot_of_vertex[sv];
-    *t = top->slot_of_vertex[dv];
-    pthread_rwlock_unlock(&top->ip_lock);
-    return *s >= 0 && *t >= 0;
+    const int32_t b = s / 64, r0 = b * 64, nr = (A - r0) < 64 ? A - r0 : 64;
+    const int64_t bytes = (int64_t)nr * A * 16;
+    double* blk = atomic_load_explicit(&sn->blocks[b], memory_order_acquire);
+    if (!blk) {
+        pthread_mutex_lock(&sn->row_mu);
+        blk = atomic_load_explicit(&sn->blocks[b], memory_order_acquire);
+        if (!blk && atomic_load(&sn->row_budget) >= bytes) {
+            blk = malloc((size_t)bytes);
+            if (blk && spe_table_download(sn->table, r0, r0 + nr, blk, blk + (size_t)nr * A, NULL, NULL) == SPE_OK) {
+                atomic_fetch_sub(&sn->row_budget, bytes);
+                atomic_store_explicit(&sn->blocks[b], blk, memory_order_release);
+            } else {
+                free(blk);
+                blk = NULL;
+            }
+        }
+        pthread_mutex_unlock(&sn->row_mu);
+    }
+    if (blk) {
+        *lat = blk[(size_t)(s - r0) * A + t];
+        *rel = blk[((size_t)nr + (s - r0)) * A + t];
+        return;
+    }
+    spe_entry e;
+    if (spe_table_get(sn->table, s, t, &e) == SPE_OK) {
+        *lat = e.latency;
+        *rel = e.reliability;
+    } else {
+        tlog(top, LOG_CRITICAL, "path table read failed: %s", spe_last_error());
+        *lat = *rel = -1.0;
+    }
+}
+
+/* ------------------------------------------------------ path cache model
+ *
+ * The reference caches a Path per ORDERED vertex pair (x, y) and answers a
+ * query (s, t) with entry (s, t), else -- undirected graphs -- (t, s); on a miss
+ * it stores entries and looks up (s, t), then (t, s) whatever the direction
+ * (_topology_getPathEntry, shd-topology.c:1952-2034).  Stores
+ * (_topology_shouldStorePath :1292-1321) never overwrite either direction of a
+ * pair and keep non-direct paths out of complete graphs and off adjacent pairs
+ * of prefer-direct graphs.  What a miss stores:
+ *   DIRECT regime (complete, or preferdirectpaths and an s -> t edge): the
+ *     single entry (s, t) (_topology_lookupDirectPath :1862-1912);
+ *   s == t otherwise: the SELF entry (s, s) (:1530-1638);
+ *   else s's Dijkstra row: (s, y) for every attached y (:1640-1860).
+ * The model keeps explicit DIRECT / SELF entries in the shard maps and a row run
+ * as one sequence number per source (run_seq), from which "was (x, y) stored by
+ * x's row" follows: the row ran, the pair is storable, and neither direction
+ * was stored before it.  The graph is one strong component, so every x != y
+ * path exists; the row's own [x] path needs x's self-loop (quirk B5). */
+
+static Shard* shard_of(Topology* top, uint64_t key) {
+    return &top->shards[(key * 0x9E3779B97F4A7C15ull) >> 58];
+}
+
+/* the record of (x, y) in its locked shard, inserted when `insert` */
+static PairRec* rec_locked(Shard* sh, uint64_t key, int insert) {
+    if (insert && (sh->size + 1) * 2 > sh->cap) {
+        const size_t nc = sh->cap ? sh->cap * 2 : 256;
+        PairRec* nt = calloc(nc, sizeof(PairRec));
+        for (size_t i = 0; i < sh->cap; ++i)
+            if (sh->tab[i].key) {
+                size_t j = (size_t)(sh->tab[i].key * 0xD6E8FEB86659FD93ull) & (nc - 1);
+                while (nt[j].key) j = (j + 1) & (nc - 1);
+                nt[j] = sh->tab[i];
+            }
+        free(sh->tab);
+        sh->tab = nt;
+        sh->cap = nc;
+    }
+    if (!sh->cap) return NULL;
+    size_t j = (size_t)(key * 0xD6E8FEB86659FD93ull) & (sh->cap - 1);
+    while (sh->tab[j].key) {
+        if (sh->tab[j].key == key) return &sh->tab[j];
+        j = (j + 1) & (sh->cap - 1);
+    }
+    if (!insert) return NULL;
+    sh->tab[j].key = key;
+    sh->size++;
+    return &sh->tab[j];
+}
+
+static uint64_t pair_key(int32_t x, int32_t y) { return (((uint64_t)(uint32_t)x << 32) | (uint32_t)y) + 1; }
+
+/* explicit entry (x, y): its store sequence (0 = none) and kind */
+static uint64_t explicit_seq(Topology* top, int32_t x, int32_t y, int32_t* kind) {
+    if (atomic_load_explicit(&top->n_explicit, memory_order_acquire) == 0) return 0;
+    const uint64_t key = pair_key(x, y);
+    Shard* sh = shard_of(top, key);
+    pthread_mutex_lock(&sh->mu);
+    const PairRec* r = rec_locked(sh, key, 0);
+    const uint64_t s = r ? r->seq : 0;
+    if (kind) *kind = r ? r->kind : K_NONE;
+    pthread_mutex_unlock(&sh->mu);
+    return s;
+}
+
+static void explicit_store(Topology* top, int32_t x, int32_t y, int32_t kind, uint64_t seq) {
+    const uint64_t key = pair_key(x, y);
+    Shard* sh = shard_of(top, key);
+    pthread_mutex_lock(&sh->mu);
+    PairRec* r = rec_locked(sh, key, 1);
+    if (!r->seq) {
+        r->seq = seq;
+        r->kind = kind;
+        atomic_fetch_add_explicit(&top->n_explicit, 1, memory_order_release);
+    }
+    pthread_mutex_unlock(&sh->mu);
+}
+
+static uint64_t pair_count(Topology* top, int32_t x, int32_t y, uint64_t add) {
+    const uint64_t key = pair_key(x, y);
+    Shard* sh = shard_of(top, key);
+    pthread_mutex_lock(&sh->mu);
+    PairRec* r = rec_locked(sh, key, add != 0);
+    uint64_t c = 0;
+    if (r) c = (r->count += add);
+    pthread_mutex_unlock(&sh->mu);
+    return c;
+}
+
+static int adjacent(Topology* top, int32_t x, int32_t y) {
+    int32_t a = 0;
+    return spe_graph_adjacent(top->graph, x, y, &a) == SPE_OK && a;
+}
+
+static int direct_regime(Topology* top, int32_t s, int32_t t) {   /* :2002 */
+    return top->complete || (top->prefer_direct && adjacent(top, s, t));
+}
+
+/* would x's Dijkstra row, run at sequence rx, store entry (x, y)?  `other` is
+ * the run sequence of y's row (0 = none, or ignored when not earlier). */
+static int row_stores(Topology* top, int32_t x, int32_t y, uint64_t rx, uint64_t ry) {
+    if (top->complete) return 0;                                /* complete && !direct */
+    if (top->prefer_direct && adjacent(top, x, y)) return 0;    /* a direct path exists */
+    if (x == y) return adjacent(top, x, x);                     /* the [x] path needs the self-loop */
+    int32_t k;
+    const uint64_t ex = explicit_seq(top, x, y, &k), ey = explicit_seq(top, y, x, &k);
+    if ((ex && ex < rx) || (ey && ey < rx)) return 0;           /* a direction already cached */
+    if (ry && ry < rx && row_stores(top, y, x, ry, 0)) return 0;
+    return 1;
+}
+
+/* store sequence of entry (x, y), 0 = not in the cache; *kind = K_DIRECT /
+ * K_SELF for an explicit entry, K_NONE for a row entry */
+static uint64_t entry_seq(Topology* top, int32_t x, int32_t y, int32_t* kind) {
+    int32_t k = K_NONE;
+    const uint64_t e = explicit_seq(top, x, y, &k);
+    if (e) {
+        if (kind) *kind = k;
+        return e;
+    }
+    if (kind) *kind = K_NONE;
+    const uint64_t rx = atomic_load_explicit(&top->run_seq[x], memory_order_acquire);
+    if (!rx) return 0;
+    const uint64_t ry = x == y ? 0 : atomic_load_explicit(&top->run_seq[y], memory_order_acquire);
+    return row_stores(top, x, y, rx, ry) ? rx : 0;
+}
+
+static int find_entry(Topology* top, int32_t s, int32_t t, int reverse, int32_t* x, int32_t* y, int32_t* kind) {
+    if (entry_seq(top, s, t, kind)) {
+        *x = s;
+        *y = t;
+        return 1;
+    }
+    if (reverse && entry_seq(top, t, s, kind)) {
+        *x = t;
+        *y = s;
+        return 1;
+    }
+    return 0;
+}
+
+static void note_min(Topology* top, double lat, int* updated) {   /* minimumPathLatency, :1359-1367 */
+    if (!(lat > 0)) return;
+    uint64_t cur = atomic_load(&top->stored_min_bits);
+    uint64_t bits;
+    memcpy(&bits, &lat, sizeof bits);
+    while (cur == 0 || bits < cur) {   /* positive doubles order as integers */
+        if (atomic_compare_exchange_weak(&top->stored_min_bits, &cur, bits)) {
+            *updated = 1;
+            break;
+        }
+    }
+}
+
+/* The per-path lines of _topology_computeSourcePaths (:1809-1829): info for
+ * the requested target, debug for the others.  The reference's path string
+ * lists every hop; the table keeps the first hop and the hop count. */
+static void log_row(Topology* top, Snap* sn, int32_t s, int32_t want) {
+    if (!log_on(top, LOG_INFO)) return;
+    const int32_t ss = sn->slot_of_vertex[s];
+    for (int32_t j = 0; j < sn->A; ++j) {
+        const int32_t t = sn->attached[j];
+        const int lvl = t == want ? LOG_INFO : LOG_DEBUG;
+        if (!log_on(top, lvl)) continue;
+        spe_entry e;
+        if (spe_table_get(sn->table, ss, j, &e) != SPE_OK || e.latency <= -1.0) continue;
+        tlog(top, lvl, "shortest path %s%s%s (%d%s%d) is %f ms with %f loss, path: first hop %s, %d hops",
+             top->vstr[VS_ID][s], top->directed ? "-->" : "<-->", top->vstr[VS_ID][t], s,
+             top->directed ? "-->" : "<-->", t, e.latency, 1 - e.reliability,
+             e.next_hop >= 0 ? top->vstr[VS_ID][e.next_hop] : "-", e.hops);
+    }
+}
+
+/* _topology_getPathEntry on the model: the cached entry (x, y) answering (s, t);
+ * stores on a miss.  Returns 0 when the reference's lookup finds no path. */
+static int cache_lookup(Topology* top, Snap* sn, int32_t s, int32_t t, int32_t* x, int32_t* y, int32_t* kind,
+                        int* min_updated) {
+    if (find_entry(top, s, t, !top->directed, x, y, kind)) return 1;
+    pthread_mutex_lock(&top->cache_mu);
+    int found = find_entry(top, s, t, !top->directed, x, y, kind);
+    int success = 1;
+    if (!found) {
+        const int ref = top->cache_mode == TOPOLOGY_ANSWER_REFERENCE;
+        if (direct_regime(top, s, t)) {
+            success = adjacent(top, s, t);   /* get_eid(s, t) must find the edge */
+            if (success && !entry_seq(top, s, t, NULL) && !entry_seq(top, t, s, NULL)) {
+                explicit_store(top, s, t, K_DIRECT, atomic_fetch_add(&top->seq, 1) + 1);
+                if (ref) {
+                    double l, r;
+                    snap_value(top, sn, sn->slot_of_vertex[s], sn->slot_of_vertex[t], &l, &r);
+                    note_min(top, l, min_updated);
+                }
+            }
+        } else if (s == t) {
+            spe_entry e;
+            success = spe_graph_self_path(top->graph, s, &e) == SPE_OK && e.hops > 0;
+            if (success && !entry_seq(top, s, s, NULL)) {
+                explicit_store(top, s, s, K_SELF, atomic_fetch_add(&top->seq, 1) + 1);
+                top->self_paths++;
+                if (ref) note_min(top, e.latency, min_updated);
+            }
+        } else {
+            /* the row run stores what it may; a re-run (directed graphs) stores nothing new */
+            if (!atomic_load(&top->run_seq[s])) {
+                const uint64_t rs = atomic_fetch_add(&top->seq, 1) + 1;
+                atomic_store_explicit(&top->run_seq[s], rs, memory_order_release);
+                log_row(top, sn, s, t);
+                if (ref) {
+                    const int32_t ss = sn->slot_of_vertex[s];
+                    for (int32_t j = 0; j < sn->A; ++j)
+                        if (entry_seq(top, s, sn->attached[j], NULL) == rs) {
+                            double l, r;
+                            snap_value(top, sn, ss, j, &l, &r);
+                            note_min(top, l, min_updated);
+                        }
+                }
+            }
+            success = adjacent(top, s, s);   /* quirk B5: the row's [s] path fails without a self-loop */
+        }
+        if (success) found = find_entry(top, s, t, 1, x, y, kind);
+    }
+    pthread_mutex_unlock(&top->cache_mu);
+    return found;
+}
+
+/* One query: resolve both addresses, publish a table that holds them if none
+ * does yet, run the cache model, read the answer.  count_add > 0 increments the
+ * packet counter of the answering entry (topology_incrementPathPacketCounter). */
+static int query(Topology* top, uint32_t src, uint32_t dst, uint64_t count_add, double* lat, double* rel,
+                 uint64_t* count_out) {
+    *lat = *rel = -1.0;
+    if (!top) return 0;
+    for (int attempt = 0; attempt < 64; ++attempt) {   /* hosts may keep attaching meanwhile */
+        pthread_rwlock_rdlock(&top->state_lock);
+        const int32_t sv = ip_get(top, src), dv = ip_get(top, dst);
+        if (sv < 0 || dv < 0) {
+            pthread_rwlock_unlock(&top->state_lock);
+            struct in_addr a = {sv < 0 ? src : dst};
+            tlog(top, LOG_CRITICAL, "invalid vertex, %s address %s is not connected to topology",
+                 sv < 0 ? "source" : "destination", inet_ntoa(a));
+            return 0;
+        }
+        Snap* sn = top->snap;
+        if (sn && sn->slot_of_vertex[sv] >= 0 && sn->slot_of_vertex[dv] >= 0) {
+            int32_t x, y, kind = K_NONE;
+            int min_updated = 0;
+            const int found = cache_lookup(top, sn, sv, dv, &x, &y, &kind, &min_updated);
+            int ok = 1;
+            if (top->cache_mode == TOPOLOGY_ANSWER_REFERENCE) {
+                if (!found) {
+                    ok = 0;
+                } else if (kind == K_SELF) {
+                    spe_entry e;
+                    spe_graph_self_path(top->graph, x, &e);
+                    *lat = e.latency;
+                    *rel = e.reliability;
+                } else {
+                    snap_value(top, sn, sn->slot_of_vertex[x], sn->slot_of_vertex[y], lat, rel);
+                }
+            } else {
+                snap_value(top, sn, sn->slot_of_vertex[sv], sn->slot_of_vertex[dv], lat, rel);
+            }
+            if (found && (count_add || count_out)) {
+                const uint64_t c = pair_count(top, x, y, count_add);
+                if (count_out) *count_out = c;
+            }
+            pthread_rwlock_unlock(&top->state_lock);
+            if (!found && top->cache_mode == TOPOLOGY_ANSWER_REFERENCE) {   /* :2023-2029 */
+                tlog(top, LOG_ERROR, "unable to find path between vertex %d (%s) and vertex %d (%s)", sv,
+                     top->vstr[VS_ID][sv], dv, top->vstr[VS_ID][dv]);
+            }
+            if (min_updated && top->minlat_fn) {   /* worker_updateMinTimeJump, :1369 */
+                double m;
+                const uint64_t b = atomic_load(&top->stored_min_bits);
+                memcpy(&m, &b, sizeof m);
+                top->minlat_fn(m, top->minlat_ctx);
+            }
+            return ok && *lat > -1.0;
+        }
+        pthread_rwlock_unlock(&top->state_lock);
+        if (topology_seal(top) != SPE_OK) return 0;
+    }
+    return 0;
 }
 
 double topology_getLatency(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {
-    int32_t s, t;
-    if (!top || !pair_slots(top, srcAddress, dstAddress, &s, &t)) return -1.0;
-    return top->lat[(size_t)s * top->A + t];
+    double l, r;
+    query(top, srcAddress, dstAddress, 0, &l, &r, NULL);
+    return l;
 }
 
 double topology_getReliability(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {
-    int32_t s, t;
-    if (!top || !pair_slots(top, srcAddress, dstAddress, &s, &t)) return -1.0;
-    return top->rel[(size_t)s * top->A + t];
+    double l, r;
+    query(top, srcAddress, dstAddress, 0, &l, &r, NULL);
+    return r;
 }
 
 int32_t topology_getPathInfo(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress, double* latency,
                              double* reliability) {
-    int32_t s, t;
-    double L = -1.0, R = -1.0;
-    if (top && pair_slots(top, srcAddress, dstAddress, &s, &t)) {
-        const size_t o = (size_t)s * top->A + t;
-        L = top->lat[o];
-        R = top->rel[o];
-    }
-    if (latency) *latency = L;
-    if (reliability) *reliability = R;
-    return L > -1 ? 1 : 0;
+    double l, r;
+    const int ok = query(top, srcAddress, dstAddress, 0, &l, &r, NULL);
+    if (latency) *latency = l;
+    if (reliability) *reliability = r;
+    return ok;
 }
 
 int32_t topology_isRoutable(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {
     return topology_getLatency(top, srcAddress, dstAddress) > -1 ? 1 : 0;   /* :2072-2075 */
 }
 
-static PairCount* count_slot(Topology* top, int32_t s, int32_t t, int insert) {
-    const uint64_t key = (((uint64_t)(uint32_t)s << 32) | (uint32_t)t) + 1;
-    size_t j = (size_t)(key * 0x9E3779B97F4A7C15ull) & (top->counts_cap - 1);
-    for (size_t probe = 0; probe < top->counts_cap; ++probe) {
-        uint64_t cur = __atomic_load_n(&top->counts[j].key, __ATOMIC_ACQUIRE);
-        if (cur == key) return &top->counts[j];
-        if (cur == 0) {
-            if (!insert) return NULL;
-            uint64_t expect = 0;
-            if (__atomic_compare_exchange_n(&top->counts[j].key, &expect, key, 0, __ATOMIC_ACQ_REL,
-                                            __ATOMIC_ACQUIRE))
-                return &top->counts[j];
-            if (expect == key) return &top->counts[j];
-        }
-        j = (j + 1) & (top->counts_cap - 1);
-    }
-    return NULL;
-}
-
 void topology_incrementPathPacketCounter(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {
-    int32_t s, t;
-    if (!top || !pair_slots(top, srcAddress, dstAddress, &s, &t)) {
-        if (top) tlog(top, LOG_ERROR, "unable to find path for packet counter");
-        return;
-    }
-    PairCount* pc = count_slot(top, s, t, 1);
-    if (pc) atomic_fetch_add_explicit(&pc->count, 1, memory_order_relaxed);
+    double l, r;
+    query(top, srcAddress, dstAddress, 1, &l, &r, NULL);   /* path->packetCount++, shd-path.c:53-56 */
 }
 
 uint64_t topology_path_packet_count(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {
-    int32_t s, t;
-    if (!top || !pair_slots(top, srcAddress, dstAddress, &s, &t)) return 0;
-    PairCount* pc = count_slot(top, s, t, 0);
-    return pc ? atomic_load(&pc->count) : 0;
+    double l, r;
+    uint64_t c = 0;
+    query(top, srcAddress, dstAddress, 0, &l, &r, &c);
+    return c;
 }
 
 double topology_min_path_latency(Topology* top) {
     if (!top || topology_seal(top) != SPE_OK) return 0.0;
-    return top->min_latency;
+    if (top->cache_mode == TOPOLOGY_ANSWER_REFERENCE) {
+        double m = 0.0;
+        const uint64_t b = atomic_load(&top->stored_min_bits);
+        memcpy(&m, &b, sizeof m);
+        return m;
+    }
+    pthread_rwlock_rdlock(&top->state_lock);
+    const double m = top->snap ? top->snap->min_latency : 0.0;
+    pthread_rwlock_unlock(&top->state_lock);
+    return m;
+}
+
+/* _topology_logAllCachedPaths (:1914-1950) over the model: every explicit entry,
+ * then every entry each source's row stored; path_toString's format
+ * (shd-path.c:58-71). */
+static void dump_entry(Topology* top, Snap* sn, int32_t x, int32_t y, int32_t kind, uint64_t count) {
+    double l = -1.0, r = -1.0;
+    if (kind == K_SELF) {
+        spe_entry e;
+        spe_graph_self_path(top->graph, x, &e);
+        l = e.latency;
+        r = e.reliability;
+    } else if (sn && sn->slot_of_vertex[x] >= 0 && sn->slot_of_vertex[y] >= 0) {
+        snap_value(top, sn, sn->slot_of_vertex[x], sn->slot_of_vertex[y], &l, &r);
+    }
+    tlog(top, LOG_INFO, "Found path %s%s%s in cache: SourceIndex=%d DestinationIndex=%d Latency=%f "
+                        "Reliability=%f PacketCount=%llu isDirect=%s",
+         top->vstr[VS_ID][x], top->directed ? "->" : "<->", top->vstr[VS_ID][y], x, y, l, r,
+         (unsigned long long)count, kind == K_DIRECT ? "True" : "False");
+}
+
+int64_t topology_cached_path_count(Topology* top) {
+    if (!top) return 0;
+    int64_t n = atomic_load(&top->n_explicit);
+    pthread_rwlock_rdlock(&top->state_lock);
+    Snap* sn = top->snap;
+    for (int32_t x = 0; sn && x < top->n; ++x) {
+        const uint64_t rx = atomic_load(&top->run_seq[x]);
+        if (!rx) continue;
+        for (int32_t j = 0; j < sn->A; ++j) {
+            int32_t k;
+            const int32_t y = sn->attached[j];
+            if (!explicit_seq(top, x, y, &k) && entry_seq(top, x, y, NULL) == rx) ++n;
+        }
+    }
+    pthread_rwlock_unlock(&top->state_lock);
+    return n;
 }
 
 void topology_free(Topology* top) {
     if (!top) return;
-    /* _topology_logAllCachedPaths (:1914-1950): the pairs that carried packets */
-    if (top->counts && top->lat)
-        for (size_t j = 0; j < top->counts_cap; ++j) {
-            const uint64_t key = top->counts[j].key;
-            if (!key) continue;
-            const int32_t s = (int32_t)((key - 1) >> 32), t = (int32_t)((key - 1) & 0xffffffffu);
-            const size_t o = (size_t)s * top->A + t;
-            tlog(top, LOG_INFO, "Found path %s%s%s in cache: SourceIndex=%d DestinationIndex=%d Latency=%f "
-                                "Reliability=%f PacketCount=%llu",
-                 top->vstr[VS_ID][top->attached[s]], top->directed ? "->" : "<->",
-                 top->vstr[VS_ID][top->attached[t]], top->attached[s], top->attached[t], top->lat[o], top->rel[o],
-                 (unsigned long long)atomic_load(&top->counts[j].count));
+    if (log_on(top, LOG_INFO)) {
+        Snap* sn = top->snap;
+        for (int i = 0; i < NSHARD; ++i)
+            for (size_t j = 0; j < top->shards[i].cap; ++j) {
+                const PairRec* r = &top->shards[i].tab[j];
+                if (!r->key || !r->seq) continue;
+                dump_entry(top, sn, (int32_t)((r->key - 1) >> 32), (int32_t)((r->key - 1) & 0xffffffffu), r->kind,
+                           r->count);
+            }
+        for (int32_t x = 0; sn && x < top->n; ++x) {
+            const uint64_t rx = atomic_load(&top->run_seq[x]);
+            if (!rx) continue;
+            for (int32_t j = 0; j < sn->A; ++j) {
+                int32_t k;
+                const int32_t y = sn->attached[j];
+                if (explicit_seq(top, x, y, &k) || entry_seq(top, x, y, NULL) != rx) continue;
+                dump_entry(top, sn, x, y, K_NONE, pair_count(top, x, y, 0));
+            }
         }
-    /* _topology_clearCache's timing line (:1262-1265) */
-    tlog(top, LOG_MESSAGE, "path cache cleared, spent %f seconds computing %lld shortest path rows on the GPU",
-         top->build_seconds, (long long)top->build_rows);
+    }
+    /* _topology_clearCache's timing line (:1262-1265); the rows are built on the GPU */
+    tlog(top, LOG_MESSAGE, "path cache cleared, spent %f seconds computing %lld shortest paths with dijkstra, "
+                           "and %f seconds computing %lld shortest self paths",
+         top->build_seconds, (long long)top->build_rows, 0.0, (long long)top->self_paths);
     topo_release(top);
 }

@@ -21,6 +21,7 @@ SPE_OK = 0
 SPE_SELF_ROW = 0
 SPE_SELF_RULE = 1
 SPE_ENGINE_AUTO, SPE_ENGINE_BATCH, SPE_ENGINE_LDS = 0, 1, 2
+SPE_GATHER_AUTO, SPE_GATHER_RCCL, SPE_GATHER_PEER = 0, 1, 2
 WAVE = 64
 
 
@@ -48,14 +49,15 @@ class TableOpts(C.Structure):
                 ("ext_latrel", C.c_void_p),
                 ("ext_next_hop", C.c_void_p), ("ext_hops", C.c_void_p), ("ext_filled", C.c_int32),
                 ("owner_rank", C.c_void_p), ("engine", C.c_int32), ("lanes_per_group", C.c_int32),
-                ("want_aux", C.c_int32)]
+                ("want_aux", C.c_int32), ("devices", C.c_void_p), ("n_devices", C.c_int32),
+                ("gather", C.c_int32)]
 
 
 class TableLayout(C.Structure):
     _fields_ = [("n_attached", C.c_int32), ("block_begin", C.c_int32), ("block_end", C.c_int32),
                 ("elems", C.c_int64), ("latrel", C.c_void_p),
                 ("next_hop", C.c_void_p), ("hops", C.c_void_p), ("groups_per_launch", C.c_int32),
-                ("engine", C.c_int32)]
+                ("engine", C.c_int32), ("n_devices", C.c_int32), ("device", C.c_int32)]
 
 
 class Entry(C.Structure):
@@ -72,7 +74,8 @@ class KernelProfile(C.Structure):
 
 class BuildStats(C.Structure):
     _fields_ = [("iterations", C.c_int64), ("active_rounds", C.c_int64), ("launches", C.c_int64),
-                ("seconds", C.c_double)]
+                ("seconds", C.c_double), ("gather_seconds", C.c_double), ("n_devices", C.c_int32),
+                ("gather", C.c_int32)]
 
 
 # every symbol include/spe.h declares (tests/test_abi.py checks the export table)
@@ -82,7 +85,8 @@ EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_
            "spe_table_profile_get", "spe_table_build_stats", "spe_table_layout_get",
            "spe_table_get", "spe_table_download", "spe_lookup_batch", "spe_table_min_latency",
            "spe_table_key", "spe_table_save", "spe_table_load", "spe_table_free",
-           "spe_graph_set_edge_aux", "spe_table_download_aux", "spe_fw_apsp"]
+           "spe_graph_set_edge_aux", "spe_table_download_aux", "spe_fw_apsp", "spe_graph_self_path",
+           "spe_graph_adjacent", "spe_device_shares"]
 
 _lib = None
 
@@ -128,6 +132,9 @@ def lib():
         L.spe_fw_apsp.argtypes = [P, P, C.c_int64, P, P, P]
         L.spe_table_free.argtypes = [P]
         L.spe_table_free.restype = None
+        L.spe_device_shares.argtypes = [C.c_int32, C.c_int32, P, P]
+        L.spe_graph_self_path.argtypes = [P, C.c_int32, P]
+        L.spe_graph_adjacent.argtypes = [P, C.c_int32, C.c_int32, P]
         _lib = L
     return _lib
 
@@ -140,6 +147,15 @@ def _check(rc: int, what: str):
 
 def _p(a: Optional[np.ndarray]):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def device_shares(n_attached: int, n_devices: int):
+    """spe_device_shares: the [begin, end) 64-source block range of each device of
+    a multi-device table (host-only)."""
+    b0 = np.empty(n_devices, np.int32)
+    b1 = np.empty(n_devices, np.int32)
+    _check(lib().spe_device_shares(int(n_attached), int(n_devices), _p(b0), _p(b1)), "spe_device_shares")
+    return list(zip(b0.tolist(), b1.tolist()))
 
 
 def device_count() -> int:
@@ -206,7 +222,8 @@ class PathTable:
 
     def __init__(self, graph: Graph, attached, self_mode: int = SPE_SELF_ROW, force_sssp: bool = False,
                  groups: int = 0, blocks=None, ext=None, ext_filled: bool = False, lanes: int = 0,
-                 owner_order=None, engine: int = 0, want_aux: bool = False):
+                 owner_order=None, engine: int = 0, want_aux: bool = False, devices=None,
+                 gather: int = SPE_GATHER_AUTO):
         self.graph = graph
         self.attached = np.ascontiguousarray(attached, np.int32)
         self.A = int(self.attached.shape[0])
@@ -223,6 +240,11 @@ class PathTable:
             o.owner_rank = self._rank.ctypes.data
         if blocks is not None:
             o.block_begin, o.block_end = int(blocks[0]), int(blocks[1])
+        if devices is not None:   # one process, several devices: shares + all-gather (spe_multi.cpp)
+            self._devs = np.ascontiguousarray(devices, np.int32)
+            o.devices = self._devs.ctypes.data
+            o.n_devices = int(self._devs.shape[0])
+            o.gather = int(gather)
         if ext is not None:  # three device pointers (ints): latrel (2 x f64), next_hop (i32), hops (u16)
             o.ext_latrel, o.ext_next_hop, o.ext_hops = [int(x) for x in ext]
             o.ext_filled = int(bool(ext_filled))

@@ -15,7 +15,9 @@ EXPORTS = ["topology_new", "topology_new_on_device", "topology_free", "topology_
            "topology_incrementPathPacketCounter", "topology_set_log_callback",
            "topology_set_min_latency_callback", "topology_seal", "topology_vertex_count",
            "topology_attached_vertex", "topology_path_packet_count", "topology_min_path_latency",
-           "topology_getPathInfo"]
+           "topology_getPathInfo", "topology_set_log_level", "topology_set_answer_mode",
+           "topology_cached_path_count", "topology_check_graphml"]
+ANSWER_ROWS, ANSWER_REFERENCE = 0, 1
 
 RANDOM_FN = C.CFUNCTYPE(C.c_double, C.c_void_p)
 MINLAT_FN = C.CFUNCTYPE(None, C.c_double, C.c_void_p)
@@ -58,8 +60,20 @@ def lib():
         L.topology_path_packet_count.restype = C.c_uint64
         L.topology_min_path_latency.argtypes = [P]
         L.topology_min_path_latency.restype = C.c_double
+        L.topology_set_log_level.argtypes = [P, C.c_int32]
+        L.topology_set_answer_mode.argtypes = [P, C.c_int32]
+        L.topology_set_answer_mode.restype = C.c_int32
+        L.topology_check_graphml.argtypes = [C.c_char_p]
+        L.topology_check_graphml.restype = C.c_int32
+        L.topology_cached_path_count.argtypes = [P]
+        L.topology_cached_path_count.restype = C.c_int64
         _lib = L
     return _lib
+
+
+def check_graphml(path: str) -> bool:
+    """topology_check_graphml: would topology_new accept this file (no GPU needed)."""
+    return bool(lib().topology_check_graphml(path.encode()))
 
 
 def ip(s: str) -> int:
@@ -121,6 +135,26 @@ class Topology:
 
     def min_latency(self) -> float:
         return float(lib().topology_min_path_latency(self.h))
+
+    def seal(self) -> int:
+        return int(lib().topology_seal(self.h))
+
+    def set_answer_mode(self, mode: int):
+        assert lib().topology_set_answer_mode(self.h, int(mode)) == 0
+
+    def cached_paths(self) -> int:
+        return int(lib().topology_cached_path_count(self.h))
+
+    def capture_logs(self, level: int = 4):
+        """Route the topology's log lines (level <= `level`) into self.logs."""
+        self.logs = []
+
+        def cb(lvl, text, _ctx):
+            self.logs.append((lvl, text.decode()))
+
+        self._log_cb = LOG_FN(cb)
+        lib().topology_set_log_callback(self.h, self._log_cb, None)
+        lib().topology_set_log_level(self.h, int(level))
 
     def close(self):
         if getattr(self, "h", None):

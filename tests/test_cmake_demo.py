@@ -78,9 +78,9 @@ def test_demo_rejects_invalid_graph(tmp_path):
     assert r.returncode == 2 and "topology_new failed" in r.stderr
 
 
-def _run_demo(path, hosts, packets, threads=4, seed=1):
-    r = subprocess.run([DEMO, str(path), str(hosts), str(packets), str(threads), str(seed)], capture_output=True,
-                       text=True, timeout=110)
+def _run_demo(path, hosts, packets, threads=4, seed=1, late=0):
+    r = subprocess.run([DEMO, str(path), str(hosts), str(packets), str(threads), str(seed), str(late)],
+                       capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout + r.stderr
     return json.loads(r.stdout.strip().splitlines()[-1])
 
@@ -113,3 +113,19 @@ def test_demo_on_sparse_graph(tmp_path, monkeypatch, engine):
     d = _run_demo(p, 400, 400_000)
     assert d["mismatches"] == 0 and d["routable"] == 400_000 and d["vertices"] == 1500
     assert d["count_pair_0_0"] >= 0 and d["min_path_latency"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.engine_fixed
+def test_demo_attach_after_seal_under_concurrent_readers(tmp_path):
+    """4 worker threads query while the main thread attaches 200 more hosts to a
+    sealed topology: each new vertex makes the next query that needs it build a
+    replacement table that is swapped in under the readers.  Getters agree with
+    getPathInfo, and the packet counters of all cached paths add up exactly to the
+    packets counted (no count lost across the swaps)."""
+    t = graphs.gen_random_small(2000, 6000, 12)
+    p = tmp_path / "late.graphml"
+    graphs.write_graphml(t, str(p))
+    d = _run_demo(p, 100, 300_000, threads=4, late=200)
+    assert d["mismatches"] == 0 and d["late_hosts"] == 200
+    assert d["counted"] == d["routable"] > 0

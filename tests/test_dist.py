@@ -84,3 +84,68 @@ def test_gloo_world2_sharded_build_and_allgather():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_chunk_plan_covers_every_block_once():
+    for nblk in (1, 7, 157, 782, 1563):
+        for world in (1, 2, 3, 8):
+            for groups in (1, 16, 48, 64):
+                rounds, G = sd.chunk_plan(nblk, world, groups)
+                assert 1 <= G <= max(1, groups) and rounds * world * G >= nblk
+                assert rounds * world * G - nblk < world * rounds   # balanced padding
+                seen = []
+                for r in range(world):
+                    for k, c, b0, b1 in sd.rank_chunks(nblk, world, r, rounds, G):
+                        assert c == k * world + r
+                        seen += list(range(b0, b1))
+                assert sorted(seen) == list(range(nblk))
+
+
+def _chunk_worker(rank, world, port, out_q):
+    """bench.py's N > 1 step on CPU: round-robin chunks, each round's records
+    all-gathered in place (sd.allgather_round) into the replicated SB64 table."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys_path_oracle()
+    from oracle import Oracle
+    top = graphs.gen_random_small(300, 900, 6)
+    A = np.arange(top.n, dtype=np.int32)
+    nblk = sd.nblocks(top.n)
+    rounds, G = sd.chunk_plan(nblk, world, 2)
+    chunk_elems = G * top.n * 64
+    lr = torch.full((rounds * world * chunk_elems, 2), float("nan"), dtype=torch.float64)
+    o = Oracle(top)
+    for k, c, b0, b1 in sd.rank_chunks(nblk, world, rank, rounds, G):
+        if b1 > b0:   # this rank's rows, written where the table keeps them
+            rows = o.rows(A[b0 * 64:min(top.n, b1 * 64)], A)
+            rows["hops"] = rows["hops"].astype(np.uint16)
+            f = sd.rows_to_sb64(rows, b0 * 64, top.n, G)
+            lr[c * chunk_elems:(c + 1) * chunk_elems] = torch.from_numpy(f["lr"])
+        sd.allgather_round(lr, k, world, rank, chunk_elems, dist)
+    ref = o.rows(A, A)
+    e = sd.sb64_index(np.repeat(A, top.n), np.tile(A, top.n), top.n)
+    got = lr.numpy()[e]
+    ok = np.array_equal(got[:, 0], ref["lat"].ravel()) and np.array_equal(got[:, 1], ref["rel"].ravel())
+    out_q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_round_robin_chunks_allgather(world):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_chunk_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(world)}

@@ -1,0 +1,155 @@
+"""GPU parity on the configurations bench.py actually measures, built exactly as
+the bench builds them.
+
+Every table here is built the bench's way: slots in spe_order_sources order,
+the AUTO engine, automatic groups per launch, the rows / relaxation overlap on
+(its default), the full table in one spe_table_build.  Rows are then checked
+bit-exact against the oracle (latency, reliability, next hop, hops, routability;
+tolerance 0 -- the north star allows 1e-9 relative) for at least the first and
+the last source of EVERY build launch, and size-independent properties are
+checked over what was downloaded.  C5 runs the 100M-query lookup batch of the
+bench against the full C3 table and checks it against spe_table_get and the
+oracle (reference: the per-packet lookups of shd-worker.c:235-247 through
+_topology_getPathEntry, shd-topology.c:1952-2075).
+"""
+import numpy as np
+import pytest
+
+from shadow_amd import graphs
+from oracle import Oracle
+
+pytestmark = [pytest.mark.gpu, pytest.mark.engine_fixed]
+
+ORACLE_THREADS = 16
+
+
+@pytest.fixture(scope="module")
+def spe():
+    from shadow_amd import spe as m
+    assert m.device_count() > 0, "no GPU visible"
+    return m
+
+
+def compare_rows(got, ref, label):
+    ok = ref["kind"] != 0
+    np.testing.assert_array_equal(got["ok"], ok, err_msg=f"{label}: routability")
+    for k in ("lat", "rel"):
+        bad = np.flatnonzero(got[k][ok] != ref[k][ok])
+        assert bad.size == 0, f"{label}: {k} differs at {bad.size} entries"
+    np.testing.assert_array_equal(got["hops"][ok], ref["hops"][ok], err_msg=f"{label}: hops")
+    np.testing.assert_array_equal(got["next"][ok], ref["next"][ok], err_msg=f"{label}: next hop")
+    assert (got["lat"][~ok] == -1).all() and (got["hops"][~ok] == 0).all()
+
+
+def launch_sample_slots(A, groups, extra_per_launch=0, seed=0):
+    """First and last source slot of every build launch (launch k covers 64-source
+    blocks [k*groups, (k+1)*groups)), plus `extra_per_launch` seeded-random ones."""
+    rng = np.random.default_rng(seed)
+    nblk = (A + 63) // 64
+    slots = []
+    for b0 in range(0, nblk, groups):
+        lo, hi = b0 * 64, min(A, (b0 + groups) * 64)
+        slots += [lo, hi - 1]
+        if extra_per_launch:
+            slots += list(rng.integers(lo, hi, extra_per_launch))
+    return np.unique(np.array(slots, dtype=np.int64))
+
+
+def bench_table(spe, top, att):
+    """The bench's build: clustered slot order, AUTO engine and groups, overlap on."""
+    g = spe.Graph(top)
+    order = g.order_sources(att)
+    t = spe.PathTable(g, order)
+    t.build()
+    return g, t, order
+
+
+def check_sampled_rows(t, top, order, slots, label):
+    ora = Oracle(top).rows(order[slots], order, nthreads=ORACLE_THREADS)
+    for i, s in enumerate(slots):
+        got = t.download(int(s), int(s) + 1)
+        ref = {k: ora[k][i:i + 1] for k in ("lat", "rel", "next", "hops", "kind")}
+        compare_rows(got, ref, f"{label} slot {s}")
+        # properties of every routable entry: hops >= 1 and the next hop is an
+        # out-neighbour of the source (or the target itself for a direct path)
+        assert (got["hops"][got["ok"]] >= 1).all()
+    return ora
+
+
+def test_c3_bench_build_every_launch(spe):
+    """C3 (50k BA) full table, bench settings: two+ rows of every launch vs the oracle."""
+    top = graphs.gen_ba(50000, 3, 3)
+    att = np.arange(top.n, dtype=np.int32)
+    g, t, order = bench_table(spe, top, att)
+    lay = t.layout()
+    assert lay["engine"] == spe.SPE_ENGINE_BATCH
+    slots = launch_sample_slots(t.A, lay["groups_per_launch"], extra_per_launch=1, seed=3)
+    nlaunch = -(-t.nblocks // lay["groups_per_launch"])
+    assert len(slots) >= 2 * nlaunch
+    check_sampled_rows(t, top, order, slots, "C3")
+
+
+def test_c2_bench_build_lds_engine(spe):
+    """C2 (10k RGG) full table, bench settings (AUTO picks the LDS engine)."""
+    top = graphs.gen_rgg(10000, 2)
+    att = np.arange(top.n, dtype=np.int32)
+    g, t, order = bench_table(spe, top, att)
+    lay = t.layout()
+    assert lay["engine"] == spe.SPE_ENGINE_LDS
+    rng = np.random.default_rng(2)
+    slots = np.unique(np.r_[0, t.A - 1, rng.integers(0, t.A, 30)])
+    check_sampled_rows(t, top, order, slots, "C2")
+
+
+def test_c4_one_gpu_full_table_every_launch(spe):
+    """C4 (200k tiered, A = 100k stubs): the whole 10^10-pair table (220 GB) built on
+    ONE GPU with the bench settings; two rows of every launch vs the oracle."""
+    top = graphs.gen_tiered()
+    att = graphs.tiered_attached(top)
+    g, t, order = bench_table(spe, top, att)
+    lay = t.layout()
+    assert lay["block_begin"] == 0 and lay["block_end"] == t.nblocks
+    slots = launch_sample_slots(t.A, lay["groups_per_launch"])
+    check_sampled_rows(t, top, order, slots, "C4")
+
+
+def test_c5_full_size_lookups(spe):
+    """C5: 100M uniform (s, t) slot pairs (seed 5, as bench.py --config c5) against
+    the full C3 table.  Every query routable; 10k sampled queries equal
+    spe_table_get; 2,048 queries planted at random positions (32 source slots x 64
+    targets) equal the oracle's rows."""
+    import torch
+    top = graphs.gen_ba(50000, 3, 3)
+    att = np.arange(top.n, dtype=np.int32)
+    g = spe.Graph(top)
+    t = spe.PathTable(g, att)      # bench.py --config c5 builds it in natural slot order
+    t.build()
+    q = 100_000_000
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    pairs = torch.randint(0, t.A, (q, 2), dtype=torch.int32, device="cuda", generator=gen)
+    rng = np.random.default_rng(55)
+    src_slots = rng.choice(t.A, 32, replace=False)
+    planted = np.stack([np.repeat(src_slots, 64), rng.integers(0, t.A, 32 * 64)], axis=1).astype(np.int32)
+    pos = rng.choice(q, planted.shape[0], replace=False)
+    pairs[torch.from_numpy(pos).cuda()] = torch.from_numpy(planted).cuda()
+    lat = torch.empty(q, dtype=torch.float64, device="cuda")
+    rel = torch.empty(q, dtype=torch.float64, device="cuda")
+    ok = torch.empty(q, dtype=torch.uint8, device="cuda")
+    t.lookup_batch(pairs.data_ptr(), q, lat.data_ptr(), rel.data_ptr(), ok.data_ptr())
+    torch.cuda.synchronize()
+    assert bool(ok.all().item()), "C3 is connected: every query is routable"
+    assert bool((lat > 0).all().item()) and bool(((rel > 0) & (rel <= 1)).all().item())
+    # 10k seeded-random queries against the per-entry C-ABI read-back
+    idx = rng.choice(q, 10_000, replace=False)
+    ip = torch.from_numpy(idx).cuda()
+    pp, ll, rr = pairs[ip].cpu().numpy(), lat[ip].cpu().numpy(), rel[ip].cpu().numpy()
+    for i in range(idx.shape[0]):
+        e = t.get(int(pp[i, 0]), int(pp[i, 1]))
+        assert e["latency"] == ll[i] and e["reliability"] == rr[i], f"query {idx[i]}"
+    # planted queries against the oracle
+    ora = Oracle(top).rows(att[src_slots], att, nthreads=ORACLE_THREADS)
+    tp = torch.from_numpy(pos).cuda()
+    gl, gr = lat[tp].cpu().numpy(), rel[tp].cpu().numpy()
+    row = np.repeat(np.arange(32), 64)
+    np.testing.assert_array_equal(gl, ora["lat"][row, planted[:, 1]])
+    np.testing.assert_array_equal(gr, ora["rel"][row, planted[:, 1]])

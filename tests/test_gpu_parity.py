@@ -172,11 +172,14 @@ def test_one_vertex_kats(spe, golden_dir):
         assert out["lat"][0, 0] == k["lat"] and out["rel"][0, 0] == k["rel"], name
 
 
-def test_lookup_batch_against_table(spe):
+def test_lookup_batch_against_oracle(spe):
+    """spe_lookup_batch (the per-packet getLatency / getReliability / isRoutable of
+    shd-worker.c:235-247) against the ORACLE's rows, not the GPU's own table."""
     import torch
-    top = graphs.gen_random_small(500, 1500, 46)
+    top = graphs.gen_random_small(500, 1500, 46, directed=True)
     A = np.arange(top.n, dtype=np.int32)
-    out, t, _ = run_gpu(spe, top, A)
+    _, t, _ = run_gpu(spe, top, A)
+    out = Oracle(top).rows(A, A)
     rng = np.random.default_rng(5)
     q = 100000
     pairs = rng.integers(0, top.n, size=(q, 2)).astype(np.int32)
@@ -190,7 +193,8 @@ def test_lookup_batch_against_table(spe):
     v = pairs[:, 0] >= 0
     np.testing.assert_array_equal(lat[v], out["lat"][pairs[v, 0], pairs[v, 1]])
     np.testing.assert_array_equal(rel[v], out["rel"][pairs[v, 0], pairs[v, 1]])
-    assert (ok[v] == 1).all() and (ok[~v] == 0).all()
+    np.testing.assert_array_equal(ok[v], out["ok"][pairs[v, 0], pairs[v, 1]].astype(np.uint8))
+    assert (ok[~v] == 0).all() and (lat[~v] == -1).all()
 
 
 def test_c3_sample_rows_full_size(spe):
