@@ -33,6 +33,16 @@
 extern "C" {
 #endif
 
+/* Inside a Shadow tree the reference's own shd-topology.h declares the
+ * topology_* names with Shadow's types; build this library (and include this
+ * header in the adapter) with -DSHD_TOPOLOGY_SPE_PREFIXED and every entry point
+ * below is spe_topology_* instead. */
+#ifdef SHD_TOPOLOGY_SPE_PREFIXED
+#define SHD_TOPO(name) spe_##name
+#else
+#define SHD_TOPO(name) name
+#endif
+
 typedef uint32_t spe_in_addr_t;          /* network byte order, like in_addr_t */
 typedef struct _Topology Topology;
 
@@ -44,38 +54,38 @@ typedef void (*topology_log_fn)(int level, const char* text, void* ctx);
 /* GraphML file -> validated topology on `device`; NULL on any validation
  * failure (shd-topology.c:2485-2490).  The file is read synchronously.
  * topology_new builds on device SHADOW_SPE_DEVICE (default 0). */
-Topology* topology_new(const char* graphPath);
-Topology* topology_new_on_device(const char* graphPath, int32_t device);
+Topology* SHD_TOPO(topology_new)(const char* graphPath);
+Topology* SHD_TOPO(topology_new_on_device)(const char* graphPath, int32_t device);
 /* The ingest and validation of topology_new alone (no device work): 1 when the
  * reference would accept the file, else 0. */
-int32_t topology_check_graphml(const char* graphPath);
-void topology_free(Topology* top);
+int32_t SHD_TOPO(topology_check_graphml)(const char* graphPath);
+void SHD_TOPO(topology_free)(Topology* top);
 
 /* Hint-matched attachment (shd-topology.c:2077-2413).  Hints may be NULL. */
-void topology_attach(Topology* top, spe_in_addr_t address, topology_random_fn random, void* random_ctx,
+void SHD_TOPO(topology_attach)(Topology* top, spe_in_addr_t address, topology_random_fn random, void* random_ctx,
                      const char* ipHint, const char* citycodeHint, const char* countrycodeHint,
                      const char* geocodeHint, const char* typeHint, uint64_t* bwDownOut, uint64_t* bwUpOut);
-void topology_detach(Topology* top, spe_in_addr_t address);
+void SHD_TOPO(topology_detach)(Topology* top, spe_in_addr_t address);
 
-int32_t topology_isRoutable(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
-double topology_getLatency(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
-double topology_getReliability(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
-void topology_incrementPathPacketCounter(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
+int32_t SHD_TOPO(topology_isRoutable)(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
+double SHD_TOPO(topology_getLatency)(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
+double SHD_TOPO(topology_getReliability)(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
+void SHD_TOPO(topology_incrementPathPacketCounter)(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
 /* worker_sendPacket's three per-packet calls (isRoutable, getReliability,
  * getLatency, shd-worker.c:235-247) answered by one slot resolution and one
  * table read: returns routable; *latency / *reliability as the two getters
  * (-1.0 when unroutable).  Either output pointer may be NULL. */
-int32_t topology_getPathInfo(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress, double* latency,
+int32_t SHD_TOPO(topology_getPathInfo)(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress, double* latency,
                              double* reliability);
 
 /* engine hooks (callbacks run on the calling thread, some inside the topology's
  * locks: they must not call back into the topology) */
-void topology_set_log_callback(Topology* top, topology_log_fn fn, void* ctx);
+void SHD_TOPO(topology_set_log_callback)(Topology* top, topology_log_fn fn, void* ctx);
 /* levels above `level` are not formatted (default 3, message; 4 enables the
  * per-path info lines of a source's first query and the cached-path dump at
  * topology_free, 5 the per-target debug lines) */
-void topology_set_log_level(Topology* top, int32_t level);
-void topology_set_min_latency_callback(Topology* top, topology_min_latency_fn fn, void* ctx);
+void SHD_TOPO(topology_set_log_level)(Topology* top, int32_t level);
+void SHD_TOPO(topology_set_min_latency_callback)(Topology* top, topology_min_latency_fn fn, void* ctx);
 
 /* What a query answers.  The reference lazily caches one Path per vertex pair,
  * first writer wins, and answers (s, t) with the cached (t, s) path when t's
@@ -93,23 +103,23 @@ void topology_set_min_latency_callback(Topology* top, topology_min_latency_fn fn
  * at topology_new. */
 #define TOPOLOGY_ANSWER_ROWS 0
 #define TOPOLOGY_ANSWER_REFERENCE 1
-int32_t topology_set_answer_mode(Topology* top, int32_t mode);
+int32_t SHD_TOPO(topology_set_answer_mode)(Topology* top, int32_t mode);
 
 /* Build the path table now (otherwise done on the first query).  Hosts may
  * attach after sealing: the published table keeps answering the pairs it holds
  * while the first query that needs a new vertex builds a replacement, which is
  * swapped in atomically (readers never see a freed or half-built table; packet
  * counts and cache state are per vertex pair and carry over). */
-int32_t topology_seal(Topology* top);
+int32_t SHD_TOPO(topology_seal)(Topology* top);
 /* introspection used by tests */
-int32_t topology_vertex_count(const Topology* top);
-int32_t topology_attached_vertex(const Topology* top, spe_in_addr_t address);   /* -1 if unknown */
+int32_t SHD_TOPO(topology_vertex_count)(const Topology* top);
+int32_t SHD_TOPO(topology_attached_vertex)(const Topology* top, spe_in_addr_t address);   /* -1 if unknown */
 /* packetCount of the cached Path the query (src, dst) hits (exact, every pair) */
-uint64_t topology_path_packet_count(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
-double topology_min_path_latency(Topology* top);
+uint64_t SHD_TOPO(topology_path_packet_count)(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress);
+double SHD_TOPO(topology_min_path_latency)(Topology* top);
 /* number of Paths the reference's cache would hold now (the lines the dump at
  * topology_free prints at log level 4) */
-int64_t topology_cached_path_count(Topology* top);
+int64_t SHD_TOPO(topology_cached_path_count)(Topology* top);
 
 #ifdef __cplusplus
 }

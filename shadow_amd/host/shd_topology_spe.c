@@ -38,6 +38,30 @@
 
 #include "spe.h"
 
+#ifdef SHD_TOPOLOGY_SPE_PREFIXED   /* the header declared spe_topology_*: define those */
+#define topology_attach spe_topology_attach
+#define topology_attached_vertex spe_topology_attached_vertex
+#define topology_cached_path_count spe_topology_cached_path_count
+#define topology_check_graphml spe_topology_check_graphml
+#define topology_detach spe_topology_detach
+#define topology_free spe_topology_free
+#define topology_getLatency spe_topology_getLatency
+#define topology_getPathInfo spe_topology_getPathInfo
+#define topology_getReliability spe_topology_getReliability
+#define topology_incrementPathPacketCounter spe_topology_incrementPathPacketCounter
+#define topology_isRoutable spe_topology_isRoutable
+#define topology_min_path_latency spe_topology_min_path_latency
+#define topology_new spe_topology_new
+#define topology_new_on_device spe_topology_new_on_device
+#define topology_path_packet_count spe_topology_path_packet_count
+#define topology_seal spe_topology_seal
+#define topology_set_answer_mode spe_topology_set_answer_mode
+#define topology_set_log_callback spe_topology_set_log_callback
+#define topology_set_log_level spe_topology_set_log_level
+#define topology_set_min_latency_callback spe_topology_set_min_latency_callback
+#define topology_vertex_count spe_topology_vertex_count
+#endif
+
 enum { LOG_ERROR = 0, LOG_CRITICAL, LOG_WARNING, LOG_MESSAGE, LOG_INFO, LOG_DEBUG };
 
 /* vertex string / numeric attributes the reference reads, by exact name */

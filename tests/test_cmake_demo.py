@@ -27,6 +27,7 @@ DEMO = os.path.join(ROOT, "shadow_amd", "shd_topology_demo")
 
 def _declared(header, prefix):
     txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", header)).read(), flags=re.S)
+    txt = re.sub(r"SHD_TOPO\((\w+)\)", r"\1", txt)   # shd_topology_spe.h's name macro (unprefixed build)
     return set(re.findall(r"\b(" + prefix + r"[A-Za-z0-9_]+)\s*\(", txt))
 
 
