@@ -1329,36 +1329,45 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
         __syncthreads();
         LDS_PHASE(4)
         {
-            // level hl settles v when H[parent] == hl - 1; a vertex settled in this
-            // level already reads hl, so no level sees a half-written parent
-            uint16_t hl = sc >= 0 ? 1 : 2;
-            for (;;) {
-                // readiness first (loads only, so the owned vertices' LDS reads can
-                // be in flight together), then the few settling vertices
-                // (branch-free: a branch per vertex would serialise the loads)
+            // No barrier per hop level: every thread retries its unsettled vertices
+            // until each one's parent has settled (H[p] != 0xFFFF), then settles it
+            // from the parent's final values.  Progress: the unsettled vertex with
+            // the smallest distance has a settled parent (d[p] < d[v]), and its
+            // owner always gets to retry it, so some thread settles a vertex in
+            // every pass.  Parent fields are published before the parent's H
+            // (workgroup release / acquire on LDS).
+            volatile uint16_t* Hv = H;
+            uint16_t par[LDS_VPT];
+#pragma unroll
+            for (int i = 0; i < LDS_VPT; ++i)
+                par[i] = ((todo >> i) & 1u) ? (uint16_t)(PF[tid + i * LDS_T] & 0xFFFFu) : (uint16_t)0;
+            while (todo) {
                 uint32_t ready = 0;
+                uint16_t hp[LDS_VPT];
 #pragma unroll
                 for (int i = 0; i < LDS_VPT; ++i) {
-                    const bool t = (todo >> i) & 1u;
-                    const uint32_t p = t ? (PF[min(tid + i * LDS_T, nc - 1)] & 0xFFFFu) : 0u;
-                    ready |= (t && H[p] == (uint16_t)(hl - 1)) ? (1u << i) : 0u;
+                    hp[i] = ((todo >> i) & 1u) ? Hv[par[i]] : (uint16_t)0xFFFF;
+                    ready |= hp[i] != 0xFFFF ? (1u << i) : 0u;
                 }
-                const bool any = ready != 0;
-                todo &= ~ready;
+                if (!ready) continue;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #pragma unroll
                 for (int i = 0; i < LDS_VPT; ++i) {
                     if (!((ready >> i) & 1u)) continue;
                     const int32_t v = tid + i * LDS_T;
-                    const uint32_t p = PF[v] & 0xFFFFu;
+                    const uint32_t p = par[i];
                     Rl[v] = Rl[p] * pa[i];
                     const uint32_t f = ((int32_t)p == sc) ? (uint32_t)v : (PF[p] >> 16);
                     PF[v] = (f << 16) | p;
-                    H[v] = hl;
                 }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+                for (int i = 0; i < LDS_VPT; ++i)
+                    if ((ready >> i) & 1u) Hv[tid + i * LDS_T] = (uint16_t)(hp[i] + 1);
+                todo &= ~ready;
                 ++nlev;
-                if (!wg_any(any, syncix, s_any)) break;
-                ++hl;
             }
+            __syncthreads();
         }
         LDS_PHASE(5)
         // 5. reliability, next hop, hops (+ latency re-fold for multigraphs)

@@ -277,3 +277,38 @@ def test_multibatch_rows_overlap_matches_serial_and_oracle(spe, monkeypatch):
     out2 = t2.download()
     for k in ("lat", "rel", "next", "hops"):
         np.testing.assert_array_equal(out2[k], out[k])
+
+
+def test_absorbed_edges_flagged_and_rows_still_match(spe):
+    """weight_floor_ok = 0 (spe_graph_info): some latency is below ulp(d)/2 of
+    the path sums, so fl(d + w) == d can happen and the bit-exactness argument
+     no longer covers the graph -- the library reports it (the
+    topology shim logs a warning at topology_new).  Such an edge never becomes
+    a parent in either implementation (igraph relaxes on strict <, the engine
+    needs fl(d[u] + w) > d[u]); rows still equal the oracle's on this graph."""
+    top = graphs.gen_random_small(300, 900, 48)
+    top.elat[:40] = 1e-14   # absorbed: fl(d + 1e-14) == d for every d > ~0.2 ms
+    A = np.arange(top.n, dtype=np.int32)
+    out, t, g = run_gpu(spe, top, A)
+    assert g.info()["weight_floor_ok"] == 0
+    compare(out, Oracle(top).rows(A, A, tie_mode=1), label="absorbed")
+
+
+def test_partially_built_table_refuses_unbuilt_rows(spe):
+    """spe_table_build_blocks over part of the owned range: rows of built blocks
+    read back; rows of unbuilt blocks, the minimum latency and the on-disk cache
+    are refused until every owned block is built."""
+    top = graphs.gen_random_small(400, 1200, 49)
+    A = np.arange(top.n, dtype=np.int32)
+    g = spe.Graph(top)
+    t = spe.PathTable(g, A)
+    t.build_blocks(0, 2)
+    ref = Oracle(top).rows(A[:128], A)
+    got = t.download(0, 128)
+    np.testing.assert_array_equal(got["lat"], ref["lat"])
+    for call in (lambda: t.get(200, 3), lambda: t.download(100, 200), t.min_latency,
+                 lambda: t.save("/tmp/never-written.bin")):
+        with pytest.raises(spe.SpeError):
+            call()
+    t.build_blocks(2, t.nblocks)
+    assert t.get(200, 3)["latency"] > 0 and t.min_latency() > 0
