@@ -120,9 +120,12 @@ def pmc_traffic(args, kernel):
     """HBM bytes per dispatch of `kernel` from a committed PMC summary (separate
     rocprofv3 --pmc passes of this same bench command), or None."""
     path = args.pmc_json
-    if path is None:
-        cand = os.path.join(ROOT, "profiles", f"r01_pmc_{args.config}.json")
-        path = cand if os.path.exists(cand) else None
+    if path is None:   # the newest committed summary of this config
+        for rnd in ("r02", "r01"):
+            cand = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{args.config}.json")
+            if os.path.exists(cand):
+                path = cand
+                break
     if not path:
         return None
     try:
