@@ -91,6 +91,8 @@ struct DevGraph {
     int32_t n_full;          // all vertices (original ids)
     const int32_t* iptr;
     const int32_t* icol;
+    const int4* ipack;       // per in-entry, one 16-B load for the relaxation: {icol, orev | heavy[icol] << 31
+                             // (undirected: the out-list is the in-list), iw as two 32-bit halves}
     const int32_t* irow;     // in-CSR entry -> its target vertex (flat edge passes)
     const double* iw;
     const double* ia;
@@ -287,12 +289,19 @@ __global__ __launch_bounds__(BLOCK) void k_seed(int32_t n, int32_t groups, const
 // Lexicographic candidate update (alt, d[u], u) against the running best of one
 // lane.  Ties against the current parent resolve with the parent's CURRENT
 // distance; an offer from the current parent itself (kk == bk) refreshes it.
+// The stored parent P is read lazily (PK_UNREAD): only an offer EQUAL to the
+// current distance (a refresh from the parent, or a tie) needs it; most offers
+// are strictly better or worse, so most visits skip the 256-B P row.
+constexpr int32_t PK_UNREAD = -3;
+
 struct Best {
     double bd;     // best alt (= distance)
-    int32_t bk;    // in-CSR index of the parent edge
+    int32_t bk;    // in-CSR index of the parent edge (PK_UNREAD: the stored one, not read yet)
     int32_t bu;    // parent vertex (-1: not resolved yet)
     double bdu;    // parent distance (-1: not resolved yet)
     bool need;     // the parent's (R, H, F) must be (re)gathered
+    int32_t pold;  // the stored parent once read (PK_UNREAD until then)
+    size_t rv;     // this lane's state index (for the lazy P read)
 };
 
 template <int L>
@@ -302,6 +311,7 @@ __device__ __forceinline__ void offer(Best& b, const DevGraph& G, const State& s
     if (alt < b.bd) {
         better = true;
     } else if (alt == b.bd) {
+        if (b.bk == PK_UNREAD) b.bk = b.pold = st.P[b.rv];
         if (kk == b.bk) {
             b.need = true;
             b.bdu = du;
@@ -360,9 +370,10 @@ __device__ __forceinline__ void scan_chunk(uint64_t sm, int32_t c0, int32_t base
 // Gather the chosen parent's (R, H, F), write the lane's state if it changed.
 template <int L>
 __device__ __forceinline__ bool finish_vertex(Best& b, const DevGraph& G, const State& st, int32_t g, int32_t n,
-                                              int32_t j, int32_t v, int32_t s, size_t rv, double d_old,
-                                              int32_t p_old) {
+                                              int32_t j, int32_t v, int32_t s, size_t rv, double d_old) {
     bool changed = false;
+    // need with b.bd == d_old implies an equal offer, which read the stored parent
+    const int32_t p_old = b.pold;
     if (b.need) {
         if (b.bu < 0) b.bu = G.icol[b.bk];
         if (G.ablate & 1) {   // diagnostic only: distances + parents, no route records
@@ -424,10 +435,10 @@ __device__ __forceinline__ bool relax_item(int64_t e, int32_t n, int32_t j, int3
     const size_t rv = sidx<L>(g, n, v, j);
     if (e >= 0) {
         d_old = st.D[rv];
-        p_old = st.P[rv];
+        p_old = d_old < INF ? PK_UNREAD : -1;   // an unreached lane has no parent (k_init_state)
     }
     const bool active = (e >= 0) && (s != -1) && (s != v);
-    Best b{d_old, p_old, -1, -1.0, false};
+    Best b{d_old, p_old, -1, -1.0, false, p_old, rv};
     // undirected graphs: the out-list IS the in-list; a single-chunk vertex keeps
     // what marking needs (neighbour, reverse entry, heavy bit) in registers
     int32_t u_last = 0, orev_last = 0;
@@ -435,13 +446,14 @@ __device__ __forceinline__ bool relax_item(int64_t e, int32_t n, int32_t j, int3
     for (int32_t c0 = k0; c0 < k1; c0 += L) {   // subgroup-uniform trip count
         const int32_t k = c0 + j;
         const bool ok = k < k1;
-        const int32_t u_j = ok ? G.icol[k] : 0;
-        const double w_j = ok ? G.iw[k] : 0.0;
+        const int4 pk = ok ? G.ipack[k] : make_int4(0, 0, 0, 0);
+        const int32_t u_j = pk.x;
+        const double w_j = __hiloint2double(pk.w, pk.z);
         const size_t fo = (size_t)g * G.nrel + k;
         const bool f = ok && fl.in_cur[fo] != 0;
         if (G.undirected && ok) {
-            orev_last = G.orev[k];
-            heavy_last = G.oheavy[k] != 0;
+            orev_last = pk.y & 0x7FFFFFFF;
+            heavy_last = pk.y < 0;
         }
         u_last = u_j;
         ok_last = ok;
@@ -451,7 +463,7 @@ __device__ __forceinline__ bool relax_item(int64_t e, int32_t n, int32_t j, int3
                             [&](int32_t kk, int32_t u, double du, double alt) { offer<L>(b, G, st, g, n, j, kk, u, du, alt); });
     }
     bool changed = false;
-    if (e >= 0) changed = finish_vertex<L>(b, G, st, g, n, j, v, s, rv, d_old, p_old);
+    if (e >= 0) changed = finish_vertex<L>(b, G, st, g, n, j, v, s, rv, d_old);
     const bool any = ((__ballot(changed) >> base) & Sub<L>::MASK) != 0;
     if (any) {
         if (G.undirected && k1 - k0 <= L) {
@@ -579,8 +591,9 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_partial(int32_t groups, int32_t
         for (int32_t c0 = kb; c0 < ke; c0 += L) {
             const int32_t k = c0 + j;
             const bool ok = k < ke;
-            const int32_t u_j = ok ? G.icol[k] : 0;
-            const double w_j = ok ? G.iw[k] : 0.0;
+            const int4 pk = ok ? G.ipack[k] : make_int4(0, 0, 0, 0);
+            const int32_t u_j = pk.x;
+            const double w_j = __hiloint2double(pk.w, pk.z);
             const size_t fo = (size_t)g * G.nrel + k;
             const bool f = ok && fl.in_cur[fo] != 0;
             if (f) fl.in_cur[fo] = 0;
@@ -633,14 +646,14 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_combine(int32_t groups, int32_t
             const size_t rv = sidx<L>(g, n, v, j);
             const double d_old = st.D[rv];
             const int32_t p_old = st.P[rv];
-            Best b{d_old, p_old, -1, -1.0, false};
+            Best b{d_old, p_old, -1, -1.0, false, p_old, rv};
             for (int32_t sgi = hp.heavy_seg0[h]; sgi < hp.heavy_seg0[h + 1]; ++sgi) {
                 const size_t o = ((size_t)g * hp.nseg + sgi) * L + j;
                 const int2 uk = pp.uk[o];
                 if (uk.x >= 0) offer<L>(b, G, st, g, n, j, uk.y, uk.x, pp.du[o], pp.alt[o]);
             }
             if (j == 0) fl.hmark_cur[(size_t)g * n + v] = 0;
-            changed = finish_vertex<L>(b, G, st, g, n, j, v, s, rv, d_old, p_old);
+            changed = finish_vertex<L>(b, G, st, g, n, j, v, s, rv, d_old);
         }
         const bool any = ((__ballot(changed) >> base) & Sub<L>::MASK) != 0;
         if (any) {
@@ -1985,6 +1998,15 @@ static int graph_upload(spe_graph* g) {
         std::vector<uint8_t> oheavy(oc.size());
         for (size_t k = 0; k < oc.size(); ++k) oheavy[k] = heavy[oc[k]];
         r = dev_upload(g->allocs, oheavy, &d.oheavy);
+        if (r) return r;
+        std::vector<int4> pack(std::max<size_t>(1, h.icol.size()));
+        for (size_t k = 0; k < h.icol.size(); ++k) {
+            uint64_t wb;
+            std::memcpy(&wb, &h.iw[k], sizeof wb);
+            const int32_t rev = h.directed ? 0 : (h.orev[k] | (heavy[h.icol[k]] ? (int32_t)0x80000000 : 0));
+            pack[k] = make_int4(h.icol[k], rev, (int32_t)(uint32_t)wb, (int32_t)(uint32_t)(wb >> 32));
+        }
+        r = dev_upload(g->allocs, pack, &d.ipack);
         if (r) return r;
     }
 #undef UP

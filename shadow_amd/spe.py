@@ -15,7 +15,8 @@ import numpy as np
 from .graphs import Topology
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libspe.so")
+# SPE_LIB: an alternative build of the library (same-box A/B experiments, tools/build_variant.sh)
+LIB_PATH = os.environ.get("SPE_LIB") or os.path.join(_HERE, "libspe.so")
 
 SPE_OK = 0
 SPE_SELF_ROW = 0
