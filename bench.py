@@ -138,46 +138,61 @@ def pmc_traffic(args, kernel):
         return None
 
 
-def bench_lookup(args):
+def bench_lookup(args, rank=0, world=1, local=0, dist=None):
     """C5: batched per-packet lookups (s_slot, t_slot) -> (latency, reliability, ok)
-    against the HBM-resident C3 table; 41 algorithmic bytes per query."""
+    against the HBM-resident C3 table; 41 algorithmic bytes per query.  N > 1:
+    replicas (the table is replicated after the all-gather; queries
+    split with no communication) -- every rank holds the whole table and answers
+    its own 100M queries per step (weak scaling)."""
     import torch
     from shadow_amd import spe
     top, att, desc = workload("c3")
-    g = spe.Graph(top, device=0)
+    dev = torch.device("cuda", local)
+    g = spe.Graph(top, device=local)
     t = spe.PathTable(g, att)
     t.build()
     q = args.queries
-    gen = torch.Generator(device="cuda").manual_seed(5)
-    pairs = torch.randint(0, t.A, (q, 2), dtype=torch.int32, device="cuda", generator=gen)
-    lat = torch.empty(q, dtype=torch.float64, device="cuda")
-    rel = torch.empty(q, dtype=torch.float64, device="cuda")
-    ok = torch.empty(q, dtype=torch.uint8, device="cuda")
-    stream = torch.cuda.current_stream().cuda_stream
+    gen = torch.Generator(device=dev).manual_seed(5 + rank)
+    pairs = torch.randint(0, t.A, (q, 2), dtype=torch.int32, device=dev, generator=gen)
+    lat = torch.empty(q, dtype=torch.float64, device=dev)
+    rel = torch.empty(q, dtype=torch.float64, device=dev)
+    ok = torch.empty(q, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
     steps = args.steps if args.steps > 0 else 10
     for _ in range(args.warmup):
         t.lookup_batch(pairs.data_ptr(), q, lat.data_ptr(), rel.data_ptr(), ok.data_ptr(), stream)
-    torch.cuda.synchronize()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record()
     for _ in range(steps):
         t.lookup_batch(pairs.data_ptr(), q, lat.data_ptr(), rel.data_ptr(), ok.data_ptr(), stream)
     ev1.record()
-    torch.cuda.synchronize()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
     el = time.perf_counter() - t0
     kern_s = ev0.elapsed_time(ev1) / 1e3 / steps
     assert bool(ok.all().item())
-    value = q * steps / el
+    if dist is not None:
+        x = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        el = float(x.item())
+    if rank != 0:
+        return
+    value = world * q * steps / el
     ach = 41.0 * q / kern_s / 1e9
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         cpu = cpu_lookup_baseline(t.A, args.cpu_seconds)
     line = {"metric": "per-packet lookup queries/s against the GPU-resident path table (config C5)",
-            "value": round(value, 1), "unit": "queries/s", "n_gpus": 1, "steps": steps, "warmup": args.warmup,
+            "value": round(value, 1), "unit": "queries/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * el / steps, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"C5: {q} uniform (s,t) slot pairs (seed 5) on the {desc} table"},
+            "config": {"workload": f"C5: {q} uniform (s,t) slot pairs per GPU (seed 5 + rank) on the {desc} table",
+                       "parallelism": f"{world} replica(s) of the table, queries split, no communication"},
             "roofline": {"bound": "hbm", "kernel": "k_lookup", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, "k_lookup"),
                          "algorithmic_bytes_per_query": 41},
@@ -481,8 +496,6 @@ def main():
     ap.add_argument("--shares", type=int, default=1, help="emulate one rank of a job with this many GPUs")
     ap.add_argument("--share-index", type=int, default=0, help="--shares: the rank whose chunks this run builds")
     args = ap.parse_args()
-    if args.config == "c5":
-        return bench_lookup(args)
     if args.config == "complete":
         return bench_complete(args)
     if args.config == "c2fw":
@@ -505,7 +518,10 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    bench_table(args, rank, world, local, dist)
+    if args.config == "c5":
+        bench_lookup(args, rank, world, local, dist)
+    else:
+        bench_table(args, rank, world, local, dist)
     if dist is not None:
         dist.destroy_process_group()
 
