@@ -664,6 +664,240 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_combine(int32_t groups, int32_t
     if (__ballot(wrote) && lane == 0) *fl.any_changed = 1;
 }
 
+// ---- L = 64 * M sources per relaxation row, M > 1: each thread holds M lanes
+// (j = lane, lane + 64, ...).  A row visit's fixed costs (frontier word, CSR
+// chunk, in-edge flags, out-edge marks) are then shared by 64 M sources while
+// the per-source work (the lanes of each neighbour row read, the own row, the
+// route gathers and writes) scales with M; a CPU model of the schedule
+// (tools/sim_schedules.py) and the measured L = 32 / 64 ratio put the lines
+// touched per source ~13 % below L = 64 at L = 128.
+
+template <int M, int INFL, typename F>
+__device__ __forceinline__ void scan_chunk_m(uint64_t sm, int32_t c0, int32_t u_j, double w_j, int32_t g, int32_t n,
+                                             int32_t lane, const bool (&active)[M], const State& st, F&& f) {
+    constexpr int L = WAVE * M;
+    while (sm) {
+        int32_t us[INFL], ks[INFL];
+        double ws[INFL], dus[INFL][M];
+#pragma unroll
+        for (int q = 0; q < INFL; ++q) {
+            us[q] = -1;
+            if (sm) {
+                const int32_t b = __builtin_ctzll(sm);
+                sm &= sm - 1;
+                us[q] = __builtin_amdgcn_readlane(u_j, b);
+                ws[q] = sub_get_d<WAVE>(w_j, b);
+                ks[q] = c0 + b;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < INFL; ++q)
+            if (us[q] >= 0) {
+                const double* row = st.D + ((size_t)g * (size_t)n + (size_t)us[q]) * L;
+#pragma unroll
+                for (int m = 0; m < M; ++m) dus[q][m] = row[lane + m * WAVE];
+            }
+#pragma unroll
+        for (int q = 0; q < INFL; ++q) {
+            if (us[q] < 0) continue;
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                const double alt = dus[q][m] + ws[q];
+                if (active[m] && alt > dus[q][m]) f(m, ks[q], us[q], dus[q][m], alt);
+            }
+        }
+    }
+}
+
+template <int M, int INFL>
+__device__ __forceinline__ bool relax_item_m(int64_t e, int32_t n, int32_t lane, const int32_t* __restrict__ srcv,
+                                             const DevGraph& G, const State& st, const Flags& fl) {
+    constexpr int L = WAVE * M;
+    int32_t g = 0, v = 0, k0 = 0, k1 = 0;
+    if (e >= 0) {
+        g = (int32_t)(e / n);
+        v = (int32_t)(e - (int64_t)g * n);
+        k0 = G.iptr[v];
+        k1 = G.iptr[v + 1];
+    }
+    Best b[M];
+    int32_t s[M];
+    double d_old[M];
+    bool active[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const int32_t j = lane + m * WAVE;
+        s[m] = e >= 0 ? srcv[g * L + j] : -1;
+        const size_t rv = sidx<L>(g, n, v, j);
+        d_old[m] = e >= 0 ? st.D[rv] : INF;
+        const int32_t p = d_old[m] < INF ? PK_UNREAD : -1;
+        b[m] = Best{d_old[m], p, -1, -1.0, false, p, rv};
+        active[m] = (e >= 0) && (s[m] != -1) && (s[m] != v);
+    }
+    int32_t u_last = 0, orev_last = 0;
+    bool heavy_last = false, ok_last = false;
+    for (int32_t c0 = k0; c0 < k1; c0 += WAVE) {   // wave-uniform trip count
+        const int32_t k = c0 + lane;
+        const bool ok = k < k1;
+        const int4 pk = ok ? G.ipack[k] : make_int4(0, 0, 0, 0);
+        const int32_t u_j = pk.x;
+        const double w_j = __hiloint2double(pk.w, pk.z);
+        const size_t fo = (size_t)g * G.nrel + k;
+        const bool f = ok && fl.in_cur[fo] != 0;
+        if (G.undirected && ok) {
+            orev_last = pk.y & 0x7FFFFFFF;
+            heavy_last = pk.y < 0;
+        }
+        u_last = u_j;
+        ok_last = ok;
+        if (f) fl.in_cur[fo] = 0;   // consumed
+        const uint64_t sm = __ballot(f);
+        scan_chunk_m<M, INFL>(sm, c0, u_j, w_j, g, n, lane, active, st,
+                              [&](int m, int32_t kk, int32_t u, double du, double alt) {
+                                  offer<L>(b[m], G, st, g, n, lane + m * WAVE, kk, u, du, alt);
+                              });
+    }
+    bool changed = false;
+    if (e >= 0) {
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+            changed |= finish_vertex<L>(b[m], G, st, g, n, lane + m * WAVE, v, s[m], b[m].rv, d_old[m]);
+    }
+    if (__ballot(changed)) {
+        if (G.undirected && k1 - k0 <= WAVE) {
+            if (ok_last) {
+                (heavy_last ? fl.hmark_next : fl.mark_next)[(size_t)g * n + u_last] = 1;
+                fl.in_next[(size_t)g * G.nrel + orev_last] = 1;
+            }
+        } else {
+            mark_out<WAVE>(G, g, n, v, lane, fl);
+        }
+    }
+    return changed;
+}
+
+template <int M, int INFL, int OCC = 1>
+__global__ __launch_bounds__(BLOCK, OCC) void k_relax_m(int32_t total, int32_t n, const int32_t* __restrict__ srcv,
+                                                      DevGraph G, State st, Flags fl) {
+    if (*fl.prev_changed == 0) return;
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    uint64_t* words = reinterpret_cast<uint64_t*>(fl.mark_cur);
+    const int64_t all_units = ((int64_t)total + 7) >> 3;
+    const int32_t xcd = blockIdx.x & 7;
+    const int64_t waves_per_xcd = ((int64_t)(gridDim.x >> 3) * BLOCK) >> 6;
+    const int64_t wave = ((int64_t)(blockIdx.x >> 3) * BLOCK + threadIdx.x) >> 6;
+    const int64_t lo = all_units * xcd / 8, hi = all_units * (xcd + 1) / 8;
+    bool wrote = false;
+    int64_t u8 = lo + wave;
+    uint64_t w_ahead = u8 < hi ? words[u8] : 0;
+    for (; u8 < hi; u8 += waves_per_xcd) {
+        const uint64_t w = uniform_u64(w_ahead);
+        const int64_t nx = u8 + waves_per_xcd;
+        w_ahead = nx < hi ? words[nx] : 0;
+        if (!w) continue;
+        if (lane == 0) words[u8] = 0;   // taken
+        for (uint32_t bm = byte_mask(w); bm; bm &= bm - 1) {
+            int64_t e = u8 * 8 + __builtin_ctz(bm);
+            if (e >= total) e = -1;
+            wrote |= relax_item_m<M, INFL>(e, n, lane, srcv, G, st, fl);
+        }
+    }
+    if (__ballot(wrote) && lane == 0) *fl.any_changed = 1;
+}
+
+template <int M, int INFL>
+__global__ __launch_bounds__(BLOCK) void k_heavy_partial_m(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
+                                                           DevGraph G, State st, HeavyPlan hp, Partial pp, Flags fl) {
+    if (*fl.prev_changed == 0) return;
+    constexpr int L = WAVE * M;
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int64_t nw = ((int64_t)gridDim.x * BLOCK) >> 6;
+    const int64_t items = (int64_t)groups * hp.nseg;
+    const int64_t first = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    for (int64_t it = first; it < items; it += nw) {   // wave-uniform
+        const int32_t g = (int32_t)(it / hp.nseg);
+        const int32_t sgi = (int32_t)(it - (int64_t)g * hp.nseg);
+        const int32_t v = hp.seg_vertex[sgi];
+        if (!fl.hmark_cur[(size_t)g * n + v]) continue;
+        const int32_t kb = hp.seg_begin[sgi];
+        const int32_t ke = min(kb + WAVE, G.iptr[v + 1]);
+        bool active[M];
+        double ba[M], bdu[M];
+        int32_t bu[M], bk[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const int32_t s = srcv[g * L + lane + m * WAVE];
+            active[m] = (s != -1) && (s != v);
+            ba[m] = INF;
+            bdu[m] = INF;
+            bu[m] = -1;
+            bk[m] = -1;
+        }
+        const int32_t k = kb + lane;
+        const bool ok = k < ke;
+        const int4 pk = ok ? G.ipack[k] : make_int4(0, 0, 0, 0);
+        const size_t fo = (size_t)g * G.nrel + k;
+        const bool f = ok && fl.in_cur[fo] != 0;
+        if (f) fl.in_cur[fo] = 0;
+        scan_chunk_m<M, INFL>(__ballot(f), kb, pk.x, __hiloint2double(pk.w, pk.z), g, n, lane, active, st,
+                              [&](int m, int32_t kk, int32_t u, double du, double alt) {
+                                  if (alt < ba[m] || (alt == ba[m] && (du < bdu[m] || (du == bdu[m] && u < bu[m])))) {
+                                      ba[m] = alt;
+                                      bdu[m] = du;
+                                      bu[m] = u;
+                                      bk[m] = kk;
+                                  }
+                              });
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const size_t o = ((size_t)g * hp.nseg + sgi) * L + lane + m * WAVE;
+            pp.alt[o] = ba[m];
+            pp.du[o] = bdu[m];
+            pp.uk[o] = make_int2(bu[m], bk[m]);
+        }
+    }
+}
+
+template <int M>
+__global__ __launch_bounds__(BLOCK) void k_heavy_combine_m(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
+                                                           DevGraph G, State st, HeavyPlan hp, Partial pp, Flags fl) {
+    if (*fl.prev_changed == 0) return;
+    constexpr int L = WAVE * M;
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int64_t nw = ((int64_t)gridDim.x * BLOCK) >> 6;
+    const int64_t items = (int64_t)groups * hp.nheavy;
+    const int64_t first = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    bool wrote = false;
+    for (int64_t it = first; it < items; it += nw) {   // wave-uniform
+        const int32_t g = (int32_t)(it / hp.nheavy);
+        const int32_t h = (int32_t)(it - (int64_t)g * hp.nheavy);
+        const int32_t v = hp.heavy_vertex[h];
+        if (!fl.hmark_cur[(size_t)g * n + v]) continue;
+        bool changed = false;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const int32_t j = lane + m * WAVE;
+            const int32_t s = srcv[g * L + j];
+            const size_t rv = sidx<L>(g, n, v, j);
+            const double d_old = st.D[rv];
+            const int32_t p_old = st.P[rv];
+            Best b{d_old, p_old, -1, -1.0, false, p_old, rv};
+            for (int32_t sgi = hp.heavy_seg0[h]; sgi < hp.heavy_seg0[h + 1]; ++sgi) {
+                const size_t o = ((size_t)g * hp.nseg + sgi) * L + j;
+                const int2 uk = pp.uk[o];
+                if (uk.x >= 0) offer<L>(b, G, st, g, n, j, uk.y, uk.x, pp.du[o], pp.alt[o]);
+            }
+            changed |= finish_vertex<L>(b, G, st, g, n, j, v, s, rv, d_old);
+        }
+        if (lane == 0) fl.hmark_cur[(size_t)g * n + v] = 0;
+        if (__ballot(changed)) {
+            mark_out<WAVE>(G, g, n, v, lane, fl);
+            wrote = true;
+        }
+    }
+    if (__ballot(wrote) && lane == 0) *fl.any_changed = 1;
+}
+
 // (s, s) entry: DIRECT self-loop, the row's [s] path, or the SELF rule.
 __device__ __forceinline__ void self_entry(const DevGraph& G, const RowMode& md, int32_t s, double& L_,
                                            double& R, int32_t& N, int32_t& H) {
@@ -812,7 +1046,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
             In& x = in[q];
             x.dc = INF;
             if (x.b >= 0 && x.s >= 0 && x.si.t != x.s) {
-                const int32_t g = x.b * (WAVE / L) + lane / L, j = lane % L;
+                const int32_t g = (x.b * WAVE + lane) / L, j = (x.b * WAVE + lane) % L;
                 const size_t rt = sidx<L>(g, n, x.si.c, j);
                 x.dc = st.D[rt];
                 x.rc = st.RT[rt];
@@ -825,7 +1059,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
             const int32_t b = x.b, jt = x.jt, s = x.s;
             const SlotInfo& si = x.si;
             const int32_t t = si.t;
-            const int32_t g = b * (WAVE / L) + lane / L, j = lane % L;
+            const int32_t g = (b * WAVE + lane) / L, j = (b * WAVE + lane) % L;
             double Lt = -1.0, R = -1.0, AX = -1.0;
             int32_t N = -1, H = 0, PV = -1;
             if (s >= 0) {
@@ -2283,9 +2517,9 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     int32_t lanes = o.lanes_per_group;
     if (lanes <= 0 && getenv("SPE_LANES")) lanes = atoi(getenv("SPE_LANES"));
     if (lanes <= 0) lanes = 64;
-    if (lanes != 16 && lanes != 32 && lanes != 64) {
+    if (lanes != 16 && lanes != 32 && lanes != 64 && lanes != 128 && lanes != 256) {
         delete t;
-        return fail(SPE_EINVAL, "lanes_per_group must be 16, 32 or 64");
+        return fail(SPE_EINVAL, "lanes_per_group must be 16, 32, 64, 128 or 256");
     }
     t->lanes = lanes;
     {
@@ -2319,7 +2553,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     t->infl = lanes == 64 ? 8 : 4;
     if (getenv("SPE_INFL")) {
         const int want = atoi(getenv("SPE_INFL"));
-        if (want == 4 || want == 8 || (lanes == 64 && want == 6)) t->infl = want;
+        if (want == 4 || want == 8 || (lanes == 64 && want == 6) || (lanes == 256 && want == 2)) t->infl = want;
     }
     t->occ = getenv("SPE_OCC") ? atoi(getenv("SPE_OCC")) : 0;
     t->tb.A = n_attached;
@@ -2393,9 +2627,11 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         TRY(dev_alloc(t->allocs, &t->lsc.par, per));
     }
     const size_t G = (size_t)t->groups;
-    const size_t GL = G * (WAVE / t->lanes);   // lane groups per batch
+    // lane groups per batch (L > 64: a group spans L / 64 blocks; an odd tail is padded)
+    const size_t GL = t->lanes <= WAVE ? G * (WAVE / t->lanes) : (G * WAVE + t->lanes - 1) / t->lanes;
+    const size_t GW = GL * (size_t)t->lanes;   // source entries per batch (>= G * 64: padding lanes)
     if (!t->md.complete && t->engine == SPE_ENGINE_BATCH) {
-        const size_t se = G * n * WAVE;
+        const size_t se = GW * n;
         t->overlap = !getenv("SPE_NO_OVERLAP");
         for (int i = 0; i < (t->overlap ? 2 : 1); ++i) {
             TRY(dev_alloc(t->allocs, &t->st_buf[i].D, se));
@@ -2410,7 +2646,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         TRY(dev_alloc(t->allocs, &t->mark[1], (GL * n + 8) & ~(size_t)7));
         TRY(dev_alloc(t->allocs, &t->hmark[0], GL * n));
         TRY(dev_alloc(t->allocs, &t->hmark[1], GL * n));
-        const size_t pe = G * std::max<size_t>(1, (size_t)g->hp.nseg) * WAVE;
+        const size_t pe = GW * std::max<size_t>(1, (size_t)g->hp.nseg);
         TRY(dev_alloc(t->allocs, &t->pp.alt, pe));
         TRY(dev_alloc(t->allocs, &t->pp.du, pe));
         TRY(dev_alloc(t->allocs, &t->pp.uk, pe));
@@ -2418,8 +2654,8 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         TRY(dev_alloc(t->allocs, &t->counts, (size_t)t->max_iters + 2));
     }
     for (int i = 0; i < (t->overlap ? 2 : 1); ++i) {
-        TRY(dev_alloc(t->allocs, &t->srcv_buf[i], G * WAVE));
-        TRY(dev_alloc(t->allocs, &t->srcc_buf[i], G * WAVE));
+        TRY(dev_alloc(t->allocs, &t->srcv_buf[i], GW));
+        TRY(dev_alloc(t->allocs, &t->srcc_buf[i], GW));
     }
     t->d_srcv = t->srcv_buf[0];
     t->d_srcc = t->srcc_buf[0];
@@ -2434,7 +2670,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
             return fail(SPE_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
         }                                                                                  \
     } while (0)
-    HTRY(hipHostMalloc((void**)&t->h_srcv, 2 * G * WAVE * sizeof(int32_t), hipHostMallocDefault));
+    HTRY(hipHostMalloc((void**)&t->h_srcv, 2 * GW * sizeof(int32_t), hipHostMallocDefault));
     HTRY(hipHostMalloc((void**)&t->h_counts, std::max<size_t>(64, (size_t)t->max_iters + 2) * sizeof(int32_t),
                        hipHostMallocDefault));
     HTRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
@@ -2499,14 +2735,17 @@ static int resolve_profile(spe_table* t, bool all = true) {
 extern "C++" {
 template <int L, int INFL, int OCC = 1>
 static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
+    constexpr int M = L > WAVE ? L / WAVE : 1;    // lanes per thread
     const spe_graph* g = t->g;
     const int32_t n = g->hg.nc;
     const int32_t nrel = (int32_t)g->hg.icol.size();
-    const int32_t groups = blocks * (WAVE / L);    // lane groups
+    const int32_t groups = M > 1 ? (blocks + M - 1) / M : blocks * (WAVE / L);    // lane groups
     const int64_t total = (int64_t)groups * n;
     // one resident wave per hardware slot (no second wave of late blocks), multiple of 8 (XCD split)
     int per_cu = 0, cus = 0;
-    const void* kfn = (const void*)k_relax<L, INFL, OCC>;
+    const void* kfn;
+    if constexpr (M > 1) kfn = (const void*)k_relax_m<M, INFL, OCC>;
+    else kfn = (const void*)k_relax<L, INFL, OCC>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, BLOCK, 0) != hipSuccess || per_cu < 1)
         per_cu = 4;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus < 1) cus = 256;
@@ -2529,7 +2768,7 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
         k_seed<L><<<(groups * L + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev, t->mark[1],
                                                                      t->hmark[1], t->inflag[1]);
     }
-    const int64_t subs_per_wave = WAVE / L;
+    const int64_t subs_per_wave = M > 1 ? 1 : WAVE / L;
     // Rounds are enqueued in chunks sized by the previous batch's round count
     // (batches of one graph converge in similar counts); rounds after the
     // converged one exit at once, so one host check per batch is typical.
@@ -2543,16 +2782,26 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
                      t->counts + it - 1};
             {
                 LaunchTimer lt(t, s, SPE_K_RELAX);
-                k_relax<L, INFL, OCC><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev, t->st, fl);
+                if constexpr (M > 1)
+                    k_relax_m<M, INFL, OCC><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev, t->st, fl);
+                else
+                    k_relax<L, INFL, OCC><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev, t->st, fl);
             }
             if (g->hp.nheavy > 0) {
                 LaunchTimer lt(t, s, SPE_K_HEAVY);
                 const int64_t pw = ((int64_t)groups * g->hp.nseg + subs_per_wave - 1) / subs_per_wave;
                 const int64_t cw = ((int64_t)groups * g->hp.nheavy + subs_per_wave - 1) / subs_per_wave;
-                k_heavy_partial<L><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcc, g->dev,
-                                                                                      t->st, g->hp, t->pp, fl);
-                k_heavy_combine<L><<<grid_for(cw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcc, g->dev,
-                                                                                      t->st, g->hp, t->pp, fl);
+                if constexpr (M > 1) {
+                    k_heavy_partial_m<M, INFL><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
+                        groups, n, t->d_srcc, g->dev, t->st, g->hp, t->pp, fl);
+                    k_heavy_combine_m<M><<<grid_for(cw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
+                        groups, n, t->d_srcc, g->dev, t->st, g->hp, t->pp, fl);
+                } else {
+                    k_heavy_partial<L><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcc, g->dev,
+                                                                                          t->st, g->hp, t->pp, fl);
+                    k_heavy_combine<L><<<grid_for(cw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcc, g->dev,
+                                                                                          t->st, g->hp, t->pp, fl);
+                }
             }
         }
         HIP_TRY(hipMemcpyAsync(t->h_counts, t->counts, sizeof(int32_t) * (size_t)it, hipMemcpyDeviceToHost, s));
@@ -2573,6 +2822,11 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
 static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
     const bool deep = t->infl == 8;
     switch (t->lanes) {
+        case 128:
+            if (t->occ == 6) return relax_to_convergence_l<128, 4, 6>(t, blocks, s);
+            return deep ? relax_to_convergence_l<128, 8>(t, blocks, s) : relax_to_convergence_l<128, 4>(t, blocks, s);
+        case 256:
+            return t->infl == 2 ? relax_to_convergence_l<256, 2>(t, blocks, s) : relax_to_convergence_l<256, 4>(t, blocks, s);
         case 16: return deep ? relax_to_convergence_l<16, 8>(t, blocks, s) : relax_to_convergence_l<16, 4>(t, blocks, s);
         case 32: return deep ? relax_to_convergence_l<32, 8>(t, blocks, s) : relax_to_convergence_l<32, 4>(t, blocks, s);
         default:
@@ -2597,6 +2851,8 @@ static void launch_rows_sssp(spe_table* t, int grid, int32_t blocks, int32_t sb0
     switch (t->lanes) {
         case 16: ROWS(16); break;
         case 32: ROWS(32); break;
+        case 128: ROWS(128); break;
+        case 256: ROWS(256); break;
         default: ROWS(64); break;
     }
 #undef ROWS
@@ -2643,15 +2899,19 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
             t->d_srcc = t->srcc_buf[buf];
             if (t->rows_pending[buf]) HIP_TRY(hipStreamWaitEvent(s, t->ev_rows[buf], 0));
         }
-        for (int32_t gi = 0; gi < groups; ++gi)
+        // blocks of source entries: a lane group of L > 64 spans L / 64 blocks, so
+        // an odd tail is padded with empty (-1) blocks
+        const int32_t bpg = std::max(1, t->lanes / WAVE);
+        const int32_t pb = (groups + bpg - 1) / bpg * bpg;
+        for (int32_t gi = 0; gi < pb; ++gi)
             for (int32_t l = 0; l < WAVE; ++l) {
                 const int32_t slot = (b + gi) * WAVE + l;
-                const int32_t v = slot < t->A ? t->attached[slot] : -1;
+                const int32_t v = (gi < groups && slot < t->A) ? t->attached[slot] : -1;
                 t->h_srcv[gi * WAVE + l] = v;
-                t->h_srcv[(groups + gi) * WAVE + l] = v < 0 ? -1 : (g->hg.core_id[v] >= 0 ? g->hg.core_id[v] : -2);
+                t->h_srcv[(pb + gi) * WAVE + l] = v < 0 ? -1 : (g->hg.core_id[v] >= 0 ? g->hg.core_id[v] : -2);
             }
-        HIP_TRY(hipMemcpyAsync(t->d_srcv, t->h_srcv, sizeof(int32_t) * groups * WAVE, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(t->d_srcc, t->h_srcv + groups * WAVE, sizeof(int32_t) * groups * WAVE,
+        HIP_TRY(hipMemcpyAsync(t->d_srcv, t->h_srcv, sizeof(int32_t) * pb * WAVE, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(t->d_srcc, t->h_srcv + pb * WAVE, sizeof(int32_t) * pb * WAVE,
                                hipMemcpyHostToDevice, s));
         const int32_t sb0 = b - t->blk0;
         const int64_t items = (int64_t)groups * t->A;

@@ -312,3 +312,22 @@ def test_partially_built_table_refuses_unbuilt_rows(spe):
             call()
     t.build_blocks(2, t.nblocks)
     assert t.get(200, 3)["latency"] > 0 and t.min_latency() > 0
+
+
+@pytest.mark.engine_fixed
+@pytest.mark.parametrize("lanes", [16, 32, 64, 128, 256])
+def test_lane_group_widths(spe, lanes):
+    """Every lane-group width of the batch engine (L = 128 / 256: each thread
+    carries 2 / 4 sources; an odd block count pads the last group) on a BA graph
+    whose hubs take the heavy-vertex kernels, and on a tiered graph whose stub
+    sources are pruned pendants."""
+    ba = graphs.gen_ba(3000, 3, seed=11)
+    A = np.arange(0, ba.n, 7, dtype=np.int32)[:5 * 64 + 13]     # 6 blocks, ragged
+    ora = Oracle(ba).rows(A, A)
+    for groups in (1, 3):
+        out, _, _ = run_gpu(spe, ba, A, groups=groups, lanes=lanes, engine=spe.SPE_ENGINE_BATCH)
+        compare(out, ora, label=f"ba L={lanes} groups={groups}")
+    tt = graphs.gen_tiered(n_core=1500, n_stub=3000, n_attached=200, seed=5)
+    At = graphs.tiered_attached(tt, n_core=1500, n_attached=200)
+    out, _, _ = run_gpu(spe, tt, At, groups=2, lanes=lanes, engine=spe.SPE_ENGINE_BATCH)
+    compare(out, Oracle(tt).rows(At, At), label=f"tiered L={lanes}")
