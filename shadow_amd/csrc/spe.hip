@@ -1544,14 +1544,24 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
         }
         __syncthreads();
         LDS_PHASE(3)
-        // 4. the parent tree top-down by hop level.  Thread-owned vertices
-        // v = tid + i * LDS_T keep (parent, 1 - p of the parent edge) in registers.
-        // X becomes PF: parent (low 16 bits) | first hop (high 16 bits, 0xFFFF =
-        // none), both relaxation-vertex ids (nc <= LDS_VPT * LDS_T < 2^16).  Each
-        // vertex is read and rewritten by its owning thread only.
+        // 4. hops, first hop and the reliability fold over the parent tree.
+        // Thread-owned vertices v = tid + i * LDS_T keep (parent, 1 - p of the
+        // parent edge) in registers (relaxation-vertex ids: nc <= LDS_VPT * LDS_T
+        // < 2^16).  Hops and first hop are integers, so pointer jumping gets them
+        // exactly in ~log2(depth) rounds: W[v] = (jump << 16) | dist, "jump is
+        // dist hops above v", ends at the terminal vertices (the seed's children
+        // for a core source, the anchor seed for a pruned pendant source), whose
+        // jump is themselves; then jump = the first hop and hops = dist + 1.  The
+        // reliability product must fold in path order, so it runs top-down, one
+        // barrier per hop level, each vertex at the level known from its hops.
+        // X becomes W, then PF: first hop (high 16 bits, 0xFFFF = none) | parent.
         uint32_t* PF = reinterpret_cast<uint32_t*>(X);
+        __shared__ uint32_t s_maxh;
         double pa[LDS_VPT];
+        uint16_t par[LDS_VPT];
+        uint32_t w[LDS_VPT];
         uint32_t todo = 0;
+        const int32_t tpar = sc >= 0 ? seed : -1;   // a parent that makes its child terminal
 #pragma unroll
         for (int i = 0; i < LDS_VPT; ++i) {
             const int32_t v = tid + i * LDS_T;
@@ -1559,62 +1569,82 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
             if (v < nc) {
                 k = X[v];
                 Xg[v] = k;
-                PF[v] = k >= 0 ? (0xFFFF0000u | (uint32_t)par_vertex(G, k)) : 0xFFFFFFFFu;
             }
             pa[i] = k >= 0 ? G.ia[k] : 0.0;
+            par[i] = k >= 0 ? (uint16_t)par_vertex(G, k) : (uint16_t)0;
             if (k >= 0) todo |= 1u << i;
+            w[i] = k < 0 ? ((v == seed && sc < 0) ? ((uint32_t)seed << 16) : 0xFFFFFFFFu)
+                         : ((int32_t)par[i] == tpar ? ((uint32_t)v << 16) : (((uint32_t)par[i] << 16) | 1u));
         }
-        for (int32_t v = tid; v < nc; v += LDS_T) H[v] = 0xFFFF;
-        __syncthreads();
-        if (tid == 0) {
-            const double fs = G.vfac[s];
-            const double r0 = has_attr(fs) ? 1.0 * fs : 1.0;   // shd-topology.c:1428-1430
-            Rl[seed] = sc >= 0 ? r0 : r0 * G.fia[G.fiptr[s]];
-            PF[seed] = sc >= 0 ? 0xFFFFFFFFu : (((uint32_t)seed << 16) | 0xFFFFu);
-            H[seed] = sc >= 0 ? 0 : 1;
+        if (tid == 0) s_maxh = 0;
+        __syncthreads();   // every X read before W overwrites it
+        uint32_t act = 0;
+#pragma unroll
+        for (int i = 0; i < LDS_VPT; ++i) {
+            const int32_t v = tid + i * LDS_T;
+            if (v < nc) PF[v] = w[i];
+            if (((todo >> i) & 1u) && (w[i] >> 16) != (uint32_t)v) act |= 1u << i;
         }
         __syncthreads();
         LDS_PHASE(4)
         {
-            // No barrier per hop level: every thread retries its unsettled vertices
-            // until each one's parent has settled (H[p] != 0xFFFF), then settles it
-            // from the parent's final values.  Progress: the unsettled vertex with
-            // the smallest distance has a settled parent (d[p] < d[v]), and its
-            // owner always gets to retry it, so some thread settles a vertex in
-            // every pass.  Parent fields are published before the parent's H
-            // (workgroup release / acquire on LDS).
-            volatile uint16_t* Hv = H;
-            uint16_t par[LDS_VPT];
+            auto wload = [&](uint32_t j) -> uint32_t {
+                return __hip_atomic_load(PF + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            };
+            // in place and asynchronous: any (jump, dist) pair read is valid, so
+            // composing with a newer one only shortens the chain
+            for (;;) {
+                uint32_t wj[LDS_VPT];
 #pragma unroll
-            for (int i = 0; i < LDS_VPT; ++i)
-                par[i] = ((todo >> i) & 1u) ? (uint16_t)(PF[tid + i * LDS_T] & 0xFFFFu) : (uint16_t)0;
-            while (todo) {
-                uint32_t ready = 0;
-                uint16_t hp[LDS_VPT];
+                for (int i = 0; i < LDS_VPT; ++i) wj[i] = ((act >> i) & 1u) ? wload(w[i] >> 16) : 0u;
 #pragma unroll
                 for (int i = 0; i < LDS_VPT; ++i) {
-                    hp[i] = ((todo >> i) & 1u) ? Hv[par[i]] : (uint16_t)0xFFFF;
-                    ready |= hp[i] != 0xFFFF ? (1u << i) : 0u;
+                    if (!((act >> i) & 1u)) continue;
+                    const uint32_t j = w[i] >> 16;
+                    if ((wj[i] >> 16) == j) {   // j is terminal: done
+                        act &= ~(1u << i);
+                    } else {
+                        w[i] = (wj[i] & 0xFFFF0000u) | ((w[i] + wj[i]) & 0xFFFFu);
+                        __hip_atomic_store(PF + tid + i * LDS_T, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
                 }
-                if (!ready) continue;
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                if (!wg_any(act != 0, syncix, s_any)) break;
+            }
+            uint32_t hmax = 0;
 #pragma unroll
-                for (int i = 0; i < LDS_VPT; ++i) {
-                    if (!((ready >> i) & 1u)) continue;
-                    const int32_t v = tid + i * LDS_T;
-                    const uint32_t p = par[i];
-                    Rl[v] = Rl[p] * pa[i];
-                    const uint32_t f = ((int32_t)p == sc) ? (uint32_t)v : (PF[p] >> 16);
-                    PF[v] = (f << 16) | p;
+            for (int i = 0; i < LDS_VPT; ++i) {
+                if (!((todo >> i) & 1u)) continue;
+                const int32_t v = tid + i * LDS_T;
+                const uint32_t h = (w[i] & 0xFFFFu) + 1u;
+                H[v] = (uint16_t)h;
+                PF[v] = (w[i] & 0xFFFF0000u) | par[i];
+                w[i] = h;
+                hmax = max(hmax, h);
+            }
+#pragma unroll
+            for (int i = 0; i < LDS_VPT; ++i) {   // no parent: the seed or unreachable
+                const int32_t v = tid + i * LDS_T;
+                if (v < nc && !((todo >> i) & 1u)) {
+                    H[v] = v == seed ? (sc >= 0 ? 0 : 1) : 0xFFFF;
+                    PF[v] = (v == seed && sc < 0) ? (((uint32_t)seed << 16) | 0xFFFFu) : 0xFFFFFFFFu;
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-#pragma unroll
-                for (int i = 0; i < LDS_VPT; ++i)
-                    if ((ready >> i) & 1u) Hv[tid + i * LDS_T] = (uint16_t)(hp[i] + 1);
-                todo &= ~ready;
-                ++nlev;
+            }
+            for (int d = 1; d < WAVE; d <<= 1) hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, d));
+            if (lane == 0 && hmax) atomicMax(&s_maxh, hmax);
+            if (tid == 0) {
+                const double fs = G.vfac[s];
+                const double r0 = has_attr(fs) ? 1.0 * fs : 1.0;   // shd-topology.c:1428-1430
+                Rl[seed] = sc >= 0 ? r0 : r0 * G.fia[G.fiptr[s]];
             }
             __syncthreads();
+            const uint32_t levels = s_maxh;
+            for (uint32_t l = 1; l <= levels; ++l) {
+#pragma unroll
+                for (int i = 0; i < LDS_VPT; ++i)
+                    if (((todo >> i) & 1u) && w[i] == l) Rl[tid + i * LDS_T] = Rl[par[i]] * pa[i];
+                __syncthreads();
+            }
+            nlev = levels;
         }
         LDS_PHASE(5)
         // 5. reliability, next hop, hops (+ latency re-fold for multigraphs)
