@@ -1231,7 +1231,10 @@ constexpr int LDS_T = 1024;                 // threads per workgroup (16 waves)
 constexpr int LDS_WAVES = LDS_T / WAVE;
 constexpr int LDS_MAX_BYTES = 160 * 1024 - 1024;   // dynamic share; the rest covers static __shared__
 constexpr int LDS_WL = 256;                 // per-wave marked-vertex list of the push pass
-constexpr int LDS_WIN = 2;                  // 64-edge windows per global round trip of the push pass
+#ifndef LDS_WIN_N
+#define LDS_WIN_N 2
+#endif
+constexpr int LDS_WIN = LDS_WIN_N;          // 64-edge windows per global round trip of the push pass
 constexpr int LDS_CAND_BYTES = LDS_WAVES * (LDS_WL * 4 + LDS_WIN * WAVE);   // push lists + owner maps (H space)
 
 __host__ __device__ constexpr size_t lds_align(size_t b) { return (b + 15) & ~(size_t)15; }
@@ -1257,18 +1260,26 @@ constexpr int LDS_VPT = 10;
 
 __device__ __forceinline__ int32_t par_vertex(const DevGraph& G, int32_t k) { return G.icol[k]; }
 
+// Inclusive prefix sum over the wave in DPP (row shifts, then the two row
+// broadcasts of the GFX9 DPP set): six VALU ops, where a shuffle-based scan is
+// six dependent ds_bpermute round trips through the LDS crossbar.
+__device__ __forceinline__ int32_t wave_incl_scan(int32_t v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);    // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);    // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);    // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);    // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 // Spread the edges of up to 64 owner lanes (lane l owns `deg` consecutive
 // items) over the wave's lanes, 64 at a time.  body(ok, o, off) runs with the
 // whole wave (so it may shuffle): item `off` of owner lane `o`, ok = a real item.
 template <typename F>
 __device__ __forceinline__ void wave_expand(int32_t lane, int32_t deg, F&& body) {
-    int32_t incl = deg;
-#pragma unroll
-    for (int d = 1; d < WAVE; d <<= 1) {
-        const int32_t y = __shfl_up(incl, d);
-        if (lane >= d) incl += y;
-    }
-    const int32_t total = __shfl(incl, WAVE - 1);
+    const int32_t incl = wave_incl_scan(deg);
+    const int32_t total = __builtin_amdgcn_readlane(incl, WAVE - 1);
     const int32_t excl = incl - deg;
     for (int32_t base = 0; base < total; base += WAVE) {
         const int32_t e = base + lane;
@@ -1375,17 +1386,12 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                     deg = (v + 1 < nc ? X[v + 1] : oend) - k0;
                     dv = D[v];
                 }
-                int32_t incl = deg;
-#pragma unroll
-                for (int d = 1; d < WAVE; d <<= 1) {
-                    const int32_t y = __shfl_up(incl, d);
-                    if (lane >= d) incl += y;
-                }
-                const int32_t total = __shfl(incl, WAVE - 1);
+                const int32_t incl = wave_incl_scan(deg);
+                const int32_t total = __builtin_amdgcn_readlane(incl, WAVE - 1);
                 const int32_t excl = incl - deg;
                 for (int32_t base = 0; base < total; base += LDS_WIN * WAVE) {
                     int32_t x[LDS_WIN];
-                    double cand[LDS_WIN];
+                    double cand[LDS_WIN], du[LDS_WIN];
                     bool ok[LDS_WIN];
                     // owner map of this window: each lane stamps its own edges
                     for (int32_t i = max(excl, base), ie = min(incl, base + LDS_WIN * WAVE); i < ie; ++i)
@@ -1397,12 +1403,17 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                     for (int h = 0; h < LDS_WIN; ++h) {
                         const int32_t e = base + h * WAVE + lane;
                         const int32_t o = e < total ? om[e - base] : 0;
-                        const int32_t k = __shfl(k0, o) + e - __shfl(excl, o);
-                        const double du = __shfl(dv, o);
                         ok[h] = e < total;
-                        x[h] = ok[h] ? G.ocol[k] : 0;
-                        cand[h] = ok[h] ? du + G.ow[k] : 0.0;
+                        // unconditional loads (index clamped): every window's edges
+                        // are in flight together, one wait for all of them
+                        const int32_t kr = __shfl(k0, o) + e - __shfl(excl, o);
+                        const int32_t k = ok[h] ? kr : 0;
+                        du[h] = __shfl(dv, o);
+                        x[h] = G.ocol[k];
+                        cand[h] = G.ow[k];
                     }
+#pragma unroll
+                    for (int h = 0; h < LDS_WIN; ++h) cand[h] += du[h];
 #pragma unroll
                     for (int h = 0; h < LDS_WIN; ++h) {
                         if (!ok[h]) continue;
@@ -1427,12 +1438,7 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                 while (pend) {
                     const bool mine = (pend >> lane) & 1ull;
                     const int32_t c = mine ? __popc(W) : 0;
-                    int32_t incl = c;
-#pragma unroll
-                    for (int d = 1; d < WAVE; d <<= 1) {
-                        const int32_t y = __shfl_up(incl, d);
-                        if (lane >= d) incl += y;
-                    }
+                    const int32_t incl = wave_incl_scan(c);
                     const bool fit = mine && incl <= LDS_WL - cnt;   // a prefix of the pending lanes
                     const uint64_t fm = __ballot(fit);
                     if (!fm) {   // list full: process it, then retry
@@ -1443,7 +1449,7 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                         int32_t pos = cnt + incl - c;
                         for (uint32_t x = W; x; x &= x - 1) wl[pos++] = wi * 32 + __builtin_ctz(x);
                     }
-                    cnt += __shfl(incl, 63 - __builtin_clzll(fm));
+                    cnt += __builtin_amdgcn_readlane(incl, 63 - __builtin_clzll(fm));
                     pend &= ~fm;
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
@@ -1469,6 +1475,9 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
         // One flat pass over the in-CSR registers every valid candidate
         // (fl(d[u] + w) == d[v] > d[u]); a vertex with exactly one takes it, a
         // vertex with several (exact ties) rescans its in-list for argmin (d[u], u).
+        // (Recording the push's improving edge and validating it instead was
+        // measured slower: Gauss-Seidel reads make a vertex re-offer the value it
+        // already gave, so equal offers cannot tell ties apart.)
         for (int32_t v = tid; v < nc; v += LDS_T) X[v] = (v == seed) ? (sc >= 0 ? -1 : -2) : -1;
         for (int32_t w = tid; w < nw; w += LDS_T) {
             F0[w] = 0;   // has a candidate
@@ -1477,20 +1486,23 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
         __syncthreads();
         {
             const int32_t m_rel = G.iptr[nc];
-            constexpr int U = 4;
+#ifndef LDS_PARENT_U
+#define LDS_PARENT_U 8
+#endif
+            constexpr int U = LDS_PARENT_U;
             for (int32_t e0 = tid; e0 < m_rel; e0 += U * LDS_T) {
                 int32_t u[U], v[U];
                 double w[U];
 #pragma unroll
-                for (int q = 0; q < U; ++q) {
-                    const int32_t e = e0 + q * LDS_T;
-                    u[q] = -1;
-                    if (e < m_rel) {
-                        u[q] = G.icol[e];
-                        v[q] = G.irow[e];
-                        w[q] = G.iw[e];
-                    }
+                for (int q = 0; q < U; ++q) {   // unconditional (clamped) loads: all U in flight
+                    const int32_t e = min(e0 + q * LDS_T, m_rel - 1);
+                    u[q] = G.icol[e];
+                    v[q] = G.irow[e];
+                    w[q] = G.iw[e];
                 }
+#pragma unroll
+                for (int q = 0; q < U; ++q)
+                    if (e0 + q * LDS_T >= m_rel) u[q] = -1;
 #pragma unroll
                 for (int q = 0; q < U; ++q) {
                     if (u[q] < 0 || v[q] == seed) continue;
@@ -1527,9 +1539,18 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
         LDS_PHASE(2)
         // 3. latencies (distances are final); unreachable targets complete here
         const int32_t sb_local = slot / WAVE - blk0, lane_s = slot % WAVE;
-        for (int32_t j = tid; j < tb.A; j += LDS_T) {
-            const SlotInfo si = slots[j];
-            if (si.t == s) continue;
+        // Targets go UR at a time: their slot records (and in pass 5 the next-hop
+        // ids) are loaded together, one memory round trip per UR targets.
+        constexpr int UR = 4;
+        for (int32_t j0 = tid; j0 < tb.A; j0 += UR * LDS_T) {
+        SlotInfo sv[UR];
+#pragma unroll
+        for (int q = 0; q < UR; ++q) sv[q] = slots[min(j0 + q * LDS_T, tb.A - 1)];
+#pragma unroll
+        for (int q = 0; q < UR; ++q) {
+            const int32_t j = j0 + q * LDS_T;
+            const SlotInfo& si = sv[q];
+            if (j >= tb.A || si.t == s) continue;
             const size_t o = tidx(sb_local, tb.A, j, lane_s);
             if (Db[si.c] == INF_BITS) {
                 tb.lr[o] = make_double2(-1.0, -1.0);
@@ -1541,6 +1562,7 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                 if (l == 0) l = 1;   // shd-topology.c:1833-1837
                 tb.lr[o].x = l;
             }
+        }
         }
         __syncthreads();
         LDS_PHASE(3)
@@ -1648,8 +1670,21 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
         }
         LDS_PHASE(5)
         // 5. reliability, next hop, hops (+ latency re-fold for multigraphs)
-        for (int32_t j = tid; j < tb.A; j += LDS_T) {
-            const SlotInfo si = slots[j];
+        for (int32_t j0 = tid; j0 < tb.A; j0 += UR * LDS_T) {
+        SlotInfo sv[UR];
+        int32_t nh[UR];
+#pragma unroll
+        for (int q = 0; q < UR; ++q) sv[q] = slots[min(j0 + q * LDS_T, tb.A - 1)];
+#pragma unroll
+        for (int q = 0; q < UR; ++q) {
+            const uint32_t fc = PF[sv[q].c] >> 16;
+            nh[q] = G.corev[fc == 0xFFFFu ? 0u : fc];
+        }
+#pragma unroll
+        for (int q = 0; q < UR; ++q) {
+            const int32_t j = j0 + q * LDS_T;
+            if (j >= tb.A) continue;
+            const SlotInfo& si = sv[q];
             const int32_t t = si.t;
             const size_t o = tidx(sb_local, tb.A, j, lane_s);
             if (t == s) {
@@ -1666,11 +1701,11 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
             const uint16_t hc = H[c];
             if (hc == 0xFFFF) continue;   // unreachable: written in pass 3
             const int32_t Hh = hc + (kt >= 0 ? 1 : 0);
-            const double ft = G.vfac[t];
             double R;
-            if (!has_attr(ft) || ft == 1.0) {
+            if (si.fast) {   // t's vertex factor absent or 1.0
                 R = Rl[c] * si.pa;   // pa = 1.0 for relaxation vertices (exact)
             } else {   // ((1 * fs) * ft) * a1 * a2 ... : the target factor comes second
+                const double ft = G.vfac[t];
                 const double fs = G.vfac[s];
                 double r = 1.0;
                 if (has_attr(fs)) r *= fs;
@@ -1710,9 +1745,10 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
             }
             tb.lr[o].y = R;
             const uint32_t fc = PF[c] >> 16;
-            tb.next[o] = kt >= 0 && hc == 0 ? t : (fc == 0xFFFFu ? -1 : G.corev[fc]);
+            tb.next[o] = kt >= 0 && hc == 0 ? t : (fc == 0xFFFFu ? -1 : nh[q]);
             tb.hops[o] = (uint16_t)Hh;
             if (tb.prev) tb.prev[o] = kt >= 0 ? G.corev[c] : (Xg[c] >= 0 ? G.corev[par_vertex(G, Xg[c])] : s);
+        }
         }
         __syncthreads();
         LDS_PHASE(6)
