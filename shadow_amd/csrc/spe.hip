@@ -94,6 +94,7 @@ struct DevGraph {
     const int4* ipack;       // per in-entry, one 16-B load for the relaxation: {icol, orev | heavy[icol] << 31
                              // (undirected: the out-list is the in-list), iw as two 32-bit halves}
     const int32_t* irow;     // in-CSR entry -> its target vertex (flat edge passes)
+    const uint32_t* ipair;   // nc <= 65535 only (LDS-engine graphs): (irow << 16) | icol, one 4-B load
     const double* iw;
     const double* ia;
     const double* iwrep;
@@ -1478,11 +1479,12 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
         // (Recording the push's improving edge and validating it instead was
         // measured slower: Gauss-Seidel reads make a vertex re-offer the value it
         // already gave, so equal offers cannot tell ties apart.)
+        // Candidate counts are u16 halves of the (idle) H space, bumped by
+        // non-returning LDS adds: a returning atomic per candidate would put an
+        // LDS round trip on every valid in-entry.
+        uint32_t* CNT = reinterpret_cast<uint32_t*>(hs);
         for (int32_t v = tid; v < nc; v += LDS_T) X[v] = (v == seed) ? (sc >= 0 ? -1 : -2) : -1;
-        for (int32_t w = tid; w < nw; w += LDS_T) {
-            F0[w] = 0;   // has a candidate
-            F1[w] = 0;   // has several
-        }
+        for (int32_t w = tid; w < (nc + 1) / 2; w += LDS_T) CNT[w] = 0;
         __syncthreads();
         {
             const int32_t m_rel = G.iptr[nc];
@@ -1496,8 +1498,9 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
 #pragma unroll
                 for (int q = 0; q < U; ++q) {   // unconditional (clamped) loads: all U in flight
                     const int32_t e = min(e0 + q * LDS_T, m_rel - 1);
-                    u[q] = G.icol[e];
-                    v[q] = G.irow[e];
+                    const uint32_t uv = G.ipair[e];   // 12 B per entry instead of 16
+                    u[q] = (int32_t)(uv & 0xFFFFu);
+                    v[q] = (int32_t)(uv >> 16);
                     w[q] = G.iw[e];
                 }
 #pragma unroll
@@ -1509,16 +1512,15 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                     const double du = D[u[q]], dv = D[v[q]];
                     const double alt = du + w[q];
                     if (du < INF && alt == dv && alt > du) {
-                        const uint32_t bit = 1u << (v[q] & 31);
-                        if (atomicOr(&F0[v[q] >> 5], bit) & bit) atomicOr(&F1[v[q] >> 5], bit);
-                        else X[v[q]] = e0 + q * LDS_T;
+                        X[v[q]] = e0 + q * LDS_T;   // the only writer unless the count says tie
+                        atomicAdd(&CNT[v[q] >> 1], 1u << ((v[q] & 1) * 16));
                     }
                 }
             }
         }
         __syncthreads();
         for (int32_t v = tid; v < nc; v += LDS_T) {   // exact ties: canonical argmin (d[u], u)
-            if (!((F1[v >> 5] >> (v & 31)) & 1u)) continue;
+            if (((CNT[v >> 1] >> ((v & 1) * 16)) & 0xFFFFu) < 2u) continue;
             const double dv = D[v];
             double bdu = INF;
             int32_t bu = -1, bk = -1;
@@ -2218,6 +2220,13 @@ static int graph_upload(spe_graph* g) {
             for (int32_t k = h.iptr[v]; k < h.iptr[v + 1]; ++k) irow[k] = v;
         r = dev_upload(g->allocs, irow, &d.irow);
         if (r) return r;
+        d.ipair = nullptr;
+        if (h.nc <= 65535) {
+            std::vector<uint32_t> ip(h.icol.size());
+            for (size_t k = 0; k < ip.size(); ++k) ip[k] = ((uint32_t)irow[k] << 16) | (uint32_t)h.icol[k];
+            r = dev_upload(g->allocs, ip, &d.ipair);
+            if (r) return r;
+        }
     }
     UP(iw, h.iw);
     UP(ia, h.ia);
