@@ -1233,7 +1233,7 @@ constexpr int LDS_WAVES = LDS_T / WAVE;
 constexpr int LDS_MAX_BYTES = 160 * 1024 - 1024;   // dynamic share; the rest covers static __shared__
 constexpr int LDS_WL = 256;                 // per-wave marked-vertex list of the push pass
 #ifndef LDS_WIN_N
-#define LDS_WIN_N 2
+#define LDS_WIN_N 3
 #endif
 constexpr int LDS_WIN = LDS_WIN_N;          // 64-edge windows per global round trip of the push pass
 constexpr int LDS_CAND_BYTES = LDS_WAVES * (LDS_WL * 4 + LDS_WIN * WAVE);   // push lists + owner maps (H space)
@@ -1472,6 +1472,9 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
             nxt = tmp;
         }
         LDS_PHASE(1)
+#ifdef SPE_LDS_PUSH_ONLY   // timing build (tools/gpu_pushonly.sh): the push alone, no rows
+        continue;
+#endif
         // 2. canonical parents: X[v] = in-CSR entry, -1 none (source), -2 pendant seed.
         // One flat pass over the in-CSR registers every valid candidate
         // (fl(d[u] + w) == d[v] > d[u]); a vertex with exactly one takes it, a
