@@ -1597,7 +1597,7 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
                 k = X[v];
                 Xg[v] = k;
             }
-            pa[i] = k >= 0 ? G.ia[k] : 0.0;
+            pa[i] = (double)k;   // the parent entry for now; its factor is loaded below
             par[i] = k >= 0 ? (uint16_t)par_vertex(G, k) : (uint16_t)0;
             if (k >= 0) todo |= 1u << i;
             w[i] = k < 0 ? ((v == seed && sc < 0) ? ((uint32_t)seed << 16) : 0xFFFFFFFFu)
@@ -1614,6 +1614,10 @@ __global__ __launch_bounds__(LDS_T) void k_sssp_lds(int32_t slot0, int32_t slot1
         }
         __syncthreads();
         LDS_PHASE(4)
+        // parent-edge factors: requested here, first needed by the level pass, so
+        // their latency hides behind the pointer jumping (unconditional, clamped)
+#pragma unroll
+        for (int i = 0; i < LDS_VPT; ++i) pa[i] = G.ia[((todo >> i) & 1u) ? (int32_t)pa[i] : 0];
         {
             auto wload = [&](uint32_t j) -> uint32_t {
                 return __hip_atomic_load(PF + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
