@@ -115,8 +115,8 @@ typedef struct spe_table_opts {
     int32_t engine;                 /* SPE_ENGINE_* */
     int32_t lanes_per_group;        /* sources sharing one relaxation frontier: 16, 32, 64, 128
                                      * or 256 (128 / 256: each thread carries 2 / 4 sources);
-                                     * 0 = default (64: 128 is within box-to-box noise of it on
-                                     * C3 / C4, 16 / 32 / 256 are slower) */
+                                     * 0 = default: 128 when groups_per_launch is even (no
+                                     * padding lanes; C3 +2 % over 64), else 64 */
     int32_t want_aux;               /* 1: also fold the graph's auxiliary edge attribute
                                      * (spe_graph_set_edge_aux) along every row's path, in path
                                      * order from 0.0 -- the offline completion tool's jitter sum

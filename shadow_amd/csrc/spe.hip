@@ -2598,7 +2598,10 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     // sources per lane group (shared frontier); 64/L groups per 64-source block
     int32_t lanes = o.lanes_per_group;
     if (lanes <= 0 && getenv("SPE_LANES")) lanes = atoi(getenv("SPE_LANES"));
-    if (lanes <= 0) lanes = 64;
+    // default: 128 sources per relaxation row (2 per thread) when every full build
+    // launch covers an even number of 64-source blocks (no padding lanes), else 64.
+    // Same-box A/B, three pairs: C3 +1.4..2.1 %, C4 within +-0.5 %.
+    if (lanes <= 0) lanes = (t->groups >= 2 && t->groups % 2 == 0) ? 128 : 64;
     if (lanes != 16 && lanes != 32 && lanes != 64 && lanes != 128 && lanes != 256) {
         delete t;
         return fail(SPE_EINVAL, "lanes_per_group must be 16, 32, 64, 128 or 256");
