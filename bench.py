@@ -417,7 +417,10 @@ def bench_table(args, rank, world, local, dist):
     b_relax, b_rows = relax_bytes(info, A, lds, direct)
     roof, extra = None, {}
     if kp is not None:
-        kname = "k_sssp_lds" if lds else ("k_rows_direct" if direct else "k_relax")
+        # the batch engine's relaxation kernel: k_relax (<= 64 sources per row) or
+        # k_relax_m (128 / 256: several sources per thread)
+        relax_k = "k_relax_m" if t.layout()["lanes_per_group"] > 64 else "k_relax"
+        kname = "k_sssp_lds" if lds else ("k_rows_direct" if direct else relax_k)
         rl = kp["lds" if lds else ("direct" if direct else "relax")]
         relax_s = rl["ms"] / 1e3
         done = built * steps   # this rank's sources (the profile is this rank's launches)
@@ -428,6 +431,7 @@ def bench_table(args, rank, world, local, dist):
                 "traffic": pmc_traffic(args, kname), "launches": rl["launches"],
                 "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
                 "algorithmic_bytes_per_source": b_relax,
+                "lanes_per_group": t.layout()["lanes_per_group"],
                 "bytes_basis": "relaxation graph: 12 m_relax + 28 n_relax + 8 (SURVEY 8d B_s minus the row stage)"}
         rw = kp["rows"]
         rows_s = rw["ms"] / 1e3

@@ -167,6 +167,7 @@ typedef struct spe_table_layout {
                                      * replica of ALL blocks (padded to n_devices equal shares),
                                      * next_hop / hops are NULL (they stay with each share's device) */
     int32_t device;                 /* the device latrel lives on */
+    int32_t lanes_per_group;        /* batch engine: sources per relaxation row (64 or 128 by default) */
 } spe_table_layout;
 
 typedef struct spe_entry {

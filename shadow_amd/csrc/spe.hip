@@ -3119,6 +3119,7 @@ int spe_table_layout_get(const spe_table* t, spe_table_layout* out) {
     out->hops = t->tb.hops;
     out->groups_per_launch = t->groups;
     out->engine = t->engine;
+    out->lanes_per_group = t->lanes;
     return SPE_OK;
 }
 

@@ -324,6 +324,7 @@ int multi_layout(const MultiDev* m, spe_table_layout* out) {
     out->hops = nullptr;
     out->groups_per_launch = p.groups_per_launch;
     out->engine = p.engine;
+    out->lanes_per_group = p.lanes_per_group;
     out->n_devices = m->n;
     out->device = m->devs[0];
     return SPE_OK;

@@ -58,7 +58,8 @@ class TableLayout(C.Structure):
     _fields_ = [("n_attached", C.c_int32), ("block_begin", C.c_int32), ("block_end", C.c_int32),
                 ("elems", C.c_int64), ("latrel", C.c_void_p),
                 ("next_hop", C.c_void_p), ("hops", C.c_void_p), ("groups_per_launch", C.c_int32),
-                ("engine", C.c_int32), ("n_devices", C.c_int32), ("device", C.c_int32)]
+                ("engine", C.c_int32), ("n_devices", C.c_int32), ("device", C.c_int32),
+                ("lanes_per_group", C.c_int32)]
 
 
 class Entry(C.Structure):
