@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import platform
 import subprocess
@@ -313,11 +314,22 @@ def relax_bytes(info, A, lds: bool, direct: bool):
     return b_relax, b_rows
 
 
-def auto_groups(info) -> int:
-    """spe_table_create's default groups per launch (spe.hip): ~2.4M (group,
-    vertex) rows per relaxation round, capped at 64 groups and 6 GB of state."""
+def auto_groups(info, nblk: int, A: int, world: int, dev) -> int:
+    """spe_table_create's default groups per launch (spe.hip): ~10M (group,
+    vertex) rows per relaxation round, within the free HBM next to the table
+    (state held twice for the rows / relaxation overlap, 4 GB kept free).  At
+    N > 1 the chunk is also cut so that every rank runs >= 4 rounds: a round's
+    all-gather then overlaps the next round's build."""
+    import torch
     n = max(1, info["n_relax_vertices"])
-    return int(max(1.0, min(64.0, round(2.4e6 / n), 6.0e9 / (n * 64 * 28.0))))
+    per_group = 2.0 * (n * 64 * 28.0 + 4.0 * n + 2.0 * info["n_relax_entries"])
+    free_b, _ = torch.cuda.mem_get_info(dev)
+    table_b = float(nblk) * A * 64 * 22.0
+    cap = max(1.0, (free_b - table_b - 4.0e9) / per_group)
+    want = max(1.0, min(round(1.0e7 / n), cap))
+    if world > 1:
+        want = min(want, math.ceil(nblk / (world * 4)))
+    return int(max(1, want))
 
 
 def bench_table(args, rank, world, local, dist):
@@ -346,7 +358,7 @@ def bench_table(args, rank, world, local, dist):
     probe.close()
     # one chunk = one build launch: the LDS engine covers every block in one launch,
     # the batch engine `groups` blocks (auto rule: ~2.4M (group, vertex) rows per round)
-    gpl = nblk if lds_engine else (args.groups if args.groups > 0 else auto_groups(info))
+    gpl = nblk if lds_engine else (args.groups if args.groups > 0 else auto_groups(info, nblk, A, world, dev))
     from shadow_amd import dist as sd
     shares = max(world, args.shares)
     emulated = shares != world   # one rank of a `shares`-GPU job: its chunks only, no gather

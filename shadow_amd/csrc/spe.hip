@@ -2584,24 +2584,44 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     t->md.self_mode = o.self_mode;
     t->md.multi_rep = g->hg.multi_rep;
     t->md.directed = g->hg.directed;
-    // groups per launch: ~2.4M (group, vertex) rows per relaxation round keep every
-    // CU busy through a round's tail (measured: C3 50k -> 48, +12 % over a fixed 16,
-    // +2 % over 24; C4's 20k core -> 64, +2 % over 60); state per group = n * 64 * 28 B, within
-    // 6 GB (held twice: the rows of one batch overlap the next batch's relaxation)
+    // groups per launch: ~10M (group, vertex) rows per relaxation round.  Fewer,
+    // larger batches cut the rounds a table takes (each batch converges in ~the
+    // same count) and the near-empty tail rounds of each batch.  Same-box sweeps
+    // (tools/gpu_groups_big.sh): C3 46 / 98 / 196 / 261 / 391 / 782 groups ->
+    // 89-94k / 98.9k / 101.5k / 102.3k / 98.5k / 98.8k sources/s (one or two
+    // batches lose the rows / relaxation overlap); C4 64 / 196 / 391 -> 278k /
+    // 315k / 335k.  Batches are balanced; the state (n * 64 * 28 B per group, held
+    // twice: the rows of one batch overlap the next batch's relaxation) must fit
+    // the device's free HBM next to the table (the table and 4 GB kept free).
     int32_t groups = o.groups_per_launch;
+    const int32_t owned = std::max(1, t->blk1 - t->blk0);
     if (groups <= 0) {
-        const double per_group = (double)n * WAVE * 28.0;
-        const double want = std::round(2.4e6 / std::max(1, n));
-        groups = (int32_t)std::max(1.0, std::min({64.0, want, 6.0e9 / per_group}));
+        const double per_group = 2.0 * ((double)n * WAVE * 28.0 + 4.0 * n + 2.0 * (double)g->hg.icol.size());
+        double want = std::max(1.0, std::round(1.0e7 / std::max(1, n)));
+        size_t free_b = 0, total_b = 0;
+        if (hipSetDevice(g->device) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
+            const bool ext = o.ext_latrel || o.ext_next_hop || o.ext_hops;
+            const double rec = 22.0 + (o.owner_rank ? 4.0 : 0.0) + (o.want_aux ? 8.0 : 0.0);
+            const double table_b = ext ? 0.0 : (double)owned * n_attached * WAVE * rec;
+            const double budget = (double)free_b - table_b - 4.0e9;
+            want = std::min(want, std::max(1.0, budget / per_group));
+        } else {
+            want = std::min(want, 6.0e9 / per_group);
+        }
+        const int32_t w = (int32_t)std::min<double>(want, owned);
+        const int32_t batches = (owned + w - 1) / w;
+        groups = (owned + batches - 1) / batches;
+        if (groups > 1 && groups % 2 && groups + 1 <= w) ++groups;   // even: no padding lanes at L = 128
     }
-    t->groups = std::max(1, std::min(groups, std::max(1, t->blk1 - t->blk0)));
+    t->groups = std::max(1, std::min(groups, owned));
     // sources per lane group (shared frontier); 64/L groups per 64-source block
     int32_t lanes = o.lanes_per_group;
     if (lanes <= 0 && getenv("SPE_LANES")) lanes = atoi(getenv("SPE_LANES"));
     // default: 128 sources per relaxation row (2 per thread) when every full build
-    // launch covers an even number of 64-source blocks (no padding lanes), else 64.
+    // launch covers an even or a large block count, else 64.
     // Same-box A/B, three pairs: C3 +1.4..2.1 %, C4 within +-0.5 %.
-    if (lanes <= 0) lanes = (t->groups >= 2 && t->groups % 2 == 0) ? 128 : 64;
+    // (an odd launch pads one block of empty lanes: 1 / (groups + 1) extra work)
+    if (lanes <= 0) lanes = (t->groups >= 2 && (t->groups % 2 == 0 || t->groups >= 32)) ? 128 : 64;
     if (lanes != 16 && lanes != 32 && lanes != 64 && lanes != 128 && lanes != 256) {
         delete t;
         return fail(SPE_EINVAL, "lanes_per_group must be 16, 32, 64, 128 or 256");
