@@ -1016,8 +1016,18 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
                                                      const SlotInfo* __restrict__ slots, DevGraph G,
                                                      RowMode md, State st, Table tb) {
     const int32_t lane = threadIdx.x & (WAVE - 1);
-    const int64_t nwaves = ((int64_t)gridDim.x * BLOCK) >> 6;
-    const int64_t items = (int64_t)blocks * tb.A;
+    const int64_t items_all = (int64_t)blocks * tb.A;
+    // XCD-contiguous slices (grid a multiple of 8; workgroups are dealt round-robin
+    // over the 8 XCDs): one XCD's waves take consecutive items, so targets that
+    // share a pendant anchor (adjacent slots) read that anchor's state row from
+    // the same L2 instead of one XCD each.
+    const bool xs = (gridDim.x & 7) == 0;
+    const int32_t xcd = xs ? (int32_t)(blockIdx.x & 7) : 0;
+    const int64_t nwaves = xs ? (((int64_t)(gridDim.x >> 3) * BLOCK) >> 6) : (((int64_t)gridDim.x * BLOCK) >> 6);
+    const int64_t lo = xs ? items_all * xcd / 8 : 0;
+    const int64_t items = xs ? items_all * (xcd + 1) / 8 : items_all;
+    const int64_t wave0 = xs ? ((((int64_t)(blockIdx.x >> 3) * BLOCK + threadIdx.x) >> 6))
+                             : ((((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6));
     // Two items per trip: every load both need (slot constants, source, the
     // target row's distance and route) is issued before either one's stores,
     // so a trip waits for two memory round trips, not four.
@@ -1028,7 +1038,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
         Route rc;
     };
     constexpr int NI = ROWS_ITEMS;
-    for (int64_t it0 = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it0 < items; it0 += NI * nwaves) {
+    for (int64_t it0 = lo + wave0; it0 < items; it0 += NI * nwaves) {
         In in[NI];
 #pragma unroll
         for (int q = 0; q < NI; ++q) {
