@@ -710,6 +710,50 @@ __device__ __forceinline__ void scan_chunk_m(uint64_t sm, int32_t c0, int32_t u_
     }
 }
 
+// finish_vertex for the M lanes a thread carries: every lane's parent id, then
+// every lane's parent route / edge factor / old route, are requested together,
+// so the M lanes wait for two memory round trips instead of 2 M.
+template <int M>
+__device__ __forceinline__ bool finish_vertex_m(Best (&b)[M], const DevGraph& G, const State& st, int32_t g, int32_t n,
+                                                int32_t lane, int32_t v, const int32_t (&s)[M],
+                                                const double (&d_old)[M]) {
+    constexpr int L = WAVE * M;
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+        if (b[m].need && b[m].bu < 0) b[m].bu = G.icol[b[m].bk];
+    Route pu[M], old[M];
+    double ia[M];
+    bool same[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        same[m] = false;
+        if (b[m].need) {
+            pu[m] = st.RT[sidx<L>(g, n, b[m].bu, lane + m * WAVE)];
+            ia[m] = G.ia[b[m].bk];
+            // need with bd == d_old implies an equal offer, which read the stored parent
+            same[m] = !(d_old[m] == INF || b[m].bd != d_old[m] || b[m].bk != b[m].pold);
+            if (same[m]) old[m] = st.RT[b[m].rv];
+        }
+    }
+    bool changed = false;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        if (!b[m].need) continue;
+        Route nr;
+        nr.r = pu[m].r * ia[m];
+        nr.h = pu[m].h + 1;
+        nr.f = (b[m].bu == s[m]) ? G.corev[v] : pu[m].f;
+        const bool ch = !same[m] || nr.r != old[m].r || nr.h != old[m].h || nr.f != old[m].f;
+        if (ch) {
+            st.D[b[m].rv] = b[m].bd;
+            st.P[b[m].rv] = b[m].bk;
+            st.RT[b[m].rv] = nr;
+        }
+        changed |= ch;
+    }
+    return changed;
+}
+
 template <int M, int INFL>
 __device__ __forceinline__ bool relax_item_m(int64_t e, int32_t n, int32_t lane, const int32_t* __restrict__ srcv,
                                              const DevGraph& G, const State& st, const Flags& fl) {
@@ -760,9 +804,13 @@ __device__ __forceinline__ bool relax_item_m(int64_t e, int32_t n, int32_t lane,
     }
     bool changed = false;
     if (e >= 0) {
+        if (G.ablate) {   // diagnostic builds only
 #pragma unroll
-        for (int m = 0; m < M; ++m)
-            changed |= finish_vertex<L>(b[m], G, st, g, n, lane + m * WAVE, v, s[m], b[m].rv, d_old[m]);
+            for (int m = 0; m < M; ++m)
+                changed |= finish_vertex<L>(b[m], G, st, g, n, lane + m * WAVE, v, s[m], b[m].rv, d_old[m]);
+        } else {
+            changed = finish_vertex_m<M>(b, G, st, g, n, lane, v, s, d_old);
+        }
     }
     if (__ballot(changed)) {
         if (G.undirected && k1 - k0 <= WAVE) {
