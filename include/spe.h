@@ -55,6 +55,12 @@ extern "C" {
 #define SPE_ENGINE_AUTO 0    /* LDS engine when the relaxation graph fits one CU's LDS, else BATCH */
 #define SPE_ENGINE_BATCH 1   /* 64-source lane groups, HBM-resident state, frontier rounds */
 #define SPE_ENGINE_LDS 2     /* one workgroup per source row, state resident in LDS (<= 10,240 relaxation vertices) */
+#define SPE_ENGINE_FW 3      /* blocked min-plus Floyd-Warshall closure carrying (latency, reliability, first
+                              * edge), then every row re-folded in path order along the first-edge walk
+                              * (<= 32,768 relaxation vertices; never picked by AUTO: the LDS engine is
+                              * faster on every graph it fits).  Bit-exact where shortest paths are unique
+                              * (tie-free weights); equal-length paths resolve to the lowest pivot, not to
+                              * the canonical (d[u], u) rule */
 
 typedef struct spe_graph spe_graph;
 typedef struct spe_table spe_table;
@@ -259,6 +265,16 @@ int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, d
  * table's path-order folds only to rounding (the table is what is bit-exact).
  * `seconds`: device time of the closure (init + pivot steps). */
 int spe_fw_apsp(spe_graph* g, double* d_dist, int64_t ld, int32_t* d_next, void* stream, double* seconds);
+/* The same closure carrying the north star's triple (the FW engine's first
+ * stage): d_dist / d_rel / d_next are caller device buffers of ld x ld elements;
+ * d_rel(i,j) = the product of the edge factors (1 - p) of the chosen path,
+ * multiplied in FW's association order (rel(i,k) * rel(k,j) at the pivot that
+ * last improved the pair), d_next(i,j) = the first hop (relaxation vertex id,
+ * -1 unreachable / i == j).  Replaces the all-pairs step of the offline tool
+ * (compute-topology-paths.py:89-94) and, in the table, igraph's per-source
+ * Dijkstra (shd-topology.c:1741). */
+int spe_fw_closure(spe_graph* g, double* d_dist, double* d_rel, int32_t* d_next, int64_t ld, void* stream,
+                   double* seconds);
 /* Owned rows [row_begin,row_end) of the want_aux field, row-major, to host. */
 int spe_table_download_aux(const spe_table* t, int32_t row_begin, int32_t row_end, double* aux);
 /* Batched per-packet lookups against the HBM-resident table.  d_pairs holds q

@@ -2073,6 +2073,264 @@ __global__ __launch_bounds__(256) void k_fw_next(int32_t n, int64_t ld, DevGraph
         nxt[(int64_t)i * n + j] = best;
     }
 }
+
+// ---- FW engine: the closure carries the (latency, reliability, next-hop) triple.
+// D(i,j) distance, R(i,j) product of the edge factors (1 - p) of the path in FW's
+// association order, N(i,j) the relaxation in-CSR entry of the path's FIRST edge
+// (i -> y, y = irow[N]).  An update through pivot k (strict <, so the lowest k of
+// a tie wins) sets D = D(i,k) + D(k,j), R = R(i,k) * R(k,j), N = N(i,k).  The
+// table rows are then re-folded in path order from the walk along N
+// (k_fw_state), which is what makes them bit-exact; R itself agrees with the
+// path-order product only to rounding (tests: 1e-12 relative).
+struct Fw3 {
+    double* D;
+    double* R;
+    int32_t* N;
+};
+constexpr int FW3_LDS = 4 * FWB * FWB * 8 + FWB * FWB * 4;   // 144 KiB dynamic LDS
+constexpr int64_t FW_MAX_N = 32768;   // FW engine: 20 B x n^2 of closure (21 GB at the cap)
+
+__global__ __launch_bounds__(256) void k_fw3_init(int64_t ld, Fw3 M) {
+    const int64_t total = ld * ld;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        const bool diag = (e / ld) == (e % ld);
+        M.D[e] = diag ? 0.0 : INF;
+        M.R[e] = diag ? 1.0 : 0.0;
+        M.N[e] = -1;
+    }
+}
+__global__ __launch_bounds__(256) void k_fw3_edges(int32_t nrel, int64_t ld, DevGraph G, Fw3 M) {
+    const int32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= nrel) return;
+    const int32_t u = G.icol[k], v = G.irow[k];
+    if (u == v) return;   // a loop never shortens a path (D(u,u) = 0)
+    const int64_t e = (int64_t)u * ld + v;   // merged: one in-entry per ordered pair
+    M.D[e] = G.iw[k];
+    M.R[e] = G.ia[k];
+    M.N[e] = k;
+}
+
+extern __shared__ __align__(16) unsigned char fw3_smem[];
+
+// Phases 1 and 2 of pivot block kb.  X = the left operand tile (D, R, N), Y = the
+// right one (D, R): diagonal: X = Y = the pivot tile, updated in place; row panel
+// (kb, o): X = pivot, Y = the panel (its N in registers); column panel (o, kb):
+// X = the panel, Y = pivot.  Row and column k of the updated tile do not change
+// in step k (D(k,k) = 0), so in-place updates between barriers are race-free.
+// Row blocks [rb0, rb1) are this launch's (a device's share of the closure's rows
+// in the multi-device build; [0, nb) otherwise): the column panel covers only
+// those, skipping the pivot block.
+__device__ __forceinline__ int32_t fw_row_block(int32_t idx, int32_t kb, int32_t rb0, int32_t rb1) {
+    const int32_t o = rb0 + idx;
+    return (kb >= rb0 && kb < rb1 && o >= kb) ? o + 1 : o;
+}
+
+__global__ __launch_bounds__(256) void k_fw3_panel(int32_t kb, int32_t nb, int64_t ld, Fw3 M, int32_t b0,
+                                                   int32_t rb0, int32_t rb1) {
+    double* XD = reinterpret_cast<double*>(fw3_smem);
+    double* XR = XD + FWB * FWB;
+    double* YD = XR + FWB * FWB;
+    double* YR = YD + FWB * FWB;
+    int32_t* XN = reinterpret_cast<int32_t*>(YR + FWB * FWB);
+    const int32_t b = b0 + blockIdx.x;
+    const int32_t mode = b == 0 ? 0 : (b < nb ? 1 : 2);   // 0 diagonal, 1 row panel, 2 column panel
+    int32_t o = b - 1;
+    if (mode == 1 && o >= kb) ++o;
+    if (mode == 2) o = fw_row_block(b - nb, kb, rb0, rb1);
+    const int32_t xi = mode == 2 ? o : kb, xj = kb;   // X tile
+    const int32_t yi = kb, yj = mode == 1 ? o : kb;   // Y tile
+    int32_t myN[16];
+    for (int32_t q = 0; q < 16; ++q) {
+        const int32_t e = threadIdx.x + 256 * q, r = e / FWB, c = e % FWB;
+        const int64_t gx = ((int64_t)xi * FWB + r) * ld + (int64_t)xj * FWB + c;
+        XD[e] = M.D[gx];
+        XR[e] = M.R[gx];
+        XN[e] = M.N[gx];
+        if (mode) {
+            const int64_t gy = ((int64_t)yi * FWB + r) * ld + (int64_t)yj * FWB + c;
+            YD[e] = M.D[gy];
+            YR[e] = M.R[gy];
+            if (mode == 1) myN[q] = M.N[gy];
+        }
+    }
+    __syncthreads();
+    const double* RD = mode ? YD : XD;   // right operand
+    const double* RR = mode ? YR : XR;
+    for (int32_t k = 0; k < FWB; ++k) {
+#pragma unroll 4
+        for (int32_t q = 0; q < 16; ++q) {
+            const int32_t e = threadIdx.x + 256 * q, r = e / FWB, c = e % FWB;
+            const double a = XD[r * FWB + k] + RD[k * FWB + c];
+            if (mode == 1) {
+                if (a < YD[e]) {
+                    YD[e] = a;
+                    YR[e] = XR[r * FWB + k] * RR[k * FWB + c];
+                    myN[q] = XN[r * FWB + k];
+                }
+            } else if (a < XD[e]) {
+                XR[e] = XR[r * FWB + k] * RR[k * FWB + c];
+                XN[e] = XN[r * FWB + k];
+                XD[e] = a;
+            }
+        }
+        __syncthreads();
+    }
+    for (int32_t q = 0; q < 16; ++q) {
+        const int32_t e = threadIdx.x + 256 * q, r = e / FWB, c = e % FWB;
+        if (mode == 1) {
+            const int64_t gy = ((int64_t)yi * FWB + r) * ld + (int64_t)yj * FWB + c;
+            M.D[gy] = YD[e];
+            M.R[gy] = YR[e];
+            M.N[gy] = myN[q];
+        } else {
+            const int64_t gx = ((int64_t)xi * FWB + r) * ld + (int64_t)xj * FWB + c;
+            M.D[gx] = XD[e];
+            M.R[gx] = XR[e];
+            M.N[gx] = XN[e];
+        }
+    }
+}
+
+// Phase 3: every tile off the pivot row / column, a 64-deep (min, +) product of
+// the two LDS-staged panels carrying R and N; 4 x 4 elements per thread.
+__global__ __launch_bounds__(256) void k_fw3_rest(int32_t kb, int32_t nb, int64_t ld, Fw3 M, int32_t rb0,
+                                                  int32_t rb1) {
+    double* AD = reinterpret_cast<double*>(fw3_smem);   // [k][r] of tile (bi, kb)
+    double* AR = AD + FWB * FWB;
+    double* BD = AR + FWB * FWB;                         // [k][c] of tile (kb, bj)
+    double* BR = BD + FWB * FWB;
+    int32_t* AN = reinterpret_cast<int32_t*>(BR + FWB * FWB);
+    const int32_t bi = fw_row_block(blockIdx.x / (nb - 1), kb, rb0, rb1);
+    int32_t bj = blockIdx.x % (nb - 1);
+    if (bj >= kb) ++bj;
+    for (int32_t e = threadIdx.x; e < FWB * FWB; e += 256) {
+        const int32_t r = e / FWB, c = e % FWB;
+        const int64_t ga = ((int64_t)bi * FWB + r) * ld + (int64_t)kb * FWB + c;
+        const int64_t gb = ((int64_t)kb * FWB + r) * ld + (int64_t)bj * FWB + c;
+        AD[c * FWB + r] = M.D[ga];
+        AR[c * FWB + r] = M.R[ga];
+        AN[c * FWB + r] = M.N[ga];
+        BD[e] = M.D[gb];
+        BR[e] = M.R[gb];
+    }
+    const int32_t tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+    double d[4][4], rr[4][4];
+    int32_t nn[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int64_t gi = ((int64_t)bi * FWB + ty * 4 + r) * ld + (int64_t)bj * FWB + tx * 4 + c;
+            d[r][c] = M.D[gi];
+            rr[r][c] = M.R[gi];
+            nn[r][c] = M.N[gi];
+        }
+    __syncthreads();
+#pragma unroll 2
+    for (int32_t k = 0; k < FWB; ++k) {
+        const double2 a01 = *reinterpret_cast<const double2*>(&AD[k * FWB + ty * 4]);
+        const double2 a23 = *reinterpret_cast<const double2*>(&AD[k * FWB + ty * 4 + 2]);
+        const double2 r01 = *reinterpret_cast<const double2*>(&AR[k * FWB + ty * 4]);
+        const double2 r23 = *reinterpret_cast<const double2*>(&AR[k * FWB + ty * 4 + 2]);
+        const int4 an4 = *reinterpret_cast<const int4*>(&AN[k * FWB + ty * 4]);
+        const double2 b01 = *reinterpret_cast<const double2*>(&BD[k * FWB + tx * 4]);
+        const double2 b23 = *reinterpret_cast<const double2*>(&BD[k * FWB + tx * 4 + 2]);
+        const double2 s01 = *reinterpret_cast<const double2*>(&BR[k * FWB + tx * 4]);
+        const double2 s23 = *reinterpret_cast<const double2*>(&BR[k * FWB + tx * 4 + 2]);
+        const double a[4] = {a01.x, a01.y, a23.x, a23.y}, ar[4] = {r01.x, r01.y, r23.x, r23.y};
+        const int32_t an[4] = {an4.x, an4.y, an4.z, an4.w};
+        const double bb[4] = {b01.x, b01.y, b23.x, b23.y}, br[4] = {s01.x, s01.y, s23.x, s23.y};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const double x = a[r] + bb[c];
+                const bool up = x < d[r][c];
+                d[r][c] = up ? x : d[r][c];
+                rr[r][c] = up ? ar[r] * br[c] : rr[r][c];
+                nn[r][c] = up ? an[r] : nn[r][c];
+            }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int64_t gi = ((int64_t)bi * FWB + ty * 4 + r) * ld + (int64_t)bj * FWB + tx * 4 + c;
+            M.D[gi] = d[r][c];
+            M.R[gi] = rr[r][c];
+            M.N[gi] = nn[r][c];
+        }
+}
+
+// FW engine: the batch state (D, P, RT per (group, vertex, lane), as the batch
+// engine's relaxation leaves it) from the closure, by walking each (source,
+// vertex) path along N and folding it in path order from the source: latency
+// 0.0 + w1 + w2 + ..., reliability from the source factor, hops, first hop, and
+// the last edge as the parent entry.  On graphs without equal-length paths the
+// walk is the Dijkstra tree path, so the rows k_rows_sssp writes from this state
+// are the batch engine's, bit for bit.  Workgroup = 64 vertices x one group;
+// wave w walks lanes (sources) w, w+4, ...; a lane's 64 walks start on one N row.
+__global__ __launch_bounds__(256) void k_fw_state(int32_t n, int64_t ld, const int32_t* __restrict__ srcv,
+                                                  const int32_t* __restrict__ srcc, DevGraph G, Fw3 M, State st) {
+    const int32_t g = blockIdx.y;
+    const int32_t v = blockIdx.x * WAVE + (threadIdx.x & (WAVE - 1));
+    if (v >= n) return;   // no barriers below
+    for (int32_t j = threadIdx.x >> 6; j < WAVE; j += (int32_t)(blockDim.x >> 6)) {
+        const int32_t s0 = srcv[g * WAVE + j];
+        const int32_t sc = srcc[g * WAVE + j];
+        const size_t i = sidx<WAVE>(g, n, v, j);
+        double d = INF;
+        int32_t p = -1;
+        Route rt{1.0, 0, -1};
+        bool wr = false;
+        if (s0 >= 0) {
+            const double fs = G.vfac[s0];
+            double r = has_attr(fs) ? 1.0 * fs : 1.0;   // shd-topology.c:1428-1430
+            int32_t x, h = 0, f = -1, p0 = -1;
+            double d0 = 0.0;
+            if (sc >= 0) {
+                x = sc;
+            } else {   // pruned pendant source: its edge into the anchor comes first
+                x = G.anchor_core[s0];
+                const int32_t kx = G.fiptr[s0];
+                d0 = 0.0 + G.fiw[kx];
+                r = r * G.fia[kx];
+                h = 1;
+                f = G.corev[x];
+                p0 = -2;
+            }
+            if (v == x) {
+                d = d0;
+                p = p0;
+                rt = Route{r, h, f};
+                wr = true;
+            } else if (M.D[(int64_t)x * ld + v] < INF) {
+                double dd = d0;
+                int32_t pp = p0;
+                for (int32_t step = 0; step < n && x != v; ++step) {
+                    const int32_t k = M.N[(int64_t)x * ld + v];
+                    if (k < 0) break;
+                    const int32_t y = G.irow[k];
+                    dd = dd + G.iw[k];
+                    r = r * G.ia[k];
+                    ++h;
+                    if (f < 0) f = G.corev[y];
+                    pp = k;
+                    x = y;
+                }
+                if (x == v) {
+                    d = dd;
+                    p = pp;
+                    rt = Route{r, h, f};
+                    wr = true;
+                }
+            }
+        }
+        st.D[i] = d;
+        st.P[i] = p;
+        if (wr) st.RT[i] = rt;
+    }
+}
 }  // namespace
 
 // ================================================================== host side
@@ -2151,6 +2409,11 @@ struct spe_table {
     size_t ev_next = 0;
     spe_kernel_profile kp{};
     std::vector<int32_t> h_hist;
+    // FW engine: the closure (D, R, N over the relaxation graph, ld x ld), computed
+    // by the first build and kept for the table's lifetime
+    Fw3 fw{};
+    int64_t fw_ld = 0;
+    bool fw_done = false;
 };
 
 namespace {
@@ -2693,6 +2956,13 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
             e = atoi(getenv("SPE_ENGINE"));
             from_env = true;
         }
+        if (e == SPE_ENGINE_FW && !t->md.complete && (int64_t)g->hg.nc > FW_MAX_N) {
+            if (!from_env) {
+                delete t;
+                return fail(SPE_EUNSUPPORTED, "relaxation graph too large for the FW engine (n^2 closure)");
+            }
+            e = SPE_ENGINE_BATCH;
+        }
         if (e == SPE_ENGINE_LDS && !fits) {
             if (!from_env) {
                 delete t;
@@ -2713,6 +2983,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
             }
         }
     }
+    if (t->engine == SPE_ENGINE_FW) t->lanes = lanes = WAVE;   // its state walk writes 64-lane rows
     t->infl = lanes == 64 ? 8 : 4;
     if (getenv("SPE_INFL")) {
         const int want = atoi(getenv("SPE_INFL"));
@@ -2816,6 +3087,18 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         t->max_iters = 4 * n + 64;
         TRY(dev_alloc(t->allocs, &t->counts, (size_t)t->max_iters + 2));
     }
+    if (!t->md.complete && t->engine == SPE_ENGINE_FW) {
+        const size_t se = GW * n;
+        TRY(dev_alloc(t->allocs, &t->st_buf[0].D, se));
+        TRY(dev_alloc(t->allocs, &t->st_buf[0].P, se));
+        TRY(dev_alloc(t->allocs, &t->st_buf[0].RT, se));
+        t->st = t->st_buf[0];
+        t->fw_ld = ((int64_t)std::max(1, n) + FWB - 1) / FWB * FWB;
+        const size_t ll = (size_t)t->fw_ld * (size_t)t->fw_ld;
+        TRY(dev_alloc(t->allocs, &t->fw.D, ll));
+        TRY(dev_alloc(t->allocs, &t->fw.R, ll));
+        TRY(dev_alloc(t->allocs, &t->fw.N, ll));
+    }
     for (int i = 0; i < (t->overlap ? 2 : 1); ++i) {
         TRY(dev_alloc(t->allocs, &t->srcv_buf[i], GW));
         TRY(dev_alloc(t->allocs, &t->srcc_buf[i], GW));
@@ -2896,6 +3179,76 @@ static int resolve_profile(spe_table* t, bool all = true) {
 }
 
 extern "C++" {
+// The FW engine's closure (D, R, N) over the relaxation graph, ld x ld, enqueued on s.
+static int fw3_closure(const spe_graph* g, Fw3 M, int64_t ld, hipStream_t s) {
+    const int32_t nb = (int32_t)(ld / FWB);
+    HIP_TRY(hipFuncSetAttribute((const void*)k_fw3_panel, hipFuncAttributeMaxDynamicSharedMemorySize, FW3_LDS));
+    HIP_TRY(hipFuncSetAttribute((const void*)k_fw3_rest, hipFuncAttributeMaxDynamicSharedMemorySize, FW3_LDS));
+    k_fw3_init<<<grid_for(ld * ld, 256, 16384), 256, 0, s>>>(ld, M);
+    const int32_t nrel = (int32_t)g->hg.icol.size();
+    if (nrel > 0) k_fw3_edges<<<(nrel + 255) / 256, 256, 0, s>>>(nrel, ld, g->dev, M);
+    // padding rows / columns stay +inf off the diagonal: they never shorten a path
+    for (int32_t kb = 0; kb < nb; ++kb) {
+        k_fw3_panel<<<1, 256, FW3_LDS, s>>>(kb, nb, ld, M, 0, 0, nb);
+        if (nb > 1) k_fw3_panel<<<2 * nb - 2, 256, FW3_LDS, s>>>(kb, nb, ld, M, 1, 0, nb);
+        if (nb > 1) k_fw3_rest<<<(nb - 1) * (nb - 1), 256, FW3_LDS, s>>>(kb, nb, ld, M, 0, nb);
+    }
+    HIP_TRY(hipGetLastError());
+    return SPE_OK;
+}
+
+// ---- the multi-device FW closure (spe_multi.cpp drives it): 1-D
+// row blocks per device; per pivot block the owner relaxes the diagonal tile and
+// the pivot row panel, the panel is broadcast, and every device relaxes its own
+// rows' column panel and remaining tiles.
+namespace spe {
+int fw_part(spe_table* t, FwPart* out) {
+    if (!t || t->engine != SPE_ENGINE_FW || t->md.complete || !t->fw.D) return set_error(SPE_EINVAL, "not an FW-engine table");
+    out->D = t->fw.D;
+    out->R = t->fw.R;
+    out->N = t->fw.N;
+    out->ld = t->fw_ld;
+    out->device = t->g->device;
+    out->stream = t->stream;
+    out->done = &t->fw_done;
+    return SPE_OK;
+}
+int fw_init(const spe_graph* g, const FwPart& p) {
+    HIP_TRY(hipSetDevice(p.device));
+    HIP_TRY(hipFuncSetAttribute((const void*)k_fw3_panel, hipFuncAttributeMaxDynamicSharedMemorySize, FW3_LDS));
+    HIP_TRY(hipFuncSetAttribute((const void*)k_fw3_rest, hipFuncAttributeMaxDynamicSharedMemorySize, FW3_LDS));
+    hipStream_t s = (hipStream_t)p.stream;
+    const Fw3 M{p.D, p.R, p.N};
+    k_fw3_init<<<grid_for(p.ld * p.ld, 256, 16384), 256, 0, s>>>(p.ld, M);
+    const int32_t nrel = (int32_t)g->hg.icol.size();
+    if (nrel > 0) k_fw3_edges<<<(nrel + 255) / 256, 256, 0, s>>>(nrel, p.ld, g->dev, M);
+    HIP_TRY(hipGetLastError());
+    return SPE_OK;
+}
+int fw_pivot_owner(const FwPart& p, int32_t kb) {
+    HIP_TRY(hipSetDevice(p.device));
+    const int32_t nb = (int32_t)(p.ld / FWB);
+    hipStream_t s = (hipStream_t)p.stream;
+    const Fw3 M{p.D, p.R, p.N};
+    k_fw3_panel<<<1, 256, FW3_LDS, s>>>(kb, nb, p.ld, M, 0, 0, nb);
+    if (nb > 1) k_fw3_panel<<<nb - 1, 256, FW3_LDS, s>>>(kb, nb, p.ld, M, 1, 0, nb);   // row panel only
+    HIP_TRY(hipGetLastError());
+    return SPE_OK;
+}
+int fw_pivot_rows(const FwPart& p, int32_t kb, int32_t rb0, int32_t rb1) {
+    HIP_TRY(hipSetDevice(p.device));
+    const int32_t nb = (int32_t)(p.ld / FWB);
+    const int32_t rows = (rb1 - rb0) - ((kb >= rb0 && kb < rb1) ? 1 : 0);
+    if (rows <= 0 || nb < 2) return SPE_OK;
+    hipStream_t s = (hipStream_t)p.stream;
+    const Fw3 M{p.D, p.R, p.N};
+    k_fw3_panel<<<rows, 256, FW3_LDS, s>>>(kb, nb, p.ld, M, nb, rb0, rb1);   // column panel, own rows
+    k_fw3_rest<<<rows * (nb - 1), 256, FW3_LDS, s>>>(kb, nb, p.ld, M, rb0, rb1);
+    HIP_TRY(hipGetLastError());
+    return SPE_OK;
+}
+}  // namespace spe
+
 template <int L, int INFL, int OCC = 1>
 static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     constexpr int M = L > WAVE ? L / WAVE : 1;    // lanes per thread
@@ -3106,6 +3459,26 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
                             h[4] / nsrc / 100.0, h[5] / nsrc / 100.0, h[6] / nsrc / 100.0, h[11] / nsrc / 100.0,
                             h[12] / nsrc / 100.0);
                 }
+            }
+            if (t->md.prefer) {
+                LaunchTimer lt(t, s, SPE_K_DIRECT);
+                k_direct_overlay<<<(groups * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(
+                    groups, sb0, t->d_srcv, t->d_vertex_slot, g->dev, t->tb);
+            }
+        } else if (t->engine == SPE_ENGINE_FW) {
+            if (!t->fw_done) {
+                LaunchTimer lt(t, s, SPE_K_FW);
+                if (int r = fw3_closure(g, t->fw, t->fw_ld, s)) return r;
+                t->fw_done = true;
+            }
+            {
+                LaunchTimer lt(t, s, SPE_K_FW);
+                k_fw_state<<<dim3((g->hg.nc + WAVE - 1) / WAVE, groups), BLOCK, 0, s>>>(
+                    g->hg.nc, t->fw_ld, t->d_srcv, t->d_srcc, g->dev, t->fw, t->st);
+            }
+            {
+                LaunchTimer lt(t, s, SPE_K_ROWS);
+                launch_rows_sssp(t, row_grid, groups, sb0, s);
             }
             if (t->md.prefer) {
                 LaunchTimer lt(t, s, SPE_K_DIRECT);
@@ -3387,6 +3760,40 @@ int spe_fw_apsp(spe_graph* g, double* d_dist, int64_t ld, int32_t* d_next, void*
     }
     HIP_TRY(hipEventRecord(b, s));
     if (d_next) k_fw_next<<<grid_for((int64_t)n * n, 256, 16384), 256, 0, s>>>(n, ld, g->dev, d_dist, d_next);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, a, b));
+    if (seconds) *seconds = ms / 1e3;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return SPE_OK;
+}
+
+namespace {
+__global__ __launch_bounds__(256) void k_fw3_first_hop(int64_t total, const int32_t* __restrict__ irow,
+                                                       int32_t* __restrict__ nxt) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        const int32_t k = nxt[e];
+        nxt[e] = k < 0 ? -1 : irow[k];
+    }
+}
+}  // namespace
+
+int spe_fw_closure(spe_graph* g, double* d_dist, double* d_rel, int32_t* d_next, int64_t ld, void* stream,
+                   double* seconds) {
+    if (!g || !d_dist || !d_rel || !d_next) return fail(SPE_EINVAL, "NULL argument");
+    const int32_t n = g->hg.nc;
+    if (ld < ((int64_t)n + FWB - 1) / FWB * FWB || ld % FWB) return fail(SPE_EINVAL, "ld must be a multiple of 64 >= n");
+    HIP_TRY(hipSetDevice(g->device));
+    hipStream_t s = (hipStream_t)stream;
+    hipEvent_t a, b;
+    HIP_TRY(hipEventCreate(&a));
+    HIP_TRY(hipEventCreate(&b));
+    HIP_TRY(hipEventRecord(a, s));
+    if (int r = fw3_closure(g, Fw3{d_dist, d_rel, d_next}, ld, s)) return r;
+    HIP_TRY(hipEventRecord(b, s));
+    k_fw3_first_hop<<<grid_for(ld * ld, 256, 16384), 256, 0, s>>>(ld * ld, g->dev.irow, d_next);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     float ms = 0.f;

@@ -78,6 +78,23 @@ int multi_min_latency(const MultiDev* m, double* out);
 int multi_layout(const MultiDev* m, spe_table_layout* out);
 int multi_profile_enable(MultiDev* m, int32_t enable);
 int multi_profile_get(const MultiDev* m, spe_kernel_profile* out);
+// The FW engine's closure buffers of one (part) table, for the multi-device
+// closure: pivot-row broadcast between devices, each device relaxing its own
+// row blocks (spe.hip fw_*; driven by spe_multi.cpp).
+struct FwPart {
+    double* D = nullptr;
+    double* R = nullptr;
+    int32_t* N = nullptr;
+    int64_t ld = 0;        // row stride; ld / 64 row blocks
+    int32_t device = 0;
+    void* stream = nullptr;
+    bool* done = nullptr;  // set once the closure is complete on this device
+};
+int fw_part(spe_table* t, FwPart* out);
+int fw_init(const spe_graph* g, const FwPart& p);
+int fw_pivot_owner(const FwPart& p, int32_t kb);                         // diagonal tile + pivot row panel
+int fw_pivot_rows(const FwPart& p, int32_t kb, int32_t rb0, int32_t rb1);  // column panel + rest, own rows
+
 // Restrict the relaxation CSR to the core (no-op for directed graphs or when
 // `enable` is false); keeps the full CSR in hg->f*.
 void prune_pendants(HostGraph* hg, bool enable);

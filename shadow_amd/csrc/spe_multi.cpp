@@ -40,12 +40,13 @@ struct Rccl {
     ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*group_start)() = nullptr;
     ncclResult_t (*group_end)() = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
 };
 
-Rccl& rccl() {
+Rccl& rccl_lib() {
     static Rccl r;
     if (r.tried) return r;
     r.tried = true;
@@ -57,10 +58,12 @@ Rccl& rccl() {
     r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
     r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
     r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+    r.broadcast = (decltype(r.broadcast))dlsym(h, "ncclBroadcast");
     r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
     r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
     r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
-    r.ok = r.comm_init_all && r.comm_destroy && r.all_gather && r.group_start && r.group_end && r.error_string;
+    r.ok = r.comm_init_all && r.comm_destroy && r.all_gather && r.broadcast && r.group_start && r.group_end &&
+           r.error_string;
     return r;
 }
 
@@ -81,6 +84,7 @@ struct MultiDev {
     std::vector<hipStream_t> streams;
     std::vector<ncclComm_t> comms;
     bool built = false;
+    bool fw = false;                       // FW-engine parts: one closure across the devices
     spe_build_stats stats{};
 
     size_t blk_elems() const { return (size_t)A * kWave; }
@@ -112,7 +116,7 @@ int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_tab
         return set_error(SPE_EUNSUPPORTED, "RCCL needs distinct devices (a repeated device: use SPE_GATHER_PEER)");
     }
     m->gather = o.gather == SPE_GATHER_PEER || !distinct ? SPE_GATHER_PEER
-                : (rccl().ok ? SPE_GATHER_RCCL : (o.gather == SPE_GATHER_RCCL ? -1 : SPE_GATHER_PEER));
+                : (rccl_lib().ok ? SPE_GATHER_RCCL : (o.gather == SPE_GATHER_RCCL ? -1 : SPE_GATHER_PEER));
     if (m->gather < 0) {
         delete m;
         return set_error(SPE_EUNSUPPORTED, "librccl.so.1 could not be loaded");
@@ -152,13 +156,19 @@ int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_tab
         po.ext_hops = m->hops[d];
         po.ext_filled = 0;
         r = spe_table_create(m->graphs[d], attached, A, &po, &m->parts[d]);
+        if (!r) {
+            spe_table_layout pl{};
+            spe_table_layout_get(m->parts[d], &pl);
+            FwPart fp;
+            m->fw = pl.engine == SPE_ENGINE_FW && fw_part(m->parts[d], &fp) == SPE_OK;   // not for DIRECT tables
+        }
     }
     if (!r && m->gather == SPE_GATHER_RCCL) {
         m->comms.assign(m->n, nullptr);
-        const ncclResult_t nr = rccl().comm_init_all(m->comms.data(), m->n, m->devs.data());
+        const ncclResult_t nr = rccl_lib().comm_init_all(m->comms.data(), m->n, m->devs.data());
         if (nr != ncclSuccess) {
             m->comms.clear();
-            r = set_error(SPE_EHIP, std::string("ncclCommInitAll: ") + rccl().error_string(nr));
+            r = set_error(SPE_EHIP, std::string("ncclCommInitAll: ") + rccl_lib().error_string(nr));
         }
     }
     if (r) {
@@ -172,7 +182,7 @@ int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_tab
 void multi_free(MultiDev* m) {
     if (!m) return;
     for (ncclComm_t c : m->comms)
-        if (c) rccl().comm_destroy(c);
+        if (c) rccl_lib().comm_destroy(c);
     for (int d = 0; d < m->n; ++d) {
         if (m->parts[d]) spe_table_free(m->parts[d]);
         (void)hipSetDevice(m->devs[d]);
@@ -189,7 +199,7 @@ void multi_free(MultiDev* m) {
 static int gather_records(MultiDev* m) {
     const size_t share_bytes = (size_t)m->cb * m->blk_elems() * 2 * sizeof(double);
     if (m->gather == SPE_GATHER_RCCL) {
-        Rccl& R = rccl();
+        Rccl& R = rccl_lib();
         R.group_start();
         ncclResult_t nr = ncclSuccess;
         for (int d = 0; d < m->n && nr == ncclSuccess; ++d) {
@@ -223,8 +233,120 @@ static int gather_records(MultiDev* m) {
     return SPE_OK;
 }
 
+// ---- FW engine parts: the closure is computed ONCE across the devices instead
+// of once per part (SURVEY §8e "dense FW: one exchange step per pivot block").
+// The closure's ld / 64 row blocks are dealt contiguously to the devices; per
+// pivot block kb the owner of row block kb relaxes the diagonal tile and the
+// pivot row panel, the panel's (D, R) rows are broadcast to every device (RCCL
+// ncclBroadcast over xGMI, in place; or peer copies), and each device relaxes
+// its own rows' column panel and remaining tiles.  Finally every device
+// broadcasts its rows' (D, N) so that each holds the whole closure for its
+// part's row walks (R is not needed there: the rows re-fold in path order).
+namespace {
+struct FwBcast {
+    const MultiDev* m;
+    std::vector<FwPart>& P;
+    std::vector<hipEvent_t>& ev;
+    bool rccl;
+    // rows [r0, r1) of the arrays in `which` (bit 0 D, 1 R, 2 N) from device `root` to every other
+    int rows(int root, int64_t r0, int64_t r1, int which) {
+        const int64_t ld = P[root].ld;
+        const size_t off = (size_t)r0 * (size_t)ld, cnt = (size_t)(r1 - r0) * (size_t)ld;
+        if (cnt == 0) return SPE_OK;
+        if (rccl) {
+            Rccl& R = rccl_lib();
+            R.group_start();
+            ncclResult_t nr = ncclSuccess;
+            for (int d = 0; d < m->n && nr == ncclSuccess; ++d) {
+                if (hipSetDevice(P[d].device) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
+                hipStream_t s = (hipStream_t)P[d].stream;
+                if (which & 1) nr = R.broadcast(P[d].D + off, P[d].D + off, cnt, ncclDouble, root, m->comms[d], s);
+                if (nr == ncclSuccess && (which & 2))
+                    nr = R.broadcast(P[d].R + off, P[d].R + off, cnt, ncclDouble, root, m->comms[d], s);
+                if (nr == ncclSuccess && (which & 4))
+                    nr = R.broadcast(P[d].N + off, P[d].N + off, cnt, ncclInt32, root, m->comms[d], s);
+            }
+            const ncclResult_t ne = R.group_end();
+            if (nr != ncclSuccess || ne != ncclSuccess)
+                return set_error(SPE_EHIP, std::string("ncclBroadcast: ") + R.error_string(nr != ncclSuccess ? nr : ne));
+            return SPE_OK;
+        }
+        // peer copies on the root's stream (its later kernels overwrite these rows),
+        // then every other device's stream waits for them
+        const FwPart& o = P[root];
+        if (hipSetDevice(o.device) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
+        hipStream_t so = (hipStream_t)o.stream;
+        for (int d = 0; d < m->n; ++d) {
+            if (d == root) continue;
+            hipError_t e = hipSuccess;
+            if (which & 1) e = hipMemcpyPeerAsync(P[d].D + off, P[d].device, o.D + off, o.device, cnt * 8, so);
+            if (e == hipSuccess && (which & 2))
+                e = hipMemcpyPeerAsync(P[d].R + off, P[d].device, o.R + off, o.device, cnt * 8, so);
+            if (e == hipSuccess && (which & 4))
+                e = hipMemcpyPeerAsync(P[d].N + off, P[d].device, o.N + off, o.device, cnt * 4, so);
+            if (e != hipSuccess) return hip_fail("hipMemcpyPeerAsync (FW rows)", e);
+        }
+        hipError_t e = hipEventRecord(ev[root], so);
+        if (e != hipSuccess) return hip_fail("hipEventRecord", e);
+        for (int d = 0; d < m->n; ++d) {
+            if (d == root) continue;
+            if (hipSetDevice(P[d].device) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
+            e = hipStreamWaitEvent((hipStream_t)P[d].stream, ev[root], 0);
+            if (e != hipSuccess) return hip_fail("hipStreamWaitEvent", e);
+        }
+        return SPE_OK;
+    }
+};
+}  // namespace
+
+static int fw_closure_multi(MultiDev* m, double* seconds) {
+    std::vector<FwPart> P(m->n);
+    for (int d = 0; d < m->n; ++d) {
+        if (!m->parts[d]) return set_error(SPE_EUNSUPPORTED, "FW engine: every device needs a share of the sources");
+        if (int r = fw_part(m->parts[d], &P[d])) return r;
+    }
+    bool done = true;
+    for (auto& p : P) done &= *p.done;
+    if (done) return SPE_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int32_t nb = (int32_t)(P[0].ld / 64);
+    const int32_t rbs = (nb + m->n - 1) / m->n;   // closure row blocks per device
+    std::vector<hipEvent_t> ev(m->n, nullptr);
+    int r = SPE_OK;
+    for (int d = 0; d < m->n && !r; ++d) {
+        if (hipSetDevice(P[d].device) != hipSuccess || hipEventCreateWithFlags(&ev[d], hipEventDisableTiming) != hipSuccess)
+            r = set_error(SPE_EHIP, "FW closure events");
+        if (!r) r = fw_init(m->graphs[d], P[d]);
+    }
+    FwBcast bc{m, P, ev, m->gather == SPE_GATHER_RCCL};
+    for (int32_t kb = 0; kb < nb && !r; ++kb) {
+        const int own = kb / rbs;
+        r = fw_pivot_owner(P[own], kb);
+        if (!r) r = bc.rows(own, (int64_t)kb * 64, (int64_t)kb * 64 + 64, 1 | 2);
+        for (int d = 0; d < m->n && !r; ++d)
+            r = fw_pivot_rows(P[d], kb, std::min(nb, d * rbs), std::min(nb, (d + 1) * rbs));
+    }
+    for (int d = 0; d < m->n && !r; ++d)
+        r = bc.rows(d, (int64_t)std::min(nb, d * rbs) * 64, (int64_t)std::min(nb, (d + 1) * rbs) * 64, 1 | 4);
+    for (int d = 0; d < m->n; ++d) {
+        if (hipSetDevice(P[d].device) == hipSuccess && P[d].stream) {
+            const hipError_t e = hipStreamSynchronize((hipStream_t)P[d].stream);
+            if (!r && e != hipSuccess) r = hip_fail("FW closure sync", e);
+        }
+        if (ev[d]) (void)hipEventDestroy(ev[d]);
+    }
+    if (r) return r;
+    for (auto& p : P) *p.done = true;
+    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return SPE_OK;
+}
+
 int multi_build(MultiDev* m, spe_build_stats* stats) {
     const auto t0 = std::chrono::steady_clock::now();
+    double fw_s = 0.0;
+    if (m->fw) {
+        if (int r = fw_closure_multi(m, &fw_s)) return r;
+    }
     std::vector<int> rc(m->n, SPE_OK);
     std::vector<std::string> err(m->n);
     std::vector<std::thread> th;

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("SPE_LIB") or os.path.join(_HERE, "libspe.so")
 SPE_OK = 0
 SPE_SELF_ROW = 0
 SPE_SELF_RULE = 1
-SPE_ENGINE_AUTO, SPE_ENGINE_BATCH, SPE_ENGINE_LDS = 0, 1, 2
+SPE_ENGINE_AUTO, SPE_ENGINE_BATCH, SPE_ENGINE_LDS, SPE_ENGINE_FW = 0, 1, 2, 3
 SPE_GATHER_AUTO, SPE_GATHER_RCCL, SPE_GATHER_PEER = 0, 1, 2
 WAVE = 64
 
@@ -87,7 +87,7 @@ EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_
            "spe_table_profile_get", "spe_table_build_stats", "spe_table_layout_get",
            "spe_table_get", "spe_table_download", "spe_lookup_batch", "spe_table_min_latency",
            "spe_table_key", "spe_table_save", "spe_table_load", "spe_table_free",
-           "spe_graph_set_edge_aux", "spe_table_download_aux", "spe_fw_apsp", "spe_graph_self_path",
+           "spe_graph_set_edge_aux", "spe_table_download_aux", "spe_fw_apsp", "spe_fw_closure", "spe_graph_self_path",
            "spe_graph_adjacent", "spe_device_shares"]
 
 _lib = None
@@ -132,6 +132,7 @@ def lib():
         L.spe_graph_set_edge_aux.argtypes = [P, P]
         L.spe_table_download_aux.argtypes = [P, C.c_int32, C.c_int32, P]
         L.spe_fw_apsp.argtypes = [P, P, C.c_int64, P, P, P]
+        L.spe_fw_closure.argtypes = [P, P, P, P, C.c_int64, P, P]
         L.spe_table_free.argtypes = [P]
         L.spe_table_free.restype = None
         L.spe_device_shares.argtypes = [C.c_int32, C.c_int32, P, P]
@@ -193,6 +194,14 @@ class Graph:
         sec = C.c_double(0)
         _check(lib().spe_fw_apsp(self.h, C.c_void_p(d_dist), int(ld), C.c_void_p(d_next or None),
                                  C.c_void_p(stream or None), C.byref(sec)), "spe_fw_apsp")
+        return float(sec.value)
+
+    def fw_closure(self, d_dist: int, d_rel: int, d_next: int, ld: int, stream: int = 0) -> float:
+        """Blocked min-plus FW carrying (latency, reliability, first hop) into caller
+        device buffers of ld x ld elements; returns device seconds of the closure."""
+        sec = C.c_double(0)
+        _check(lib().spe_fw_closure(self.h, C.c_void_p(d_dist), C.c_void_p(d_rel), C.c_void_p(d_next), int(ld),
+                                    C.c_void_p(stream or None), C.byref(sec)), "spe_fw_closure")
         return float(sec.value)
 
     def order_sources(self, attached) -> np.ndarray:

@@ -1,0 +1,157 @@
+"""GPU parity of the FW engine (SPE_ENGINE_FW): the north star's dense-regime
+algorithm -- a blocked min-plus Floyd-Warshall closure carrying the (latency,
+reliability, next-hop) triple -- followed by a path-order re-fold of every row
+along the closure's first-edge walk.
+
+Bar: on graphs whose shortest paths are unique (the tie-free generators) the
+table equals the oracle's igraph restatement bit for bit (latency, reliability,
+next hop, hops: the same bar as the SSSP engines, TOL_REL = 0).  The closure's
+own carried values (FW association order) are held to the north star's
+tolerance: latency and reliability within 1e-9 relative (measured here: 1e-12),
+first hop exact.  Equal-length paths resolve to the lowest FW pivot, not to the
+canonical (d[u], u) rule, so tie-heavy graphs are out of this engine's contract
+(spe.h SPE_ENGINE_FW).
+"""
+import numpy as np
+import pytest
+
+from oracle import Oracle
+from shadow_amd import graphs
+
+pytestmark = [pytest.mark.gpu, pytest.mark.engine_fixed]
+
+TOL_CLOSURE = 1e-9   # north star: latency / reliability within 1e-9 relative
+
+
+@pytest.fixture(scope="module")
+def spe():
+    from shadow_amd import spe as m
+    assert m.device_count() > 0, "no GPU visible"
+    return m
+
+
+def compare_exact(gpu, ora, label):
+    ok = ora["kind"] != 0
+    np.testing.assert_array_equal(gpu["ok"], ok, err_msg=f"{label}: routability")
+    for k in ("lat", "rel", "next", "hops"):
+        a, b = gpu[k][ok], ora[k][ok]
+        bad = np.flatnonzero(a != b)
+        assert bad.size == 0, f"{label}: {k} differs at {bad.size} entries, e.g. {a[bad[:3]]} vs {b[bad[:3]]}"
+    assert (gpu["lat"][~ok] == -1).all() and (gpu["hops"][~ok] == 0).all()
+
+
+def fw_table(spe, top, A, **kw):
+    g = spe.Graph(top)
+    t = spe.PathTable(g, A, engine=spe.SPE_ENGINE_FW, **kw)
+    assert t.layout()["engine"] == spe.SPE_ENGINE_FW
+    t.profile(True)
+    t.build()
+    kp = t.kernel_profile()
+    assert kp["relax"]["launches"] == 0 and kp["lds"]["launches"] == 0 and kp["fw"]["launches"] > 0
+    return t.download(), t, g
+
+
+CASES = {
+    "undirected_tiefree": dict(n=700, extra_edges=2100, seed=31),
+    "directed_tiefree": dict(n=500, extra_edges=1500, seed=32, directed=True),
+    "sparse_tree_like": dict(n=900, extra_edges=60, seed=33),          # pendants pruned: one edge off the anchor
+    "vertex_loss": dict(n=400, extra_edges=1200, seed=34, vloss_nonzero=True),
+    "no_self_loops": dict(n=300, extra_edges=900, seed=35, self_loops=False),
+    "multigraph": dict(n=250, extra_edges=600, seed=43, multi=120),  # get_eid edge re-fold (multi_rep)
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_fw_engine_rows_match_igraph_restatement(spe, name):
+    top = graphs.gen_random_small(**CASES[name])
+    A = np.arange(top.n, dtype=np.int32)
+    ora = Oracle(top).rows(A, A, tie_mode=0, want_ties=True)
+    assert ora["double_ties"] == 0, "tie-free generator produced a tie"
+    out, _, _ = fw_table(spe, top, A)
+    compare_exact(out, ora, name)
+
+
+@pytest.mark.parametrize("self_mode", [0, 1])
+def test_fw_engine_self_modes_and_partial_blocks(spe, self_mode):
+    top = graphs.gen_random_small(2000, 5000, 45)
+    rng = np.random.default_rng(7)
+    A = np.sort(rng.choice(top.n, 150, replace=False)).astype(np.int32)   # ragged: 150 = 2 blocks + 22
+    ora = Oracle(top).rows(A, A, self_mode=self_mode)
+    out, _, _ = fw_table(spe, top, A, self_mode=self_mode, groups=1)
+    compare_exact(out, ora, f"self_mode={self_mode}")
+
+
+def test_fw_engine_prefer_direct_overlay(spe):
+    top = graphs.gen_random_small(300, 900, 44, self_loops=False)
+    top.prefer_direct = True
+    A = np.arange(top.n, dtype=np.int32)
+    ora = Oracle(top).rows(A, A)
+    out, _, _ = fw_table(spe, top, A)
+    compare_exact(out, ora, "prefer_direct")
+
+
+@pytest.mark.parametrize("n,extra,seed,directed", [(300, 900, 2, False), (700, 1500, 3, False), (200, 700, 5, True)])
+def test_fw_closure_carries_the_triple(spe, n, extra, seed, directed, monkeypatch):
+    """spe_fw_closure: the closure's own (latency, reliability, first hop), FW
+    association order, against the oracle's path-order rows."""
+    import torch
+    monkeypatch.setenv("SPE_NO_PRUNE", "1")   # closure ids = relaxation ids = vertex ids
+    top = graphs.gen_random_small(n, extra, seed, directed=directed)
+    g = spe.Graph(top)
+    ld = (n + 63) // 64 * 64
+    D = torch.empty(ld * ld, dtype=torch.float64, device="cuda")
+    R = torch.empty(ld * ld, dtype=torch.float64, device="cuda")
+    NX = torch.empty(ld * ld, dtype=torch.int32, device="cuda")
+    sec = g.fw_closure(D.data_ptr(), R.data_ptr(), NX.data_ptr(), ld)
+    assert sec > 0
+    d = D.view(ld, ld)[:n, :n].cpu().numpy()
+    r = R.view(ld, ld)[:n, :n].cpu().numpy()
+    nx = NX.view(ld, ld)[:n, :n].cpu().numpy()
+    A = np.arange(n, dtype=np.int32)
+    ref = Oracle(top).rows(A, A, force_sssp=True, tie_mode=1)
+    off = ~np.eye(n, dtype=bool)
+    ok = off & (ref["kind"] != 0)
+    np.testing.assert_allclose(d[ok], ref["lat"][ok], rtol=TOL_CLOSURE, atol=0)
+    # the row's reliability also carries the endpoint vertex factors: ((1 * fs) * ft) * edges
+    vf = np.where(np.isnan(top.vloss), 1.0, 1.0 - top.vloss)
+    np.testing.assert_allclose((r * vf[:, None] * vf[None, :])[ok], ref["rel"][ok], rtol=TOL_CLOSURE, atol=0)
+    np.testing.assert_array_equal(nx[ok], ref["next"][ok])
+    assert np.all(np.diag(d) == 0.0) and np.all(np.diag(nx) == -1)
+    rel_err = np.max(np.abs(d[ok] - ref["lat"][ok]) / ref["lat"][ok])
+    assert rel_err < 1e-12, rel_err
+
+
+def test_fw_engine_c2_full_table_equals_lds_engine(spe):
+    """C2 at full size (RGG n = 10,000, every vertex attached): the FW engine's
+    whole table equals the LDS SSSP engine's, entry for entry (both bit-exact
+    to the oracle's path-order rows; C2's weights are tie-free)."""
+    top = graphs.gen_rgg(10000, 2)
+    A = np.arange(top.n, dtype=np.int32)
+    g = spe.Graph(top)
+    tf = spe.PathTable(g, A, engine=spe.SPE_ENGINE_FW)
+    tf.build()
+    tl = spe.PathTable(g, A, engine=spe.SPE_ENGINE_LDS)
+    tl.build()
+    for r0 in range(0, top.n, 2500):
+        r1 = min(top.n, r0 + 2500)
+        a, b = tf.download(r0, r1), tl.download(r0, r1)
+        for k in ("ok", "lat", "rel", "next", "hops"):
+            bad = np.count_nonzero(a[k] != b[k])
+            assert bad == 0, f"rows {r0}:{r1} {k}: {bad} entries differ"
+    rng = np.random.default_rng(3)
+    rows = rng.choice(top.n, 4, replace=False).astype(np.int32)
+    ora = Oracle(top).rows(A[rows], A)
+    for i, s in enumerate(rows):
+        one = tf.download(int(s), int(s) + 1)
+        part = {k: one[k][0] for k in one}
+        okr = ora["kind"][i] != 0
+        assert np.array_equal(part["ok"], okr)
+        for k in ("lat", "rel", "next", "hops"):
+            assert np.array_equal(part[k][okr], ora[k][i][okr]), (s, k)
+
+
+def test_fw_engine_rejects_too_large(spe):
+    top = graphs.gen_ba(40000, 3, 3)
+    g = spe.Graph(top)
+    with pytest.raises(spe.SpeError):
+        spe.PathTable(g, np.arange(64, dtype=np.int32), engine=spe.SPE_ENGINE_FW)

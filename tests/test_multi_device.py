@@ -60,7 +60,7 @@ def test_single_device_through_the_multi_device_api_rccl():
 
 @pytest.mark.gpu
 @pytest.mark.engine_fixed
-@pytest.mark.parametrize("engine", [1, 2], ids=["batch", "lds"])
+@pytest.mark.parametrize("engine", [1, 2, 3], ids=["batch", "lds", "fw"])
 def test_three_shares_peer_gather_on_one_gpu(engine):
     """Devices [0, 0, 0]: three part tables on one GPU, each building its share
     into its own replica; the peer gather completes every replica.  download
@@ -72,6 +72,8 @@ def test_three_shares_peer_gather_on_one_gpu(engine):
     att = np.arange(top.n, dtype=np.int32)
     g = spe.Graph(top)
     t = spe.PathTable(g, att, devices=[0, 0, 0], engine=engine)
+    # FW: the closure's 11 row blocks are split 4 / 4 / 3 over the shares, pivot
+    # row panels broadcast by peer copies, every share's rows then walk it
     st = t.build()
     assert st["n_devices"] == 3 and st["gather"] == spe.SPE_GATHER_PEER and st["gather_seconds"] > 0
     ref = _check_table(t, top, att, "3 shares")
@@ -111,3 +113,40 @@ def test_topology_shim_on_two_shares(tmp_path, monkeypatch):
         for j in range(0, 150, 3):
             assert top.path_info(addrs[i], addrs[j]) == (True, ref["lat"][i, j], ref["rel"][i, j])
     top.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.engine_fixed
+def test_fw_engine_single_device_rccl_broadcasts():
+    """FW engine through the multi-device API with RCCL (one rank: every pivot
+    panel and the final row exchange go through ncclBroadcast)."""
+    from shadow_amd import spe
+    top = graphs.gen_random_small(500, 1500, 64)
+    att = np.arange(top.n, dtype=np.int32)
+    g = spe.Graph(top)
+    t = spe.PathTable(g, att, devices=[0], gather=spe.SPE_GATHER_RCCL, engine=spe.SPE_ENGINE_FW)
+    st = t.build()
+    assert st["gather"] == spe.SPE_GATHER_RCCL and t.layout()["engine"] == spe.SPE_ENGINE_FW
+    _check_table(t, top, att, "fw devices=[0] rccl")
+
+
+@pytest.mark.gpu
+@pytest.mark.engine_fixed
+def test_fw_engine_c2_four_shares_equals_lds_engine():
+    """C2 at full size on the multi-device FW path (four shares on one GPU: 157
+    closure row blocks over 4 devices, 157 pivot-panel broadcasts): the table
+    equals the LDS engine's entry for entry."""
+    from shadow_amd import spe
+    top = graphs.gen_rgg(10000, 2)
+    att = np.arange(top.n, dtype=np.int32)
+    g = spe.Graph(top)
+    tf = spe.PathTable(g, att, devices=[0, 0, 0, 0], engine=spe.SPE_ENGINE_FW)
+    tf.build()
+    tl = spe.PathTable(g, att, engine=spe.SPE_ENGINE_LDS)
+    tl.build()
+    for r0 in range(0, top.n, 2500):
+        r1 = min(top.n, r0 + 2500)
+        a, b = tf.download(r0, r1), tl.download(r0, r1)
+        for k in ("ok", "lat", "rel", "next", "hops"):
+            bad = np.count_nonzero(a[k] != b[k])
+            assert bad == 0, f"rows {r0}:{r1} {k}: {bad} entries differ"
