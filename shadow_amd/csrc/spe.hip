@@ -271,6 +271,75 @@ struct Flags {
     const int32_t* prev_changed;   // the previous round's flag: 0 = converged, the round is a no-op
 };
 
+// Delta-stepping schedule (SPE_DELTA=<ms>, experimental): each lane
+// group relaxes only offers below its bucket bound; a row whose lanes saw larger
+// offers is parked (pending) with the smallest of them, and when the group's round
+// changes nothing its bound moves to that offer + Delta and its parked rows are
+// rescanned over every in-edge.  Converges to the same fixpoint (every edge is
+// eventually offered with no bound in the way), so rows are unchanged.
+struct DeltaState {
+    double* bound;               // [lane group] current bucket bound
+    unsigned long long* minrej;  // [lane group] smallest deferred offer (f64 bits) since the last advance
+    uint8_t* pending;            // [lane group][vertex] rows with deferred offers
+    int32_t* gchanged;           // [lane group] some lane of the group changed this round
+};
+
+__device__ __forceinline__ double wave_min_f64(double x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o));
+    return x;
+}
+
+// after a (group, v) item: park it if an offer was deferred, flag the group's change
+__device__ __forceinline__ void delta_note(const DeltaState& ds, int32_t g, int32_t n, int32_t v, double rej,
+                                           bool any, bool item, int32_t lane) {
+    const double r = wave_min_f64(rej);
+    if (item && lane == 0) {
+        if (r < INF) {
+            ds.pending[(size_t)g * n + v] = 1;
+            atomicMin(&ds.minrej[g], (unsigned long long)__double_as_longlong(r));
+        }
+        if (any) ds.gchanged[g] = 1;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_delta_init(int32_t groups, double delta, DeltaState ds) {
+    const int32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= groups) return;
+    ds.bound[g] = delta;
+    ds.minrej[g] = 0x7FF0000000000000ull;   // +inf
+    ds.gchanged[g] = 0;
+}
+
+// After round r: a lane group that changed nothing and has parked rows moves its
+// bound to (smallest deferred offer + Delta) and puts every parked row into round
+// r+1's frontier with all its in-edges flagged.  One workgroup per lane group.
+__global__ __launch_bounds__(BLOCK) void k_delta_advance(int32_t n, int32_t nrel, double delta, DevGraph G,
+                                                         DeltaState ds, uint8_t* mark_next, uint8_t* in_next,
+                                                         int32_t* any_changed) {
+    __shared__ int32_t go;
+    const int32_t g = blockIdx.x;
+    if (threadIdx.x == 0) {
+        const unsigned long long mr = ds.minrej[g];
+        go = ds.gchanged[g] == 0 && mr != 0x7FF0000000000000ull;
+        if (go) {
+            ds.bound[g] = __longlong_as_double((long long)mr) + delta;
+            ds.minrej[g] = 0x7FF0000000000000ull;
+            *any_changed = 1;
+        }
+        ds.gchanged[g] = 0;
+    }
+    __syncthreads();
+    if (!go) return;
+    for (int32_t v = threadIdx.x; v < n; v += BLOCK) {
+        uint8_t* pv = ds.pending + (size_t)g * n + v;
+        if (!*pv) continue;
+        *pv = 0;
+        mark_next[(size_t)g * n + v] = 1;
+        for (int32_t k = G.iptr[v]; k < G.iptr[v + 1]; ++k) in_next[(size_t)g * nrel + k] = 1;
+    }
+}
+
 template <int L>
 __global__ __launch_bounds__(BLOCK) void k_seed(int32_t n, int32_t groups, const int32_t* __restrict__ srcv,
                                                 DevGraph G, uint8_t* mark, uint8_t* hmark, uint8_t* in_flags) {
@@ -419,10 +488,10 @@ __device__ __forceinline__ void mark_out(const DevGraph& G, int32_t g, int32_t n
 // Relaxation of one light (in-degree <= 64) item e = g * n + v by one subgroup
 // (lane j = source g*L + j); e < 0: this subgroup has no item (it still takes
 // part in the wave-wide ballots).  Returns this lane's "changed".
-template <int L, int INFL>
+template <int L, int INFL, bool DELTA = false>
 __device__ __forceinline__ bool relax_item(int64_t e, int32_t n, int32_t j, int32_t base,
                                            const int32_t* __restrict__ srcv, const DevGraph& G, const State& st,
-                                           const Flags& fl) {
+                                           const Flags& fl, const DeltaState& ds) {
     int32_t g = 0, v = 0, k0 = 0, k1 = 0, s = -1;
     double d_old = INF;
     int32_t p_old = -1;
@@ -440,6 +509,8 @@ __device__ __forceinline__ bool relax_item(int64_t e, int32_t n, int32_t j, int3
     }
     const bool active = (e >= 0) && (s != -1) && (s != v);
     Best b{d_old, p_old, -1, -1.0, false, p_old, rv};
+    const double bnd = (DELTA && e >= 0) ? ds.bound[g] : INF;
+    double rej = INF;
     // undirected graphs: the out-list IS the in-list; a single-chunk vertex keeps
     // what marking needs (neighbour, reverse entry, heavy bit) in registers
     int32_t u_last = 0, orev_last = 0;
@@ -461,11 +532,18 @@ __device__ __forceinline__ bool relax_item(int64_t e, int32_t n, int32_t j, int3
         if (f) fl.in_cur[fo] = 0;   // consumed
         const uint64_t sm = (__ballot(f) >> base) & Sub<L>::MASK;
         scan_chunk<L, INFL>(sm, c0, base, u_j, w_j, g, n, j, active, st,
-                            [&](int32_t kk, int32_t u, double du, double alt) { offer<L>(b, G, st, g, n, j, kk, u, du, alt); });
+                            [&](int32_t kk, int32_t u, double du, double alt) {
+                                if (DELTA && alt >= bnd) {   // beyond the group's bucket: deferred
+                                    rej = fmin(rej, alt);
+                                    return;
+                                }
+                                offer<L>(b, G, st, g, n, j, kk, u, du, alt);
+                            });
     }
     bool changed = false;
     if (e >= 0) changed = finish_vertex<L>(b, G, st, g, n, j, v, s, rv, d_old);
     const bool any = ((__ballot(changed) >> base) & Sub<L>::MASK) != 0;
+    if constexpr (DELTA) delta_note(ds, g, n, v, rej, any, e >= 0, j);   // L == 64 only (host-enforced)
     if (any) {
         if (G.undirected && k1 - k0 <= L) {
             if (ok_last) {
@@ -498,9 +576,9 @@ __device__ __forceinline__ uint32_t byte_mask(uint64_t w) {
 // wave).  XCD-aware split (speed only, never correctness): blocks are dealt
 // round-robin over the 8 XCDs, so blocks with equal blockIdx % 8 share an L2;
 // each such class gets one contiguous eighth of the (group, vertex) space.
-template <int L, int INFL, int OCC = 1>
+template <int L, int INFL, int OCC = 1, bool DELTA = false>
 __global__ __launch_bounds__(BLOCK, OCC) void k_relax(int32_t total, int32_t n, const int32_t* __restrict__ srcv,
-                                                 DevGraph G, State st, Flags fl) {
+                                                 DevGraph G, State st, Flags fl, DeltaState ds) {
     if (*fl.prev_changed == 0) return;   // converged: rounds are enqueued ahead of the host's check
     constexpr int V = Sub<L>::V;
     const int32_t lane = threadIdx.x & (WAVE - 1);
@@ -535,7 +613,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_relax(int32_t total, int32_t n, 
             bm = t;
             int64_t e = mine >= 0 ? u8 * 8 + mine : -1;
             if (e >= total) e = -1;
-            wrote |= relax_item<L, INFL>(e, n, j, base, srcv, G, st, fl);
+            wrote |= relax_item<L, INFL, DELTA>(e, n, j, base, srcv, G, st, fl, ds);
         }
     }
     if (__ballot(wrote) && lane == 0) *fl.any_changed = 1;   // at most one plain store per wave
@@ -754,9 +832,10 @@ __device__ __forceinline__ bool finish_vertex_m(Best (&b)[M], const DevGraph& G,
     return changed;
 }
 
-template <int M, int INFL>
+template <int M, int INFL, bool DELTA = false>
 __device__ __forceinline__ bool relax_item_m(int64_t e, int32_t n, int32_t lane, const int32_t* __restrict__ srcv,
-                                             const DevGraph& G, const State& st, const Flags& fl) {
+                                             const DevGraph& G, const State& st, const Flags& fl,
+                                             const DeltaState& ds) {
     constexpr int L = WAVE * M;
     int32_t g = 0, v = 0, k0 = 0, k1 = 0;
     if (e >= 0) {
@@ -779,6 +858,8 @@ __device__ __forceinline__ bool relax_item_m(int64_t e, int32_t n, int32_t lane,
         b[m] = Best{d_old[m], p, -1, -1.0, false, p, rv};
         active[m] = (e >= 0) && (s[m] != -1) && (s[m] != v);
     }
+    const double bnd = (DELTA && e >= 0) ? ds.bound[g] : INF;
+    double rej = INF;
     int32_t u_last = 0, orev_last = 0;
     bool heavy_last = false, ok_last = false;
     for (int32_t c0 = k0; c0 < k1; c0 += WAVE) {   // wave-uniform trip count
@@ -799,6 +880,10 @@ __device__ __forceinline__ bool relax_item_m(int64_t e, int32_t n, int32_t lane,
         const uint64_t sm = __ballot(f);
         scan_chunk_m<M, INFL>(sm, c0, u_j, w_j, g, n, lane, active, st,
                               [&](int m, int32_t kk, int32_t u, double du, double alt) {
+                                  if (DELTA && alt >= bnd) {   // beyond the group's bucket: deferred
+                                      rej = fmin(rej, alt);
+                                      return;
+                                  }
                                   offer<L>(b[m], G, st, g, n, lane + m * WAVE, kk, u, du, alt);
                               });
     }
@@ -812,6 +897,7 @@ __device__ __forceinline__ bool relax_item_m(int64_t e, int32_t n, int32_t lane,
             changed = finish_vertex_m<M>(b, G, st, g, n, lane, v, s, d_old);
         }
     }
+    if constexpr (DELTA) delta_note(ds, g, n, v, rej, __ballot(changed) != 0, e >= 0, lane);
     if (__ballot(changed)) {
         if (G.undirected && k1 - k0 <= WAVE) {
             if (ok_last) {
@@ -825,9 +911,9 @@ __device__ __forceinline__ bool relax_item_m(int64_t e, int32_t n, int32_t lane,
     return changed;
 }
 
-template <int M, int INFL, int OCC = 1>
+template <int M, int INFL, int OCC = 1, bool DELTA = false>
 __global__ __launch_bounds__(BLOCK, OCC) void k_relax_m(int32_t total, int32_t n, const int32_t* __restrict__ srcv,
-                                                      DevGraph G, State st, Flags fl) {
+                                                      DevGraph G, State st, Flags fl, DeltaState ds) {
     if (*fl.prev_changed == 0) return;
     const int32_t lane = threadIdx.x & (WAVE - 1);
     uint64_t* words = reinterpret_cast<uint64_t*>(fl.mark_cur);
@@ -848,7 +934,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_relax_m(int32_t total, int32_t n
         for (uint32_t bm = byte_mask(w); bm; bm &= bm - 1) {
             int64_t e = u8 * 8 + __builtin_ctz(bm);
             if (e >= total) e = -1;
-            wrote |= relax_item_m<M, INFL>(e, n, lane, srcv, G, st, fl);
+            wrote |= relax_item_m<M, INFL, DELTA>(e, n, lane, srcv, G, st, fl, ds);
         }
     }
     if (__ballot(wrote) && lane == 0) *fl.any_changed = 1;
@@ -2414,6 +2500,9 @@ struct spe_table {
     Fw3 fw{};
     int64_t fw_ld = 0;
     bool fw_done = false;
+    // experimental Delta-stepping schedule of the batch engine (SPE_DELTA=<ms> at creation)
+    double delta = 0.0;
+    DeltaState ds{};
 };
 
 namespace {
@@ -3086,6 +3175,15 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         TRY(dev_alloc(t->allocs, &t->pp.uk, pe));
         t->max_iters = 4 * n + 64;
         TRY(dev_alloc(t->allocs, &t->counts, (size_t)t->max_iters + 2));
+        if (getenv("SPE_DELTA") && atof(getenv("SPE_DELTA")) > 0.0 && (t->lanes == 64 || t->lanes == 128)) {
+            t->delta = atof(getenv("SPE_DELTA"));
+            t->max_iters = 64 * n + 4096;   // buckets add rounds
+            TRY(dev_alloc(t->allocs, &t->counts, (size_t)t->max_iters + 2));
+            TRY(dev_alloc(t->allocs, &t->ds.bound, GL));
+            TRY(dev_alloc(t->allocs, &t->ds.minrej, GL));
+            TRY(dev_alloc(t->allocs, &t->ds.gchanged, GL));
+            TRY(dev_alloc(t->allocs, &t->ds.pending, GL * n));
+        }
     }
     if (!t->md.complete && t->engine == SPE_ENGINE_FW) {
         const size_t se = GW * n;
@@ -3249,7 +3347,7 @@ int fw_pivot_rows(const FwPart& p, int32_t kb, int32_t rb0, int32_t rb1) {
 }
 }  // namespace spe
 
-template <int L, int INFL, int OCC = 1>
+template <int L, int INFL, int OCC = 1, bool DELTA = false>
 static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     constexpr int M = L > WAVE ? L / WAVE : 1;    // lanes per thread
     const spe_graph* g = t->g;
@@ -3260,8 +3358,8 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     // one resident wave per hardware slot (no second wave of late blocks), multiple of 8 (XCD split)
     int per_cu = 0, cus = 0;
     const void* kfn;
-    if constexpr (M > 1) kfn = (const void*)k_relax_m<M, INFL, OCC>;
-    else kfn = (const void*)k_relax<L, INFL, OCC>;
+    if constexpr (M > 1) kfn = (const void*)k_relax_m<M, INFL, OCC, DELTA>;
+    else kfn = (const void*)k_relax<L, INFL, OCC, DELTA>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, BLOCK, 0) != hipSuccess || per_cu < 1)
         per_cu = 4;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus < 1) cus = 256;
@@ -3278,11 +3376,16 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
         const dim3 ig(grid_for((int64_t)n * L, BLOCK, std::max(8, 16384 / std::max(1, (int)groups))), groups);
         k_init_state<L><<<ig, BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev.vfac, g->dev, t->st);
     }
+    if constexpr (DELTA) {
+        HIP_TRY(hipMemsetAsync(t->ds.pending, 0, (size_t)total, s));
+        k_delta_init<<<(groups + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(groups, t->delta, t->ds);
+    }
     {
         LaunchTimer lt(t, s, SPE_K_SEED);
         // the sources "changed in round 0": their out-edges form round 1's frontier
+        // (Delta: heavy vertices stay in the light frontier, relaxed by the same kernel)
         k_seed<L><<<(groups * L + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev, t->mark[1],
-                                                                     t->hmark[1], t->inflag[1]);
+                                                                     DELTA ? t->mark[1] : t->hmark[1], t->inflag[1]);
     }
     const int64_t subs_per_wave = M > 1 ? 1 : WAVE / L;
     // Rounds are enqueued in chunks sized by the previous batch's round count
@@ -3296,14 +3399,20 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
             Flags fl{t->mark[it & 1],   t->mark[(it + 1) & 1],   t->hmark[it & 1],
                      t->hmark[(it + 1) & 1], t->inflag[it & 1], t->inflag[(it + 1) & 1], t->counts + it,
                      t->counts + it - 1};
+            if constexpr (DELTA) fl.hmark_next = fl.mark_next;   // heavy rows relaxed by k_relax too
             {
                 LaunchTimer lt(t, s, SPE_K_RELAX);
                 if constexpr (M > 1)
-                    k_relax_m<M, INFL, OCC><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev, t->st, fl);
+                    k_relax_m<M, INFL, OCC, DELTA><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev,
+                                                                                t->st, fl, t->ds);
                 else
-                    k_relax<L, INFL, OCC><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev, t->st, fl);
+                    k_relax<L, INFL, OCC, DELTA><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev,
+                                                                              t->st, fl, t->ds);
             }
-            if (g->hp.nheavy > 0) {
+            if constexpr (DELTA) {
+                k_delta_advance<<<groups, BLOCK, 0, s>>>(n, nrel, t->delta, g->dev, t->ds, fl.mark_next, fl.in_next,
+                                                         t->counts + it);
+            } else if (g->hp.nheavy > 0) {
                 LaunchTimer lt(t, s, SPE_K_HEAVY);
                 const int64_t pw = ((int64_t)groups * g->hp.nseg + subs_per_wave - 1) / subs_per_wave;
                 const int64_t cw = ((int64_t)groups * g->hp.nheavy + subs_per_wave - 1) / subs_per_wave;
@@ -3337,6 +3446,9 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
 
 static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
     const bool deep = t->infl == 8;
+    if (t->delta > 0.0)   // experimental schedule
+        return t->lanes == 128 ? relax_to_convergence_l<128, 4, 1, true>(t, blocks, s)
+                               : relax_to_convergence_l<64, 8, 1, true>(t, blocks, s);
     switch (t->lanes) {
         case 128:
             if (t->occ == 6) return relax_to_convergence_l<128, 4, 6>(t, blocks, s);
