@@ -280,7 +280,7 @@ struct Flags {
 struct DeltaState {
     double* bound;               // [lane group] current bucket bound
     unsigned long long* minrej;  // [lane group] smallest deferred offer (f64 bits) since the last advance
-    uint8_t* pending;            // [lane group][vertex] rows with deferred offers
+    double* pending;             // [lane group][vertex] smallest deferred offer of a parked row (>= 1e300: none)
     int32_t* gchanged;           // [lane group] some lane of the group changed this round
 };
 
@@ -295,8 +295,9 @@ __device__ __forceinline__ void delta_note(const DeltaState& ds, int32_t g, int3
                                            bool any, bool item, int32_t lane) {
     const double r = wave_min_f64(rej);
     if (item && lane == 0) {
-        if (r < INF) {
-            ds.pending[(size_t)g * n + v] = 1;
+        if (r < INF) {   // (g, v) is this wave's alone within a round: plain read-modify-write
+            double* pv = ds.pending + (size_t)g * n + v;
+            *pv = fmin(*pv, r);
             atomicMin(&ds.minrej[g], (unsigned long long)__double_as_longlong(r));
         }
         if (any) ds.gchanged[g] = 1;
@@ -312,32 +313,48 @@ __global__ __launch_bounds__(BLOCK) void k_delta_init(int32_t groups, double del
 }
 
 // After round r: a lane group that changed nothing and has parked rows moves its
-// bound to (smallest deferred offer + Delta) and puts every parked row into round
-// r+1's frontier with all its in-edges flagged.  One workgroup per lane group.
+// bound to (smallest deferred offer + Delta) -- empty buckets are skipped -- and
+// puts the parked rows whose smallest deferred offer is now below the bound into
+// round r+1's frontier with all their in-edges flagged; the others stay parked
+// (their minimum becomes the group's next one).  One workgroup per lane group.
 __global__ __launch_bounds__(BLOCK) void k_delta_advance(int32_t n, int32_t nrel, double delta, DevGraph G,
                                                          DeltaState ds, uint8_t* mark_next, uint8_t* in_next,
                                                          int32_t* any_changed) {
     __shared__ int32_t go;
+    __shared__ double bnd;
+    __shared__ unsigned long long left;
     const int32_t g = blockIdx.x;
     if (threadIdx.x == 0) {
         const unsigned long long mr = ds.minrej[g];
         go = ds.gchanged[g] == 0 && mr != 0x7FF0000000000000ull;
         if (go) {
-            ds.bound[g] = __longlong_as_double((long long)mr) + delta;
-            ds.minrej[g] = 0x7FF0000000000000ull;
+            bnd = __longlong_as_double((long long)mr) + delta;
+            ds.bound[g] = bnd;
             *any_changed = 1;
         }
+        left = 0x7FF0000000000000ull;
         ds.gchanged[g] = 0;
     }
     __syncthreads();
     if (!go) return;
+    double keep = INF;
     for (int32_t v = threadIdx.x; v < n; v += BLOCK) {
-        uint8_t* pv = ds.pending + (size_t)g * n + v;
-        if (!*pv) continue;
-        *pv = 0;
+        double* pv = ds.pending + (size_t)g * n + v;
+        const double p = *pv;
+        if (p >= 1e300) continue;
+        if (p >= bnd) {
+            keep = fmin(keep, p);
+            continue;
+        }
+        *pv = 1e301;
         mark_next[(size_t)g * n + v] = 1;
         for (int32_t k = G.iptr[v]; k < G.iptr[v + 1]; ++k) in_next[(size_t)g * nrel + k] = 1;
     }
+    keep = wave_min_f64(keep);
+    if ((threadIdx.x & (WAVE - 1)) == 0 && keep < INF)
+        atomicMin(&left, (unsigned long long)__double_as_longlong(keep));
+    __syncthreads();
+    if (threadIdx.x == 0) ds.minrej[g] = left;
 }
 
 template <int L>
@@ -3377,7 +3394,7 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
         k_init_state<L><<<ig, BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev.vfac, g->dev, t->st);
     }
     if constexpr (DELTA) {
-        HIP_TRY(hipMemsetAsync(t->ds.pending, 0, (size_t)total, s));
+        HIP_TRY(hipMemsetAsync(t->ds.pending, 0x7F, sizeof(double) * (size_t)total, s));   // 1.4e306: none
         k_delta_init<<<(groups + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(groups, t->delta, t->ds);
     }
     {
