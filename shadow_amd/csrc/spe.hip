@@ -2190,7 +2190,8 @@ struct Fw3 {
     double* R;
     int32_t* N;
 };
-constexpr int FW3_LDS = 4 * FWB * FWB * 8 + FWB * FWB * 4;   // 144 KiB dynamic LDS
+constexpr int FW3_LDS = 4 * FWB * FWB * 8 + FWB * FWB * 4;   // 144 KiB dynamic LDS (panel kernel)
+constexpr int FW3_REST_LDS = FW3_LDS / 2;                      // 72 KiB: the rest kernel stages 32-deep halves
 constexpr int64_t FW_MAX_N = 32768;   // FW engine: 20 B x n^2 of closure (21 GB at the cap)
 
 __global__ __launch_bounds__(256) void k_fw3_init(int64_t ld, Fw3 M) {
@@ -2298,24 +2299,16 @@ __global__ __launch_bounds__(256) void k_fw3_panel(int32_t kb, int32_t nb, int64
 // the two LDS-staged panels carrying R and N; 4 x 4 elements per thread.
 __global__ __launch_bounds__(256) void k_fw3_rest(int32_t kb, int32_t nb, int64_t ld, Fw3 M, int32_t rb0,
                                                   int32_t rb1) {
-    double* AD = reinterpret_cast<double*>(fw3_smem);   // [k][r] of tile (bi, kb)
-    double* AR = AD + FWB * FWB;
-    double* BD = AR + FWB * FWB;                         // [k][c] of tile (kb, bj)
-    double* BR = BD + FWB * FWB;
-    int32_t* AN = reinterpret_cast<int32_t*>(BR + FWB * FWB);
+    // the 64-deep product in two 32-deep halves: 72 KiB of panels, two workgroups per CU
+    constexpr int KH = FWB / 2;
+    double* AD = reinterpret_cast<double*>(fw3_smem);   // [k][r] of tile (bi, kb), this half's k
+    double* AR = AD + KH * FWB;
+    double* BD = AR + KH * FWB;                          // [k][c] of tile (kb, bj)
+    double* BR = BD + KH * FWB;
+    int32_t* AN = reinterpret_cast<int32_t*>(BR + KH * FWB);
     const int32_t bi = fw_row_block(blockIdx.x / (nb - 1), kb, rb0, rb1);
     int32_t bj = blockIdx.x % (nb - 1);
     if (bj >= kb) ++bj;
-    for (int32_t e = threadIdx.x; e < FWB * FWB; e += 256) {
-        const int32_t r = e / FWB, c = e % FWB;
-        const int64_t ga = ((int64_t)bi * FWB + r) * ld + (int64_t)kb * FWB + c;
-        const int64_t gb = ((int64_t)kb * FWB + r) * ld + (int64_t)bj * FWB + c;
-        AD[c * FWB + r] = M.D[ga];
-        AR[c * FWB + r] = M.R[ga];
-        AN[c * FWB + r] = M.N[ga];
-        BD[e] = M.D[gb];
-        BR[e] = M.R[gb];
-    }
     const int32_t tx = threadIdx.x % 16, ty = threadIdx.x / 16;
     double d[4][4], rr[4][4];
     int32_t nn[4][4];
@@ -2328,31 +2321,45 @@ __global__ __launch_bounds__(256) void k_fw3_rest(int32_t kb, int32_t nb, int64_
             rr[r][c] = M.R[gi];
             nn[r][c] = M.N[gi];
         }
-    __syncthreads();
+    for (int32_t h = 0; h < 2; ++h) {
+        if (h) __syncthreads();   // the first half's panels are read
+        for (int32_t e = threadIdx.x; e < KH * FWB; e += 256) {
+            const int32_t r = e / KH, c = e % KH;      // A: row r of the tile, column h*KH + c
+            const int64_t ga = ((int64_t)bi * FWB + r) * ld + (int64_t)kb * FWB + h * KH + c;
+            AD[c * FWB + r] = M.D[ga];
+            AR[c * FWB + r] = M.R[ga];
+            AN[c * FWB + r] = M.N[ga];
+            const int32_t rb = e / FWB, cb = e % FWB;  // B: row h*KH + rb of the pivot panel
+            const int64_t gb = ((int64_t)kb * FWB + h * KH + rb) * ld + (int64_t)bj * FWB + cb;
+            BD[e] = M.D[gb];
+            BR[e] = M.R[gb];
+        }
+        __syncthreads();
 #pragma unroll 2
-    for (int32_t k = 0; k < FWB; ++k) {
-        const double2 a01 = *reinterpret_cast<const double2*>(&AD[k * FWB + ty * 4]);
-        const double2 a23 = *reinterpret_cast<const double2*>(&AD[k * FWB + ty * 4 + 2]);
-        const double2 r01 = *reinterpret_cast<const double2*>(&AR[k * FWB + ty * 4]);
-        const double2 r23 = *reinterpret_cast<const double2*>(&AR[k * FWB + ty * 4 + 2]);
-        const int4 an4 = *reinterpret_cast<const int4*>(&AN[k * FWB + ty * 4]);
-        const double2 b01 = *reinterpret_cast<const double2*>(&BD[k * FWB + tx * 4]);
-        const double2 b23 = *reinterpret_cast<const double2*>(&BD[k * FWB + tx * 4 + 2]);
-        const double2 s01 = *reinterpret_cast<const double2*>(&BR[k * FWB + tx * 4]);
-        const double2 s23 = *reinterpret_cast<const double2*>(&BR[k * FWB + tx * 4 + 2]);
-        const double a[4] = {a01.x, a01.y, a23.x, a23.y}, ar[4] = {r01.x, r01.y, r23.x, r23.y};
-        const int32_t an[4] = {an4.x, an4.y, an4.z, an4.w};
-        const double bb[4] = {b01.x, b01.y, b23.x, b23.y}, br[4] = {s01.x, s01.y, s23.x, s23.y};
+        for (int32_t k = 0; k < KH; ++k) {
+            const double2 a01 = *reinterpret_cast<const double2*>(&AD[k * FWB + ty * 4]);
+            const double2 a23 = *reinterpret_cast<const double2*>(&AD[k * FWB + ty * 4 + 2]);
+            const double2 r01 = *reinterpret_cast<const double2*>(&AR[k * FWB + ty * 4]);
+            const double2 r23 = *reinterpret_cast<const double2*>(&AR[k * FWB + ty * 4 + 2]);
+            const int4 an4 = *reinterpret_cast<const int4*>(&AN[k * FWB + ty * 4]);
+            const double2 b01 = *reinterpret_cast<const double2*>(&BD[k * FWB + tx * 4]);
+            const double2 b23 = *reinterpret_cast<const double2*>(&BD[k * FWB + tx * 4 + 2]);
+            const double2 s01 = *reinterpret_cast<const double2*>(&BR[k * FWB + tx * 4]);
+            const double2 s23 = *reinterpret_cast<const double2*>(&BR[k * FWB + tx * 4 + 2]);
+            const double a[4] = {a01.x, a01.y, a23.x, a23.y}, ar[4] = {r01.x, r01.y, r23.x, r23.y};
+            const int32_t an[4] = {an4.x, an4.y, an4.z, an4.w};
+            const double bb[4] = {b01.x, b01.y, b23.x, b23.y}, br[4] = {s01.x, s01.y, s23.x, s23.y};
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+            for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const double x = a[r] + bb[c];
-                const bool up = x < d[r][c];
-                d[r][c] = up ? x : d[r][c];
-                rr[r][c] = up ? ar[r] * br[c] : rr[r][c];
-                nn[r][c] = up ? an[r] : nn[r][c];
-            }
+                for (int c = 0; c < 4; ++c) {
+                    const double x = a[r] + bb[c];
+                    const bool up = x < d[r][c];
+                    d[r][c] = up ? x : d[r][c];
+                    rr[r][c] = up ? ar[r] * br[c] : rr[r][c];
+                    nn[r][c] = up ? an[r] : nn[r][c];
+                }
+        }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -3298,7 +3305,7 @@ extern "C++" {
 static int fw3_closure(const spe_graph* g, Fw3 M, int64_t ld, hipStream_t s) {
     const int32_t nb = (int32_t)(ld / FWB);
     HIP_TRY(hipFuncSetAttribute((const void*)k_fw3_panel, hipFuncAttributeMaxDynamicSharedMemorySize, FW3_LDS));
-    HIP_TRY(hipFuncSetAttribute((const void*)k_fw3_rest, hipFuncAttributeMaxDynamicSharedMemorySize, FW3_LDS));
+    HIP_TRY(hipFuncSetAttribute((const void*)k_fw3_rest, hipFuncAttributeMaxDynamicSharedMemorySize, FW3_REST_LDS));
     k_fw3_init<<<grid_for(ld * ld, 256, 16384), 256, 0, s>>>(ld, M);
     const int32_t nrel = (int32_t)g->hg.icol.size();
     if (nrel > 0) k_fw3_edges<<<(nrel + 255) / 256, 256, 0, s>>>(nrel, ld, g->dev, M);
@@ -3306,7 +3313,7 @@ static int fw3_closure(const spe_graph* g, Fw3 M, int64_t ld, hipStream_t s) {
     for (int32_t kb = 0; kb < nb; ++kb) {
         k_fw3_panel<<<1, 256, FW3_LDS, s>>>(kb, nb, ld, M, 0, 0, nb);
         if (nb > 1) k_fw3_panel<<<2 * nb - 2, 256, FW3_LDS, s>>>(kb, nb, ld, M, 1, 0, nb);
-        if (nb > 1) k_fw3_rest<<<(nb - 1) * (nb - 1), 256, FW3_LDS, s>>>(kb, nb, ld, M, 0, nb);
+        if (nb > 1) k_fw3_rest<<<(nb - 1) * (nb - 1), 256, FW3_REST_LDS, s>>>(kb, nb, ld, M, 0, nb);
     }
     HIP_TRY(hipGetLastError());
     return SPE_OK;
@@ -3331,7 +3338,7 @@ int fw_part(spe_table* t, FwPart* out) {
 int fw_init(const spe_graph* g, const FwPart& p) {
     HIP_TRY(hipSetDevice(p.device));
     HIP_TRY(hipFuncSetAttribute((const void*)k_fw3_panel, hipFuncAttributeMaxDynamicSharedMemorySize, FW3_LDS));
-    HIP_TRY(hipFuncSetAttribute((const void*)k_fw3_rest, hipFuncAttributeMaxDynamicSharedMemorySize, FW3_LDS));
+    HIP_TRY(hipFuncSetAttribute((const void*)k_fw3_rest, hipFuncAttributeMaxDynamicSharedMemorySize, FW3_REST_LDS));
     hipStream_t s = (hipStream_t)p.stream;
     const Fw3 M{p.D, p.R, p.N};
     k_fw3_init<<<grid_for(p.ld * p.ld, 256, 16384), 256, 0, s>>>(p.ld, M);
@@ -3358,7 +3365,7 @@ int fw_pivot_rows(const FwPart& p, int32_t kb, int32_t rb0, int32_t rb1) {
     hipStream_t s = (hipStream_t)p.stream;
     const Fw3 M{p.D, p.R, p.N};
     k_fw3_panel<<<rows, 256, FW3_LDS, s>>>(kb, nb, p.ld, M, nb, rb0, rb1);   // column panel, own rows
-    k_fw3_rest<<<rows * (nb - 1), 256, FW3_LDS, s>>>(kb, nb, p.ld, M, rb0, rb1);
+    k_fw3_rest<<<rows * (nb - 1), 256, FW3_REST_LDS, s>>>(kb, nb, p.ld, M, rb0, rb1);
     HIP_TRY(hipGetLastError());
     return SPE_OK;
 }
