@@ -331,3 +331,35 @@ def test_lane_group_widths(spe, lanes):
     At = graphs.tiered_attached(tt, n_core=1500, n_attached=200)
     out, _, _ = run_gpu(spe, tt, At, groups=2, lanes=lanes, engine=spe.SPE_ENGINE_BATCH)
     compare(out, Oracle(tt).rows(At, At), label=f"tiered L={lanes}")
+
+
+K3_GRAPHML = """<graphml xmlns="http://graphml.graphdrawing.org/xmlns">
+ <key attr.name="preferdirectpaths" attr.type="string" for="graph" id="g0"/>
+ <key attr.name="packetloss" attr.type="double" for="edge" id="d4"/>
+ <key attr.name="latency" attr.type="double" for="edge" id="d3"/>
+ <key attr.name="packetloss" attr.type="double" for="node" id="d0"/>
+ <graph edgedefault="undirected"><data key="g0">True</data>
+  <node id="poi-1"><data key="d0">0.0</data></node><node id="poi-2"/><node id="poi-3"><data key="d0">0.0</data></node>
+  <edge source="poi-1" target="poi-2"><data key="d3">10.0</data><data key="d4">0.05</data></edge>
+  <edge source="poi-2" target="poi-3"><data key="d3">10.0</data><data key="d4">0.05</data></edge>
+  <edge source="poi-1" target="poi-3"><data key="d3">50.0</data><data key="d4">0.05</data></edge>
+ </graph></graphml>"""
+
+
+@pytest.mark.parametrize("prefer", [True, False])
+def test_k3_triangle_known_answers(spe, prefer):
+    """K3 (generate_test_graph.py:4-13 restated): with preferdirectpaths
+    (1,3) is DIRECT 50.0 / 0.95 and (1,1) the SELF rule 2 x 10.0 / 0.95^2 (no
+    self-loop); without it (1,3) goes through poi-2: 20.0 / 0.95^2, next hop poi-2,
+    2 hops.  Every entry also equals the oracle's."""
+    top = graphs.load_graphml(K3_GRAPHML, is_text=True)
+    top.prefer_direct = prefer
+    A = np.arange(3, dtype=np.int32)
+    out, _, _ = run_gpu(spe, top, A)
+    compare(out, Oracle(top).rows(A, A), label=f"K3 prefer={prefer}")
+    if prefer:
+        assert out["lat"][0, 2] == 50.0 and out["rel"][0, 2] == 1.0 * 1.0 * (1.0 - 0.05)
+        assert out["lat"][0, 0] == 20.0 and out["rel"][0, 0] == 0.95 * 0.95
+    else:
+        assert out["lat"][0, 2] == 20.0 and out["rel"][0, 2] == ((1.0 * 1.0) * 1.0) * 0.95 * 0.95
+        assert out["next"][0, 2] == 1 and out["hops"][0, 2] == 2

@@ -15,6 +15,8 @@ for C in c3 c2 c4 c5; do
   python tools/pmc_to_json.py $O/pmc_$C profiles/${R}_pmc_$C.json > /dev/null
   timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $O/kt_$C -o run --output-format csv -- python bench.py $A > $O/kt_$C.log 2>&1
 done
+timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $O/kt_c2fw -o run --output-format csv -- python bench.py --config c2fw --steps 1 > $O/kt_c2fw.log 2>&1
+timeout -k 10 300 python -u bench.py --config c2fw > $O/bench_c2fw.log 2>&1 || { tail -20 $O/bench_c2fw.log; exit 1; }
 timeout -k 10 300 python -u bench.py > $O/bench_c3.log 2>&1 || { tail -20 $O/bench_c3.log; exit 1; }
 tail -1 $O/bench_c3.log
 timeout -k 10 300 python -u bench.py --config c2 > $O/bench_c2.log 2>&1 || { tail -20 $O/bench_c2.log; exit 1; }
