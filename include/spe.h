@@ -226,6 +226,10 @@ int spe_graph_set_edge_aux(spe_graph* g, const double* edge_aux);
  *                        for undirected graphs; a self-loop for from == to). */
 int spe_graph_self_path(const spe_graph* g, int32_t v, spe_entry* out);
 int spe_graph_adjacent(const spe_graph* g, int32_t from, int32_t to, int32_t* out);
+/* The get_eid edge from -> to (shd-topology.c:387-429 _topology_getEdgeHelper, the
+ * highest-id parallel edge as DESIGN §1 restates igraph): its latency and
+ * reliability 1 - packetloss; SPE_EINVAL when there is no such edge.  Host-only. */
+int spe_graph_edge(const spe_graph* g, int32_t from, int32_t to, double* latency, double* reliability);
 void spe_graph_free(spe_graph* g);
 
 /* attached[i] = vertex of source/target slot i (unique vertices). */
@@ -275,6 +279,15 @@ int spe_fw_apsp(spe_graph* g, double* d_dist, int64_t ld, int32_t* d_next, void*
  * Dijkstra (shd-topology.c:1741). */
 int spe_fw_closure(spe_graph* g, double* d_dist, double* d_rel, int32_t* d_next, int64_t ld, void* stream,
                    double* seconds);
+/* The shortest-path tree the SSSP row of source slot s_slot follows:
+ * parent[v] (n_vertices entries, original ids) = the vertex before v on the
+ * row's path from s to v; -1 for s itself and unreachable v.  The row's path to
+ * any v is the parent walk from v back to s -- what the reference's per-path log
+ * line prints (shd-topology.c:1809-1829, the path string of :1413-1493).  The
+ * source's block is recomputed (its rows are rewritten with the same values),
+ * so this is for logging and diagnostics, not the query path.  Not for DIRECT
+ * (complete-graph) tables. */
+int spe_table_source_tree(spe_table* t, int32_t s_slot, int32_t* parent);
 /* Owned rows [row_begin,row_end) of the want_aux field, row-major, to host. */
 int spe_table_download_aux(const spe_table* t, int32_t row_begin, int32_t row_end, double* aux);
 /* Batched per-packet lookups against the HBM-resident table.  d_pairs holds q

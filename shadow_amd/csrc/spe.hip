@@ -2853,6 +2853,34 @@ int spe_graph_adjacent(const spe_graph* g, int32_t from, int32_t to, int32_t* ou
     return SPE_OK;
 }
 
+int spe_graph_edge(const spe_graph* g, int32_t from, int32_t to, double* latency, double* reliability) {
+    if (!g) return fail(SPE_EINVAL, "NULL argument");
+    const spe::HostGraph& h = g->hg;
+    if (from < 0 || from >= h.n || to < 0 || to >= h.n) return fail(SPE_EINVAL, "vertex out of range");
+    double w = NAN, a = NAN;
+    if (from == to) {
+        if (h.loop_eid[(size_t)from] >= 0) {
+            w = h.loop_w[(size_t)from];
+            a = h.loop_a[(size_t)from];
+        }
+    } else {
+        const std::vector<int32_t>& ptr = h.directed ? h.optr : h.fiptr;
+        const std::vector<int32_t>& col = h.directed ? h.ocol : h.ficol;
+        const int32_t row = h.directed ? from : to, key = h.directed ? to : from;
+        const auto b = col.begin() + ptr[(size_t)row], e = col.begin() + ptr[(size_t)row + 1];
+        const auto it = std::lower_bound(b, e, key);
+        if (it != e && *it == key) {
+            const size_t k = (size_t)(it - col.begin());
+            w = h.directed ? h.owrep[k] : h.fiwrep[k];
+            a = h.directed ? h.oarep[k] : h.fia[k];
+        }
+    }
+    if (std::isnan(w)) return fail(SPE_EINVAL, "no such edge");
+    if (latency) *latency = w;
+    if (reliability) *reliability = a;
+    return SPE_OK;
+}
+
 int spe_order_sources(const spe_graph* g, const int32_t* attached, int32_t n_attached, int32_t* order_out) {
     if (!g || (n_attached > 0 && (!attached || !order_out))) return fail(SPE_EINVAL, "NULL argument");
     if (n_attached < 0) return fail(SPE_EINVAL, "negative n_attached");
@@ -3937,6 +3965,63 @@ int spe_fw_closure(spe_graph* g, double* d_dist, double* d_rel, int32_t* d_next,
     if (seconds) *seconds = ms / 1e3;
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
+    return SPE_OK;
+}
+
+int spe_table_source_tree(spe_table* t, int32_t s_slot, int32_t* parent) {
+    if (!t || !parent) return fail(SPE_EINVAL, "NULL argument");
+    if (t->multi) return spe::multi_source_tree(t->multi, s_slot, parent);
+    if (s_slot < 0 || s_slot >= t->A) return fail(SPE_EINVAL, "slot out of range");
+    const int32_t b = s_slot / WAVE;
+    if (b < t->blk0 || b >= t->blk1) return fail(SPE_EINVAL, "source block not owned by this table");
+    if (t->md.complete) return fail(SPE_EUNSUPPORTED, "DIRECT table: every path is its one edge");
+    const spe::HostGraph& h = t->g->hg;
+    const int32_t nc = h.nc, s = t->attached[(size_t)s_slot];
+    // pk[v]: in-CSR entry of the relaxation vertex v's parent edge; -1 none (root or
+    // unreached); -2 (batch / FW state) the pruned pendant source itself
+    std::vector<int32_t> pk((size_t)std::max(1, nc), -1);
+    HIP_TRY(hipSetDevice(t->g->device));
+    if (t->engine == SPE_ENGINE_LDS) {
+        // one workgroup re-runs this source (its row is rewritten with the same bits); the
+        // parent entries stay in that workgroup's scratch
+        k_sssp_lds<<<1, LDS_T, lds_bytes(nc), t->stream>>>(s_slot, s_slot + 1, t->d_slots, t->blk0, t->g->dev, t->md,
+                                                         t->tb, t->lsc, nullptr);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(pk.data(), t->lsc.par, sizeof(int32_t) * (size_t)nc, hipMemcpyDeviceToHost, t->stream));
+        HIP_TRY(hipStreamSynchronize(t->stream));
+        // preferdirectpaths: the row just rewritten lacks the DIRECT overlay; rebuild the block
+        if (t->md.prefer)
+            if (int r = spe_table_build_blocks(t, b, b + 1, nullptr)) return r;
+    } else {
+        // rebuild the source's block (same rows); its state is left in the first buffer
+        if (int r = spe_table_build_blocks(t, b, b + 1, nullptr)) return r;
+        const int32_t L = t->lanes, j = s_slot % WAVE;
+        const int32_t g = L <= WAVE ? j / L : 0, lane = L <= WAVE ? j % L : j;
+        const int32_t* P = t->st_buf[0].P + ((size_t)g * nc) * (size_t)L + (size_t)lane;
+        HIP_TRY(hipMemcpy2D(pk.data(), sizeof(int32_t), P, sizeof(int32_t) * (size_t)L, sizeof(int32_t), (size_t)nc,
+                            hipMemcpyDeviceToHost));
+    }
+    std::fill(parent, parent + h.n, -1);
+    const int32_t sc = h.core_id[(size_t)s];
+    const int32_t root = sc >= 0 ? sc : h.anchor_core[(size_t)s];   // relaxation vertex the tree grows from
+    std::vector<uint8_t> reach((size_t)std::max(1, nc), 0);
+    for (int32_t v = 0; v < nc; ++v) {
+        const int32_t k = pk[(size_t)v];
+        if (k >= 0) {
+            parent[h.corev[(size_t)v]] = h.corev[(size_t)h.icol[(size_t)k]];
+            reach[(size_t)v] = 1;
+        } else if (v == root) {
+            if (sc < 0) parent[h.corev[(size_t)v]] = s;   // s -> anchor: the pendant source's edge
+            reach[(size_t)v] = 1;
+        }
+    }
+    if (h.pruned)
+        for (int32_t v = 0; v < h.n; ++v) {
+            if (h.core_id[(size_t)v] >= 0 || v == s) continue;
+            const int32_t a = h.anchor_core[(size_t)v];
+            if (a >= 0 && reach[(size_t)a]) parent[v] = h.corev[(size_t)a];
+        }
+    parent[s] = -1;
     return SPE_OK;
 }
 

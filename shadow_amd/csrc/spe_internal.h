@@ -78,6 +78,7 @@ int multi_min_latency(const MultiDev* m, double* out);
 int multi_layout(const MultiDev* m, spe_table_layout* out);
 int multi_profile_enable(MultiDev* m, int32_t enable);
 int multi_profile_get(const MultiDev* m, spe_kernel_profile* out);
+int multi_source_tree(MultiDev* m, int32_t s_slot, int32_t* parent);
 // The FW engine's closure buffers of one (part) table, for the multi-device
 // closure: pivot-row broadcast between devices, each device relaxing its own
 // row blocks (spe.hip fw_*; driven by spe_multi.cpp).

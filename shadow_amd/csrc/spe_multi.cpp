@@ -396,6 +396,11 @@ int multi_get(const MultiDev* m, int32_t s_slot, int32_t t_slot, spe_entry* out)
     return spe_table_get(m->parts[owner_of(m, s_slot)], s_slot, t_slot, out);
 }
 
+int multi_source_tree(MultiDev* m, int32_t s_slot, int32_t* parent) {
+    if (s_slot < 0 || s_slot >= m->A) return set_error(SPE_EINVAL, "slot out of range");
+    return spe_table_source_tree(m->parts[owner_of(m, s_slot)], s_slot, parent);
+}
+
 int multi_download(const MultiDev* m, int32_t row_begin, int32_t row_end, double* latency, double* reliability,
                    int32_t* next_hop, int32_t* hops) {
     if (row_begin < 0 || row_end > m->A || row_begin > row_end) return set_error(SPE_EINVAL, "row range out of bounds");

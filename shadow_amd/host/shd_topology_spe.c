@@ -1307,23 +1307,80 @@ static void note_min(Topology* top, double lat, int* updated) {   /* minimumPath
     }
 }
 
+/* growable text for the path strings of log_row */
+typedef struct {
+    char* p;
+    size_t len, cap;
+} Buf;
+static void buf_printf(Buf* b, const char* fmt, ...) {
+    for (;;) {
+        va_list ap;
+        va_start(ap, fmt);
+        const int k = vsnprintf(b->p ? b->p + b->len : NULL, b->p ? b->cap - b->len : 0, fmt, ap);
+        va_end(ap);
+        if (k < 0) return;
+        if (b->p && b->len + (size_t)k < b->cap) {
+            b->len += (size_t)k;
+            return;
+        }
+        const size_t want = (b->cap ? b->cap : 256) * 2 + (size_t)k;
+        char* q = realloc(b->p, want);
+        if (!q) return;
+        b->p = q;
+        b->cap = want;
+    }
+}
+
 /* The per-path lines of _topology_computeSourcePaths (:1809-1829): info for
- * the requested target, debug for the others.  The reference's path string
- * lists every hop; the table keeps the first hop and the hop count. */
+ * the requested target, debug for the others, with the reference's path string
+ * (:1413-1493): the source id, then "<--[latency,loss]-->id" per edge of the
+ * get_eid edges along the row's path ("--[...]-->" when directed).  The path is
+ * the parent walk of the row's shortest-path tree (spe_table_source_tree: the
+ * source's rows are recomputed once, only when info lines are enabled). */
 static void log_row(Topology* top, Snap* sn, int32_t s, int32_t want) {
     if (!log_on(top, LOG_INFO)) return;
     const int32_t ss = sn->slot_of_vertex[s];
+    const int32_t n = top->n;
+    int32_t* par = malloc(sizeof(int32_t) * (size_t)n);
+    int32_t* vs = malloc(sizeof(int32_t) * ((size_t)n + 1));
+    if (par && spe_table_source_tree(sn->table, ss, par) != SPE_OK) {
+        free(par);
+        par = NULL;
+    }
+    Buf b = {NULL, 0, 0};
+    const char* arrow = top->directed ? "-->" : "<-->";
     for (int32_t j = 0; j < sn->A; ++j) {
         const int32_t t = sn->attached[j];
         const int lvl = t == want ? LOG_INFO : LOG_DEBUG;
         if (!log_on(top, lvl)) continue;
         spe_entry e;
         if (spe_table_get(sn->table, ss, j, &e) != SPE_OK || e.latency <= -1.0) continue;
-        tlog(top, lvl, "shortest path %s%s%s (%d%s%d) is %f ms with %f loss, path: first hop %s, %d hops",
-             top->vstr[VS_ID][s], top->directed ? "-->" : "<-->", top->vstr[VS_ID][t], s,
-             top->directed ? "-->" : "<-->", t, e.latency, 1 - e.reliability,
-             e.next_hop >= 0 ? top->vstr[VS_ID][e.next_hop] : "-", e.hops);
+        b.len = 0;
+        buf_printf(&b, "%s", top->vstr[VS_ID][s]);
+        int32_t nv = 0;
+        if (par && vs) {   /* the path's vertices after the source ([s] for t == s: its self-loop) */
+            for (int32_t x = t; x != s && x >= 0 && nv < n; x = par[x]) vs[nv++] = x;
+            if (t == s) vs[nv++] = s;
+            for (int32_t i = 0; i < nv / 2; ++i) {
+                const int32_t tmp = vs[i];
+                vs[i] = vs[nv - 1 - i];
+                vs[nv - 1 - i] = tmp;
+            }
+        }
+        int ok = 1;
+        for (int32_t i = 0, from = s; i < nv && ok; ++i) {
+            double w = 0.0, r = 0.0;
+            ok = spe_graph_edge(top->graph, from, vs[i], &w, &r) == SPE_OK;   /* (s,s) needs its self-loop */
+            buf_printf(&b, "%s[%f,%f]-->%s", top->directed ? "--" : "<--", w, 1.0f - r, top->vstr[VS_ID][vs[i]]);
+            from = vs[i];
+        }
+        if (!ok) continue;
+        tlog(top, lvl, "shortest path %s%s%s (%d%s%d) is %f ms with %f loss, path: %s", top->vstr[VS_ID][s], arrow,
+             top->vstr[VS_ID][t], s, arrow, t, e.latency, 1 - e.reliability, b.p ? b.p : "");
     }
+    free(b.p);
+    free(vs);
+    free(par);
 }
 
 /* _topology_getPathEntry on the model: the cached entry (x, y) answering (s, t);

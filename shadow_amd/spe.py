@@ -88,7 +88,7 @@ EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_
            "spe_table_get", "spe_table_download", "spe_lookup_batch", "spe_table_min_latency",
            "spe_table_key", "spe_table_save", "spe_table_load", "spe_table_free",
            "spe_graph_set_edge_aux", "spe_table_download_aux", "spe_fw_apsp", "spe_fw_closure", "spe_graph_self_path",
-           "spe_graph_adjacent", "spe_device_shares"]
+           "spe_graph_adjacent", "spe_device_shares", "spe_graph_edge", "spe_table_source_tree"]
 
 _lib = None
 
@@ -138,6 +138,8 @@ def lib():
         L.spe_device_shares.argtypes = [C.c_int32, C.c_int32, P, P]
         L.spe_graph_self_path.argtypes = [P, C.c_int32, P]
         L.spe_graph_adjacent.argtypes = [P, C.c_int32, C.c_int32, P]
+        L.spe_graph_edge.argtypes = [P, C.c_int32, C.c_int32, P, P]
+        L.spe_table_source_tree.argtypes = [P, C.c_int32, P]
         _lib = L
     return _lib
 
@@ -203,6 +205,12 @@ class Graph:
         _check(lib().spe_fw_closure(self.h, C.c_void_p(d_dist), C.c_void_p(d_rel), C.c_void_p(d_next), int(ld),
                                     C.c_void_p(stream or None), C.byref(sec)), "spe_fw_closure")
         return float(sec.value)
+
+    def edge(self, u: int, v: int):
+        """spe_graph_edge: (latency, reliability) of the get_eid edge u -> v."""
+        w, a = C.c_double(0), C.c_double(0)
+        _check(lib().spe_graph_edge(self.h, int(u), int(v), C.byref(w), C.byref(a)), "spe_graph_edge")
+        return float(w.value), float(a.value)
 
     def order_sources(self, attached) -> np.ndarray:
         """spe_order_sources: a slot order clustering sources by relaxation anchor."""
@@ -310,6 +318,12 @@ class PathTable:
                                         _p(out.get("next")), _p(out.get("hops"))), "spe_table_download")
         if "lat" in out:
             out["ok"] = out["lat"] > -1.0
+        return out
+
+    def source_tree(self, s_slot: int) -> np.ndarray:
+        """spe_table_source_tree: parent[v] on the row of source slot s_slot (-1: root / unreachable)."""
+        out = np.empty(self.graph.top.n, np.int32)
+        _check(lib().spe_table_source_tree(self.h, int(s_slot), _p(out)), "spe_table_source_tree")
         return out
 
     def download_aux(self, row_begin: int = 0, row_end: Optional[int] = None) -> np.ndarray:
