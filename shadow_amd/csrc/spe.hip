@@ -3065,7 +3065,9 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
             const bool ext = o.ext_latrel || o.ext_next_hop || o.ext_hops;
             const double rec = 22.0 + (o.owner_rank ? 4.0 : 0.0) + (o.want_aux ? 8.0 : 0.0);
             const double table_b = ext ? 0.0 : (double)owned * n_attached * WAVE * rec;
-            const double budget = (double)free_b - table_b - 4.0e9;
+            const double ldf = std::ceil(std::max(1, n) / 64.0) * 64.0;   // FW engine: its closure, 20 B x ld^2
+            const double closure_b = o.engine == SPE_ENGINE_FW ? 20.0 * ldf * ldf : 0.0;
+            const double budget = (double)free_b - table_b - closure_b - 4.0e9;
             want = std::min(want, std::max(1.0, budget / per_group));
         } else {
             want = std::min(want, 6.0e9 / per_group);
