@@ -543,7 +543,7 @@ SIDE_CONFIGS = (
 )
 
 
-def side_configs(timeout_s: float = 240.0):
+def side_configs(timeout_s: float = 120.0):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
