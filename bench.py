@@ -530,7 +530,8 @@ def bench_table(args, rank, world, local, dist):
     return None
 
 
-# The default run (C3 at N = 1) also measures BASELINE's other configurations,
+# The default run (C3 at N = 1) also measures BASELINE's other configurations
+# (and C2 on the FW engine),
 # each in a child process of its own once the C3 table is freed (C4's table alone
 # is 220 GB), so that every config has a line on the driver's box.  A child that
 # fails is recorded with its exit status and the tail of its output; the C3 line
@@ -540,6 +541,7 @@ SIDE_CONFIGS = (
     ("c2", ["--config", "c2", "--cpu-seconds", "6"]),
     ("c4", ["--config", "c4", "--steps", "2", "--cpu-seconds", "6"]),
     ("c1", ["--config", "c1", "--cpu-seconds", "4"]),
+    ("c2fw", ["--config", "c2fw", "--steps", "1"]),   # the FW engine's whole C2 table
 )
 
 
