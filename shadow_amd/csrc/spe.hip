@@ -400,6 +400,9 @@ __device__ __forceinline__ void offer(Best& b, const DevGraph& G, const State& s
     } else if (alt == b.bd) {
         if (b.bk == PK_UNREAD) b.bk = b.pold = st.P[b.rv];
         if (kk == b.bk) {
+#ifdef SPE_DIAGNOSTICS   // experiments only: SPE_ABLATE bit 1 skips parent refreshes (inexact)
+            if (G.ablate & 2) return;
+#endif
             b.need = true;
             b.bdu = du;
             b.bu = u;
