@@ -2342,26 +2342,41 @@ __global__ __launch_bounds__(256) void k_fw3_rest(int32_t kb, int32_t nb, int64_
         for (int32_t k = 0; k < KH; ++k) {
             const double2 a01 = *reinterpret_cast<const double2*>(&AD[k * FWB + ty * 4]);
             const double2 a23 = *reinterpret_cast<const double2*>(&AD[k * FWB + ty * 4 + 2]);
-            const double2 r01 = *reinterpret_cast<const double2*>(&AR[k * FWB + ty * 4]);
-            const double2 r23 = *reinterpret_cast<const double2*>(&AR[k * FWB + ty * 4 + 2]);
-            const int4 an4 = *reinterpret_cast<const int4*>(&AN[k * FWB + ty * 4]);
             const double2 b01 = *reinterpret_cast<const double2*>(&BD[k * FWB + tx * 4]);
             const double2 b23 = *reinterpret_cast<const double2*>(&BD[k * FWB + tx * 4 + 2]);
-            const double2 s01 = *reinterpret_cast<const double2*>(&BR[k * FWB + tx * 4]);
-            const double2 s23 = *reinterpret_cast<const double2*>(&BR[k * FWB + tx * 4 + 2]);
-            const double a[4] = {a01.x, a01.y, a23.x, a23.y}, ar[4] = {r01.x, r01.y, r23.x, r23.y};
-            const int32_t an[4] = {an4.x, an4.y, an4.z, an4.w};
-            const double bb[4] = {b01.x, b01.y, b23.x, b23.y}, br[4] = {s01.x, s01.y, s23.x, s23.y};
+            const double a[4] = {a01.x, a01.y, a23.x, a23.y};
+            const double bb[4] = {b01.x, b01.y, b23.x, b23.y};
+            double x[4][4];
+            bool up[4][4], any = false;
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const double x = a[r] + bb[c];
-                    const bool up = x < d[r][c];
-                    d[r][c] = up ? x : d[r][c];
-                    rr[r][c] = up ? ar[r] * br[c] : rr[r][c];
-                    nn[r][c] = up ? an[r] : nn[r][c];
+                    x[r][c] = a[r] + bb[c];
+                    up[r][c] = x[r][c] < d[r][c];
+                    any |= up[r][c];
                 }
+            // Improvements get rare after the first pivots: the reliability and
+            // first-edge panels are read from LDS, and the products and selects done,
+            // only by waves with an improvement at this k (the common step is the
+            // distance-only closure's: two panel reads, add + compare).
+            if (__ballot(any)) {
+                const double2 r01 = *reinterpret_cast<const double2*>(&AR[k * FWB + ty * 4]);
+                const double2 r23 = *reinterpret_cast<const double2*>(&AR[k * FWB + ty * 4 + 2]);
+                const int4 an4 = *reinterpret_cast<const int4*>(&AN[k * FWB + ty * 4]);
+                const double2 s01 = *reinterpret_cast<const double2*>(&BR[k * FWB + tx * 4]);
+                const double2 s23 = *reinterpret_cast<const double2*>(&BR[k * FWB + tx * 4 + 2]);
+                const double ar[4] = {r01.x, r01.y, r23.x, r23.y}, br[4] = {s01.x, s01.y, s23.x, s23.y};
+                const int32_t an[4] = {an4.x, an4.y, an4.z, an4.w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        d[r][c] = up[r][c] ? x[r][c] : d[r][c];
+                        rr[r][c] = up[r][c] ? ar[r] * br[c] : rr[r][c];
+                        nn[r][c] = up[r][c] ? an[r] : nn[r][c];
+                    }
+            }
         }
     }
 #pragma unroll
