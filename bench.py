@@ -147,9 +147,11 @@ def bench_lookup(args, rank=0, world=1, local=0, dist=None):
     its own 100M queries per step (weak scaling)."""
     import torch
     from shadow_amd import spe
-    top, att, desc = workload("c3")
+    top, att, desc = workload(args.c5_table)
     dev = torch.device("cuda", local)
     g = spe.Graph(top, device=local)
+    if args.c5_table != "c3":
+        att = g.order_sources(att)
     t = spe.PathTable(g, att)
     t.build()
     q = args.queries
@@ -195,7 +197,7 @@ def bench_lookup(args, rank=0, world=1, local=0, dist=None):
             "config": {"workload": f"C5: {q} uniform (s,t) slot pairs per GPU (seed 5 + rank) on the {desc} table",
                        "parallelism": f"{world} replica(s) of the table, queries split, no communication"},
             "roofline": {"bound": "hbm", "kernel": "k_lookup", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, "k_lookup"),
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, "k_lookup") if args.c5_table == "c3" else None,
                          "algorithmic_bytes_per_query": 41},
             "cpu_baseline": cpu}
     if cpu:
@@ -542,6 +544,7 @@ SIDE_CONFIGS = (
     ("c4", ["--config", "c4", "--steps", "2", "--cpu-seconds", "6"]),
     ("c1", ["--config", "c1", "--cpu-seconds", "4"]),
     ("c2fw", ["--config", "c2fw", "--steps", "1"]),   # the FW engine's whole C2 table
+    ("c5_on_c4", ["--config", "c5", "--c5-table", "c4", "--steps", "10", "--warmup", "2", "--no-cpu-baseline"]),
 )
 
 
@@ -581,6 +584,8 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the all-gather (build only)")
     ap.add_argument("--queries", type=int, default=100_000_000, help="c5: lookups per step")
+    ap.add_argument("--c5-table", default="c3", choices=("c3", "c4"),
+                    help="c5: the table the lookups read (c4: 100k x 100k, 220 GB on one GPU)")
     ap.add_argument("--pois", type=int, default=10000, help="complete: POIs")
     ap.add_argument("--pmc-json", default=None, help="per-dispatch HBM bytes from tools/pmc_to_json.py")
     ap.add_argument("--full-table", action="store_true", help="(the default; kept for old command lines)")
