@@ -286,7 +286,7 @@ int spe_fw_closure(spe_graph* g, double* d_dist, double* d_rel, int32_t* d_next,
  * line prints (shd-topology.c:1809-1829, the path string of :1413-1493).  The
  * source's block is recomputed (its rows are rewritten with the same values),
  * so this is for logging and diagnostics, not the query path.  Not for DIRECT
- * (complete-graph) tables. */
+ * (complete-graph) tables nor owner-replay tables (SPE_EUNSUPPORTED). */
 int spe_table_source_tree(spe_table* t, int32_t s_slot, int32_t* parent);
 /* Owned rows [row_begin,row_end) of the want_aux field, row-major, to host. */
 int spe_table_download_aux(const spe_table* t, int32_t row_begin, int32_t row_end, double* aux);

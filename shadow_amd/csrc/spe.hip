@@ -3995,6 +3995,8 @@ int spe_table_source_tree(spe_table* t, int32_t s_slot, int32_t* parent) {
     const int32_t b = s_slot / WAVE;
     if (b < t->blk0 || b >= t->blk1) return fail(SPE_EINVAL, "source block not owned by this table");
     if (t->md.complete) return fail(SPE_EUNSUPPORTED, "DIRECT table: every path is its one edge");
+    // owner replay rewrites pairs across blocks (k_owner_replay): rebuilding one block would undo it
+    if (t->d_rank) return fail(SPE_EUNSUPPORTED, "owner-replay table: its entries are not one source's tree");
     const spe::HostGraph& h = t->g->hg;
     const int32_t nc = h.nc, s = t->attached[(size_t)s_slot];
     // pk[v]: in-CSR entry of the relaxation vertex v's parent edge; -1 none (root or

@@ -144,3 +144,21 @@ def test_shim_per_path_log_lines_carry_the_path(tmp_path):
         seen += 1
         assert (lvl == 4) == (tt == verts[3])
     assert seen >= 15
+
+
+def test_source_tree_refuses_owner_replay_and_direct_tables(spe):
+    top = graphs.gen_random_small(200, 600, 76)
+    A = np.arange(top.n, dtype=np.int32)
+    g = spe.Graph(top)
+    t = spe.PathTable(g, A, owner_order=np.arange(top.n))
+    t.build()
+    with pytest.raises(spe.SpeError):
+        t.source_tree(3)
+    z = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "shipped_topology.npz"))
+    shipped = graphs.Topology(n=int(z["n"]), esrc=z["esrc"], edst=z["edst"], elat=z["elat"], eloss=z["eloss"],
+                              vloss=z["vloss"], directed=bool(z["directed"]), prefer_direct=bool(z["prefer_direct"]))
+    gs = spe.Graph(shipped)
+    td = spe.PathTable(gs, np.arange(shipped.n, dtype=np.int32))
+    td.build()
+    with pytest.raises(spe.SpeError):
+        td.source_tree(0)
