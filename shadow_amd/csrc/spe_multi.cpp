@@ -302,7 +302,8 @@ struct FwBcast {
 static int fw_closure_multi(MultiDev* m, double* seconds) {
     std::vector<FwPart> P(m->n);
     for (int d = 0; d < m->n; ++d) {
-        if (!m->parts[d]) return set_error(SPE_EUNSUPPORTED, "FW engine: every device needs a share of the sources");
+        // an empty share (more devices than source blocks): every part computes its own closure
+        if (!m->parts[d]) return SPE_OK;
         if (int r = fw_part(m->parts[d], &P[d])) return r;
     }
     bool done = true;
