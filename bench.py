@@ -400,9 +400,11 @@ def bench_table(args, rank, world, local, dist):
     from shadow_amd import dist as sd
     shares = max(world, args.shares)
     emulated = shares != world   # one rank of a `shares`-GPU job: its chunks only, no gather
-    rounds, G = sd.chunk_plan(nblk, shares, gpl)
-    mine = sd.rank_chunks(nblk, shares, args.share_index if emulated else rank, rounds, G)
-    padded = rounds * shares * G
+    # per-round chunk sizes: at N > 1 a short first round starts the gathers early
+    sizes = sd.chunk_schedule(nblk, shares, gpl)
+    rounds, G = len(sizes), max(sizes)
+    mine = sd.rank_chunks_sched(nblk, shares, args.share_index if emulated else rank, sizes)
+    padded = shares * sum(sizes)
     elems = padded * A * 64
     gather = world > 1 and not args.no_gather
     # the table in caller-owned HBM (spe_table_opts.ext_*): every rank holds the
@@ -412,17 +414,17 @@ def bench_table(args, rank, world, local, dist):
     hp = torch.empty(elems, dtype=torch.int16, device=dev)
     t = spe.PathTable(g, att, blocks=(0, nblk), ext=[lr.data_ptr(), nx.data_ptr(), hp.data_ptr()], groups=G,
                       engine=args.engine)
-    chunk_elems = G * A * 64
+    blk_elems = A * 64
 
     def one_table():
         works, tb, tg, its = [], 0.0, 0.0, 0
-        for k, c, b0, b1 in mine:
+        for k, off, gk, b0, b1 in mine:
             t0 = time.perf_counter()
             if b1 > b0:
                 its += t.build_blocks(b0, b1)["iterations"]
             tb += time.perf_counter() - t0
             if gather:   # overlaps the next round's build (RCCL runs on its own stream)
-                w = sd.allgather_round(lr, k, world, rank, chunk_elems, dist, async_op=True)
+                w = sd.allgather_span(lr, off, gk, world, rank, blk_elems, dist, async_op=True)
                 if w is not None:
                     works.append(w)
         t1 = time.perf_counter()
@@ -459,7 +461,7 @@ def bench_table(args, rank, world, local, dist):
     if dist is not None:
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
     el, tb_sum, tg_sum = (float(v) for v in x.tolist())
-    built = sum(min(A, b1 * 64) - b0 * 64 for _, _, b0, b1 in mine if b1 > b0)
+    built = sum(min(A, b1 * 64) - b0 * 64 for _, _, _, b0, b1 in mine if b1 > b0)
     total = built if emulated else A
     value = total * steps / el
     lds = kp is not None and kp["lds"]["launches"] > 0
@@ -514,14 +516,14 @@ def bench_table(args, rank, world, local, dist):
                        "slot_order_ms": round(1e3 * t_ord, 1),
                        "step": "one whole path table (every source row)" + (
                            f"; emulated share {args.share_index} of {shares} (no gather)" if emulated else ""),
-                       "chunk_blocks": G, "rounds": rounds,
+                       "chunk_blocks": G, "rounds": rounds, "chunk_schedule": sizes,
                        "parallelism": (f"source chunks round-robin over {world} GPUs, RCCL all-gather of the "
                                        f"latency/reliability records overlapped with the next chunk's build"
                                        if gather else f"{world} GPU(s), no collective")},
             "full_table_time_s": round(el / steps, 4) if not emulated else None,
             "build_s_per_step": round(tb_sum / steps, 4),
             "gather_wait_s_per_step": round(tg_sum / steps, 4) if gather else None,
-            "gather_bytes_per_gpu_per_step": int((world - 1) * rounds * chunk_elems * 16) if gather else None,
+            "gather_bytes_per_gpu_per_step": int((world - 1) * sum(sizes) * blk_elems * 16) if gather else None,
             "relax_rounds_per_step": round(it_total / max(1, steps), 1),
             "roofline": roof, "cpu_baseline": cpu,
         }

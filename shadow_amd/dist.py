@@ -111,6 +111,50 @@ def rank_chunks(nblk: int, world: int, rank: int, rounds: int, G: int):
     return out
 
 
+def chunk_schedule(nblk: int, world: int, groups: int, lead: int = 4):
+    """Per-round chunk sizes (blocks per rank) for the overlapped build + gather:
+    round k covers the contiguous blocks [off_k, off_k + world * sizes[k]).  At
+    N > 1 the first round is short (groups / lead) so the first all-gather starts
+    early -- the step is then about the first build plus the gathers, which xGMI
+    bounds -- then rounds of `groups`; the last one is trimmed to what
+    is left.  N = 1: uniform rounds (chunk_plan's)."""
+    groups = max(1, groups)
+    if world <= 1:
+        rounds, G = chunk_plan(nblk, 1, groups)
+        return [G] * rounds
+    sizes, left = [], nblk
+    first = max(1, -(-groups // lead))
+    while left > 0:
+        g = first if not sizes else groups
+        g = min(g, -(-left // world))
+        sizes.append(g)
+        left -= world * g
+    return sizes
+
+
+def rank_chunks_sched(nblk: int, world: int, rank: int, sizes):
+    """[(round, first block of the round, size, b0, b1)] of `rank` under chunk_schedule."""
+    out, off = [], 0
+    for k, g in enumerate(sizes):
+        out.append((k, off, g, min(nblk, off + rank * g), min(nblk, off + (rank + 1) * g)))
+        off += world * g
+    return out
+
+
+def allgather_span(lr, off: int, g: int, world: int, rank: int, blk_elems: int, dist, async_op: bool = False):
+    """All-gather one chunk_schedule round in place: blocks [off, off + world * g)
+    of the SB64 records, rank r's part being [off + r g, off + (r + 1) g)."""
+    grp = lr[off * blk_elems:(off + world * g) * blk_elems]
+    own = lr[(off + rank * g) * blk_elems:(off + (rank + 1) * g) * blk_elems]
+    if dist.get_backend() == "gloo":
+        parts = [p.clone() for p in grp.chunk(world)]
+        dist.all_gather(parts, own.clone())
+        for p, dst in zip(parts, grp.chunk(world)):
+            dst.copy_(p)
+        return None
+    return dist.all_gather_into_tensor(grp, own, async_op=async_op)
+
+
 def allgather_round(lr, k: int, world: int, rank: int, chunk_elems: int, dist, async_op: bool = False):
     """All-gather round k's records in place: rank r's chunk (k * world + r) sits
     at element (k * world + r) * chunk_elems of `lr` on every rank, so the round

@@ -101,6 +101,76 @@ def test_chunk_plan_covers_every_block_once():
                 assert sorted(seen) == list(range(nblk))
 
 
+def test_chunk_schedule_front_loaded_and_covering():
+    """bench.py's N > 1 rounds: a short first round, then rounds of `groups`, the
+    last trimmed; every block built exactly once, rounds contiguous."""
+    for nblk in (1, 7, 157, 782, 1563):
+        for world in (1, 2, 3, 8):
+            for groups in (1, 16, 25, 98):
+                sizes = sd.chunk_schedule(nblk, world, groups)
+                assert all(1 <= g <= max(1, groups) for g in sizes)
+                assert world * sum(sizes) >= nblk
+                if world > 1 and len(sizes) > 1:
+                    assert sizes[0] <= -(-groups // 4)
+                seen, off = [], 0
+                for r in range(world):
+                    ch = sd.rank_chunks_sched(nblk, world, r, sizes)
+                    assert [c[1] for c in ch] == list(np.cumsum([0] + [world * g for g in sizes[:-1]]))
+                    for k, o, g, b0, b1 in ch:
+                        assert b0 == min(nblk, o + r * g) and b1 == min(nblk, o + (r + 1) * g)
+                        seen += list(range(b0, b1))
+                assert sorted(seen) == list(range(nblk))
+
+
+def _sched_worker(rank, world, port, out_q):
+    """The same with chunk_schedule + allgather_span (what bench.py runs)."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys_path_oracle()
+    from oracle import Oracle
+    top = graphs.gen_random_small(700, 2100, 8)
+    A = np.arange(top.n, dtype=np.int32)
+    nblk = sd.nblocks(top.n)
+    sizes = sd.chunk_schedule(nblk, world, 2)
+    blk = top.n * 64
+    lr = torch.full((world * sum(sizes) * blk, 2), float("nan"), dtype=torch.float64)
+    o = Oracle(top)
+    for k, off, g, b0, b1 in sd.rank_chunks_sched(nblk, world, rank, sizes):
+        if b1 > b0:
+            rows = o.rows(A[b0 * 64:min(top.n, b1 * 64)], A)
+            rows["hops"] = rows["hops"].astype(np.uint16)
+            f = sd.rows_to_sb64(rows, b0 * 64, top.n, b1 - b0)
+            lr[b0 * blk:b1 * blk] = torch.from_numpy(f["lr"])
+        sd.allgather_span(lr, off, g, world, rank, blk, dist)
+    ref = o.rows(A, A)
+    e = sd.sb64_index(np.repeat(A, top.n), np.tile(A, top.n), top.n)
+    got = lr.numpy()[e]
+    ok = np.array_equal(got[:, 0], ref["lat"].ravel()) and np.array_equal(got[:, 1], ref["rel"].ravel())
+    out_q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_chunk_schedule_allgather(world):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sched_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(world)}
+
+
 def _chunk_worker(rank, world, port, out_q):
     """bench.py's N > 1 step on CPU: round-robin chunks, each round's records
     all-gathered in place (sd.allgather_round) into the replicated SB64 table."""
