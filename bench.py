@@ -329,7 +329,8 @@ def bench_fw(args):
                          "achieved": round(2 * relax / closure / 1e12, 2), "peak": 78.6, "unit": "TFLOP/s",
                          "frac": round(2 * relax / closure / 1e12 / 78.6, 4),
                          "note": "2 FP64 ops (add, min) per (min,+) relaxation, ld^3 relaxations; carrying R and "
-                                 "N adds a multiply and three selects per relaxation"},
+                                 "N adds a multiply and three selects per relaxation",
+                         "traffic": pmc_traffic(args, "k_fw3_rest")},
             "closure_triple_s": round(closure, 4), "closure_distance_only_s": round(dist_only, 4),
             "fw_kernels_ms_in_table_build": round(fw_ms, 2), "rows_ms": round(kp["rows"]["ms"], 2),
             "lds_engine_table_s": round(lds_s, 4),
