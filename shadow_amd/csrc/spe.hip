@@ -2482,10 +2482,10 @@ struct spe_table {
     int32_t groups = 8;            // 64-source blocks per batch
     int32_t lanes = 16;            // sources per lane group (L)
     int32_t engine = SPE_ENGINE_BATCH;   // resolved engine
-    int32_t infl = 8;              // neighbour rows in flight per subgroup (4 or 8)
+    int32_t infl = 8;              // neighbour rows in flight per subgroup (2, 3, 4, 6 or 8)
     bool trace = getenv("SPE_TRACE") != nullptr;   // diagnostic: per-launch times to stderr
     unsigned long long* d_lds_dbg = nullptr;       // diagnostic (SPE_LDS_DEBUG): LDS engine phase clocks
-    int32_t occ = 0;               // diagnostic: forced waves/SIMD of k_relax (0 = compiler's choice)
+    int32_t occ = 0;               // forced waves/SIMD of k_relax (0 = compiler's choice; 6 at 128 lanes)
     RowMode md{};
     bool ext = false;
     bool built = false;              // every owned block holds its rows
@@ -3145,12 +3145,15 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         }
     }
     if (t->engine == SPE_ENGINE_FW) t->lanes = lanes = WAVE;   // its state walk writes 64-lane rows
-    t->infl = lanes == 64 ? 8 : 4;
+    // rows in flight per k_relax wave: 8 at 64 lanes; at 128 lanes 2, with the
+    // kernel held to 6 waves / SIMD (80 VGPRs, a few spilled) — more waves beat
+    // deeper per-wave gathers there
+    t->infl = lanes == 64 ? 8 : lanes == 128 ? 2 : 4;
     if (getenv("SPE_INFL")) {
         const int want = atoi(getenv("SPE_INFL"));
-        if (want == 4 || want == 8 || (lanes == 64 && want == 6) || (lanes == 256 && want == 2)) t->infl = want;
+        if (want == 4 || want == 8 || (lanes == 64 && want == 6) || (lanes == 256 && want == 2) || (lanes == 128 && (want == 2 || want == 3))) t->infl = want;
     }
-    t->occ = getenv("SPE_OCC") ? atoi(getenv("SPE_OCC")) : 0;
+    t->occ = getenv("SPE_OCC") ? atoi(getenv("SPE_OCC")) : (lanes == 128 && t->infl == 2 ? 6 : 0);
     t->tb.A = n_attached;
     const size_t elems = (size_t)(t->blk1 - t->blk0) * n_attached * WAVE;
     int r = SPE_OK;
@@ -3523,7 +3526,12 @@ static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
                                : relax_to_convergence_l<64, 8, 1, true>(t, blocks, s);
     switch (t->lanes) {
         case 128:
-            if (t->occ == 6) return relax_to_convergence_l<128, 4, 6>(t, blocks, s);
+            if (t->infl == 3) return t->occ == 6 ? relax_to_convergence_l<128, 3, 6>(t, blocks, s) : relax_to_convergence_l<128, 3>(t, blocks, s);
+            if (t->occ == 6 && t->infl == 4) return relax_to_convergence_l<128, 4, 6>(t, blocks, s);
+            if (t->infl == 2) {
+                if (t->occ == 7) return relax_to_convergence_l<128, 2, 7>(t, blocks, s);
+                return t->occ == 6 ? relax_to_convergence_l<128, 2, 6>(t, blocks, s) : relax_to_convergence_l<128, 2>(t, blocks, s);
+            }
             return deep ? relax_to_convergence_l<128, 8>(t, blocks, s) : relax_to_convergence_l<128, 4>(t, blocks, s);
         case 256:
             return t->infl == 2 ? relax_to_convergence_l<256, 2>(t, blocks, s) : relax_to_convergence_l<256, 4>(t, blocks, s);
