@@ -358,7 +358,8 @@ def auto_groups(info, nblk: int, A: int, world: int, dev) -> int:
     vertex) rows per relaxation round, within the free HBM next to the table
     (state held twice for the rows / relaxation overlap, 4 GB kept free).  At
     N > 1 the chunk is also cut so that every rank runs >= 4 rounds: a round's
-    all-gather then overlaps the next round's build."""
+    all-gather then overlaps the next round's build, and rounded up to an even
+    count (spe_table_create picks 64-source rows for an odd count below 32)."""
     import torch
     n = max(1, info["n_relax_vertices"])
     per_group = 2.0 * (n * 64 * 28.0 + 4.0 * n + 2.0 * info["n_relax_entries"])
@@ -368,6 +369,8 @@ def auto_groups(info, nblk: int, A: int, world: int, dev) -> int:
     want = max(1.0, min(round(1.0e7 / n), cap))
     if world > 1:
         want = min(want, math.ceil(nblk / (world * 4)))
+        if want > 1 and int(want) % 2:
+            want = int(want) + 1   # even: the table keeps 128-source rows (k_relax_m), e.g. C3 at N = 8: 25 -> 26
     return int(max(1, want))
 
 
