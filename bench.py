@@ -72,12 +72,14 @@ def workload(name: str):
     return top, att, desc
 
 
-def cpu_baseline(top, att, seconds: float, seed: int = 6):
+def cpu_baseline(top, att, seconds: float, sources: int = 0, seed: int = 6):
     """Oracle (C restatement of igraph Dijkstra + Shadow row rules, -O2) timed on a
-    bounded sample of this workload's sources: 1 core (the reference serialises
-    its Dijkstra runs under graphLock, shd-topology.c:1732-1766), then all cores
-    (OpenMP over sources: a bound the reference cannot reach).  Sources are drawn
-    in a seeded random order, cycling when the sample outlasts A (C1)."""
+    sample of this workload's sources: 1 core (the reference serialises its
+    Dijkstra runs under graphLock, shd-topology.c:1732-1766), then all cores
+    (OpenMP over sources: a bound the reference cannot reach).  The 1-core leg
+    times exactly `sources` seeded-random sources when given (BASELINE.md plans
+    1,000 for C3 and C4), else as many as fit `seconds`; sources cycle when the
+    sample outlasts A (C1)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Oracle
     o = Oracle(top)
@@ -88,10 +90,11 @@ def cpu_baseline(top, att, seconds: float, seed: int = 6):
         return att[order[np.arange(start, start + k) % A]]
 
     done, t0, dj = 0, time.perf_counter(), 0.0
-    while time.perf_counter() - t0 < seconds:
-        r = o.rows(take(done, 8), att, nthreads=1, want_dijkstra_time=True)
+    while (done < sources) if sources > 0 else (time.perf_counter() - t0 < seconds):
+        k = min(8, sources - done) if sources > 0 else 8
+        r = o.rows(take(done, k), att, nthreads=1, want_dijkstra_time=True)
         dj += r["dijkstra_seconds"]
-        done += 8
+        done += k
     el = time.perf_counter() - t0
     model = ""
     try:
@@ -117,13 +120,13 @@ def cpu_baseline(top, att, seconds: float, seed: int = 6):
             "cpu_model": model, "host_nproc": os.cpu_count()}
 
 
-def pmc_traffic(args, kernel):
+def pmc_traffic(args, kernel, config=None):
     """HBM bytes per dispatch of `kernel` from a committed PMC summary (separate
     rocprofv3 --pmc passes of this same bench command), or None."""
     path = args.pmc_json
     if path is None:   # the newest committed summary of this config
-        for rnd in ("r02", "r01"):
-            cand = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{args.config}.json")
+        for rnd in ("r03", "r02", "r01"):
+            cand = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{config or args.config}.json")
             if os.path.exists(cand):
                 path = cand
                 break
@@ -195,9 +198,9 @@ def bench_lookup(args, rank=0, world=1, local=0, dist=None):
             "ms_per_step": round(1e3 * el / steps, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"C5: {q} uniform (s,t) slot pairs per GPU (seed 5 + rank) on the {desc} table",
-                       "parallelism": f"{world} replica(s) of the table, queries split, no communication"},
+                       "parallelism": f"{world} replica(s) of the table, each GPU answering its own queries (no communication)"},
             "roofline": {"bound": "hbm", "kernel": "k_lookup", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, "k_lookup") if args.c5_table == "c3" else None,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, "k_lookup", "c5" if args.c5_table == "c3" else "c5_on_c4"),
                          "algorithmic_bytes_per_query": 41},
             "cpu_baseline": cpu}
     if cpu:
@@ -353,7 +356,7 @@ def relax_bytes(info, A, lds: bool, direct: bool):
     return b_relax, b_rows
 
 
-def auto_groups(info, nblk: int, A: int, world: int, dev) -> int:
+def auto_groups(info, nblk: int, A: int, world: int, dev, span_blocks: int = 0) -> int:
     """spe_table_create's default groups per launch (spe.hip): ~10M (group,
     vertex) rows per relaxation round, within the free HBM next to the table
     (state held twice for the rows / relaxation overlap, 4 GB kept free).  At
@@ -364,27 +367,66 @@ def auto_groups(info, nblk: int, A: int, world: int, dev) -> int:
     n = max(1, info["n_relax_vertices"])
     per_group = 2.0 * (n * 64 * 28.0 + 4.0 * n + 2.0 * info["n_relax_entries"])
     free_b, _ = torch.cuda.mem_get_info(dev)
-    table_b = float(nblk) * A * 64 * 22.0
+    table_b = float(span_blocks or nblk) * A * 64 * 22.0
     cap = max(1.0, (free_b - table_b - 4.0e9) / per_group)
     want = max(1.0, min(round(1.0e7 / n), cap))
     if world > 1:
         want = min(want, math.ceil(nblk / (world * 4)))
         if want > 1 and int(want) % 2:
-            want = int(want) + 1   # even: the table keeps 128-source rows (k_relax_m), e.g. C3 at N = 8: 25 -> 26
+            want = int(want) + 1   # even: the table keeps 128-source rows, e.g. C3 at N = 8: 25 -> 26
     return int(max(1, want))
 
 
-def bench_table(args, rank, world, local, dist):
+def calibrate_split(t, lr, blk_elems, nblk, world, rank, dev, dist, span_blocks):
+    """N > 1: the inputs of dist.shared_fraction, measured untimed on this job --
+    the one-GPU whole-table build time T1 (from a build of this rank's share of a
+    pure-sharding schedule, scaled by N) and the all-gather bandwidth B (one
+    in-place all_gather_into_tensor of up to 2 GB per rank) -- agreed over the
+    ranks (max T1, min B) so every rank takes the same schedule."""
+    import torch
+    share = max(1, nblk // world)
+    b0 = min(nblk - 1, rank * share)
+    b1 = min(nblk, b0 + share)
+    nx = torch.empty((b1 - b0) * blk_elems, dtype=torch.int32, device=dev)
+    hp = torch.empty((b1 - b0) * blk_elems, dtype=torch.int16, device=dev)
+    t1 = 0.0
+    for _ in range(2):   # the second build is timed (the first loads code objects)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        t.build_blocks_into(b0, b1, lr[b0 * blk_elems:].data_ptr(), nx.data_ptr(), hp.data_ptr())
+        t1 = (time.perf_counter() - t0) * nblk / max(1, b1 - b0)
+    del nx, hp
+    from shadow_amd import dist as sd
+    per = max(1, min(span_blocks // world, int(2e9 // (blk_elems * 16))))
+    sd.allgather_span(lr, 0, per, world, rank, blk_elems, dist)   # warm the communicator
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    sd.allgather_span(lr, 0, per, world, rank, blk_elems, dist)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    recv = (world - 1) * per * blk_elems * 16.0
+    x = torch.tensor([t1, -recv / max(el, 1e-9)], dtype=torch.float64, device=dev)
+    dist.all_reduce(x, op=dist.ReduceOp.MAX)
+    return float(x[0].item()), float(-x[1].item())
+
+
+def bench_table(args, rank, world, local, dist, config=None):
     """The default measurement: a step is one WHOLE path table (every source
     row) of the config -- BASELINE's "full path-table time".  At N > 1 (one rank
-    per GPU, torchrun) the source blocks are dealt round-robin in chunks of one
-    build launch, and every chunk's {latency, reliability} records are
-    all-gathered over RCCL into the replicated table on every GPU, overlapped with
-    the next chunk's build; the step ends when every rank holds the whole table
-    (strong scaling: the total work per step is fixed)."""
+    per GPU, torchrun) the table is replicated on every GPU at the end of a step,
+    and the work is split between sharing and recomputing (DESIGN §6,
+    dist.shared_fraction): the first S source blocks are dealt round-robin in
+    chunks of one build launch, every chunk's {latency, reliability} records
+    all-gathered over RCCL in place (overlapped with the next build), and the
+    remaining blocks are built by every rank itself while the gathers run.  Next
+    hops / hop counts stay with the rank that built them (its own chunks and the
+    local remainder, packed).  The step ends when every rank holds the whole record
+    span (strong scaling: the total work per step is fixed)."""
     import torch
     from shadow_amd import spe
-    top, att, desc = workload(args.config)
+    config = config or args.config
+    top, att, desc = workload(config)
     g = spe.Graph(top, device=local)
     t_ord = time.perf_counter()
     att = g.order_sources(att)   # slot numbering is the caller's: clustered sources (host side)
@@ -393,44 +435,59 @@ def bench_table(args, rank, world, local, dist):
     A = int(att.shape[0])
     nblk = (A + 63) // 64
     dev = torch.device("cuda", local)
-    # the engine's groups per launch (auto rule: ~2.4M (group, vertex) rows per
-    # round) bounds the chunk: one chunk = one build launch
     probe = spe.PathTable(g, att[:64], engine=args.engine)   # the engine AUTO picks for this graph
     lds_engine = probe.layout()["engine"] == spe.SPE_ENGINE_LDS
     probe.close()
-    # one chunk = one build launch: the LDS engine covers every block in one launch,
-    # the batch engine `groups` blocks (auto rule: ~2.4M (group, vertex) rows per round)
-    gpl = nblk if lds_engine else (args.groups if args.groups > 0 else auto_groups(info, nblk, A, world, dev))
     from shadow_amd import dist as sd
     shares = max(world, args.shares)
     emulated = shares != world   # one rank of a `shares`-GPU job: its chunks only, no gather
-    # per-round chunk sizes: at N > 1 a short first round starts the gathers early
-    sizes = sd.chunk_schedule(nblk, shares, gpl)
-    rounds, G = len(sizes), max(sizes)
-    mine = sd.rank_chunks_sched(nblk, shares, args.share_index if emulated else rank, sizes)
-    padded = shares * sum(sizes)
-    elems = padded * A * 64
     gather = world > 1 and not args.no_gather
-    # the table in caller-owned HBM (spe_table_opts.ext_*): every rank holds the
-    # whole record span (its own chunks built in place, the others' gathered in)
-    lr = torch.empty((elems, 2), dtype=torch.float64, device=dev)
-    nx = torch.empty(elems, dtype=torch.int32, device=dev)
-    hp = torch.empty(elems, dtype=torch.int16, device=dev)
-    t = spe.PathTable(g, att, blocks=(0, nblk), ext=[lr.data_ptr(), nx.data_ptr(), hp.data_ptr()], groups=G,
-                      engine=args.engine)
+    # one chunk = one build launch: the LDS engine covers every block in one launch,
+    # the batch engine `groups` blocks (auto rule above)
+    gpl = nblk if lds_engine else (args.groups if args.groups > 0 else auto_groups(info, nblk, A, world, dev))
     blk_elems = A * 64
+    pad_blocks = shares * sum(sd.chunk_schedule(nblk, shares, gpl))   # the pure-sharding span (>= nblk)
+    lr = torch.empty((pad_blocks * blk_elems, 2), dtype=torch.float64, device=dev)
+    # the table owns no storage of its own that is ever written: every build goes
+    # into the caller's buffers (spe_table_build_blocks_into); lr doubles as its
+    # nominal external storage
+    t = spe.PathTable(g, att, blocks=(0, nblk), ext=[lr.data_ptr(), lr.data_ptr(), lr.data_ptr()], groups=gpl,
+                      engine=args.engine)
+    calib = None
+    frac = 1.0 if not gather else args.shared_frac
+    if gather and frac < 0:   # auto: measure T1 and B on this job, then plan
+        calib = calibrate_split(t, lr, blk_elems, nblk, world, rank, dev, dist, pad_blocks)
+        frac = sd.shared_fraction(world, calib[0], nblk * blk_elems * 16.0, calib[1])
+    sizes, S = sd.split_schedule(nblk, shares, gpl, max(0.0, frac) if gather else 1.0)
+    slots, nslot = sd.rank_next_hop_slots(nblk, shares, args.share_index if emulated else rank, sizes, S)
+    # next hop (i32) and hop count (u16) of this rank's own blocks only, packed
+    nx = torch.empty(max(1, nslot) * blk_elems, dtype=torch.int32, device=dev)
+    hp = torch.empty(max(1, nslot) * blk_elems, dtype=torch.int16, device=dev)
+    nx_base, hp_base = nx.data_ptr(), hp.data_ptr()
+    mine = sd.rank_chunks_sched(nblk, shares, args.share_index if emulated else rank, sizes)
+    l0, l1 = sd.local_span(nblk, S)
+    slot_of = {(b0, b1): s0 for b0, b1, s0 in slots}
+
+    def into(b0, b1):
+        s0 = slot_of[(b0, b1)]
+        return t.build_blocks_into(b0, b1, lr[b0 * blk_elems:].data_ptr(), nx_base + s0 * blk_elems * 4,
+                                   hp_base + s0 * blk_elems * 2)
 
     def one_table():
         works, tb, tg, its = [], 0.0, 0.0, 0
         for k, off, gk, b0, b1 in mine:
             t0 = time.perf_counter()
             if b1 > b0:
-                its += t.build_blocks(b0, b1)["iterations"]
+                its += into(b0, b1)["iterations"]
             tb += time.perf_counter() - t0
-            if gather:   # overlaps the next round's build (RCCL runs on its own stream)
+            if gather:   # overlaps the next round's build and the local part (RCCL runs on its own stream)
                 w = sd.allgather_span(lr, off, gk, world, rank, blk_elems, dist, async_op=True)
                 if w is not None:
                     works.append(w)
+        if l1 > l0 and not emulated:   # built by every rank itself: no exchange
+            t0 = time.perf_counter()
+            its += into(l0, l1)["iterations"]
+            tb += time.perf_counter() - t0
         t1 = time.perf_counter()
         for w in works:
             w.wait()
@@ -461,11 +518,18 @@ def bench_table(args, rank, world, local, dist):
     barrier()
     el = time.perf_counter() - t0
     kp = t.kernel_profile() if not args.no_profile else None
-    x = torch.tensor([el, tb_sum, tg_sum], dtype=torch.float64, device=dev)
+    per_rank = None
     if dist is not None:
+        mine_t = torch.tensor([[el, tb_sum / steps, tg_sum / steps]], dtype=torch.float64, device=dev)
+        allt = [torch.empty_like(mine_t) for _ in range(world)]
+        dist.all_gather(allt, mine_t)
+        per_rank = [[round(float(v), 4) for v in a[0, 1:].tolist()] for a in allt]
+        x = torch.tensor([el, tb_sum, tg_sum], dtype=torch.float64, device=dev)
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
-    el, tb_sum, tg_sum = (float(v) for v in x.tolist())
+        el, tb_sum, tg_sum = (float(v) for v in x.tolist())
     built = sum(min(A, b1 * 64) - b0 * 64 for _, _, _, b0, b1 in mine if b1 > b0)
+    if not emulated and l1 > l0:
+        built += min(A, l1 * 64) - l0 * 64
     total = built if emulated else A
     value = total * steps / el
     lds = kp is not None and kp["lds"]["launches"] > 0
@@ -473,9 +537,11 @@ def bench_table(args, rank, world, local, dist):
     b_relax, b_rows = relax_bytes(info, A, lds, direct)
     roof, extra = None, {}
     if kp is not None:
-        # the batch engine's relaxation kernel: k_relax (<= 64 sources per row) or
-        # k_relax_m (128 / 256: several sources per thread)
-        relax_k = "k_relax_m" if t.layout()["lanes_per_group"] > 64 else "k_relax"
+        # the batch engine's relaxation kernel: k_relax (64 sources per row), k_relax_s
+        # (128, LDS-ring neighbour rows) or k_relax_m (128, register-staged)
+        lay = t.layout()
+        relax_k = ("k_relax" if lay["lanes_per_group"] <= 64 else
+                   "k_relax_s" if lay["relax_kernel"] == spe.SPE_RELAX_LDS_RING else "k_relax_m")
         kname = "k_sssp_lds" if lds else ("k_rows_direct" if direct else relax_k)
         rl = kp["lds" if lds else ("direct" if direct else "relax")]
         relax_s = rl["ms"] / 1e3
@@ -484,10 +550,10 @@ def bench_table(args, rank, world, local, dist):
         roof = {"bound": "hbm", "kernel": kname + (" (SSSP + rows, LDS-resident state)" if lds else
                                                    (" (DIRECT rows)" if direct else " (SSSP stage)")),
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(args, kname), "launches": rl["launches"],
+                "traffic": pmc_traffic(args, kname, config), "launches": rl["launches"],
                 "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
                 "algorithmic_bytes_per_source": b_relax,
-                "lanes_per_group": t.layout()["lanes_per_group"],
+                "lanes_per_group": lay["lanes_per_group"],
                 "bytes_basis": "relaxation graph: 12 m_relax + 28 n_relax + 8 (SURVEY 8d B_s minus the row stage)"}
         rw = kp["rows"]
         rows_s = rw["ms"] / 1e3
@@ -509,8 +575,9 @@ def bench_table(args, rank, world, local, dist):
                     "engine relaxes the pruned graph, so this overstates the kernel's achieved bandwidth"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not emulated:
-        cpu = cpu_baseline(top, att, args.cpu_seconds)
+        cpu = cpu_baseline(top, att, args.cpu_seconds, args.cpu_sources)
     if rank == 0:
+        gathered = int((world - 1) * sum(sizes) * blk_elems * 16) if gather else None
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "sources/s", "n_gpus": world, "steps": steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * el / steps, 3), "higher_is_better": True,
@@ -520,17 +587,24 @@ def bench_table(args, rank, world, local, dist):
                        "slot_order_ms": round(1e3 * t_ord, 1),
                        "step": "one whole path table (every source row)" + (
                            f"; emulated share {args.share_index} of {shares} (no gather)" if emulated else ""),
-                       "chunk_blocks": G, "rounds": rounds, "chunk_schedule": sizes,
-                       "parallelism": (f"source chunks round-robin over {world} GPUs, RCCL all-gather of the "
-                                       f"latency/reliability records overlapped with the next chunk's build"
+                       "chunk_blocks": max(sizes) if sizes else 0, "rounds": len(sizes), "chunk_schedule": sizes,
+                       "parallelism": (f"{S if S < nblk else nblk} of {nblk} source blocks in round-robin chunks over "
+                                       f"{world} GPUs with an RCCL all-gather of the latency/reliability records per "
+                                       f"round (overlapped), blocks [{l0}, {l1}) built by every GPU itself"
                                        if gather else f"{world} GPU(s), no collective")},
             "full_table_time_s": round(el / steps, 4) if not emulated else None,
             "build_s_per_step": round(tb_sum / steps, 4),
             "gather_wait_s_per_step": round(tg_sum / steps, 4) if gather else None,
-            "gather_bytes_per_gpu_per_step": int((world - 1) * sum(sizes) * blk_elems * 16) if gather else None,
+            "gather_bytes_per_gpu_per_step": gathered,
             "relax_rounds_per_step": round(it_total / max(1, steps), 1),
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if gather:
+            line["split"] = {"shared_fraction": round(frac, 4), "shared_blocks": min(S, nblk), "local_blocks": l1 - l0,
+                             "model": "x* = T1 N / ((N - 1) (S / B + T1)) (DESIGN 6)",
+                             "calibration": None if calib is None else {"t1_s": round(calib[0], 4),
+                                                                        "gather_GBps": round(calib[1] / 1e9, 1)},
+                             "per_rank_build_gather_s": per_rank}
         line.update(extra)
         if cpu:
             line["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)
@@ -546,15 +620,15 @@ def bench_table(args, rank, world, local, dist):
 # stands either way.
 SIDE_CONFIGS = (
     ("c5", ["--config", "c5", "--steps", "10", "--warmup", "2", "--cpu-seconds", "6"]),
-    ("c2", ["--config", "c2", "--cpu-seconds", "6"]),
-    ("c4", ["--config", "c4", "--steps", "2", "--cpu-seconds", "6"]),
-    ("c1", ["--config", "c1", "--cpu-seconds", "4"]),
+    ("c2", ["--config", "c2", "--cpu-seconds", "6", "--cpu-sources", "0"]),
+    ("c4", ["--config", "c4", "--steps", "2", "--cpu-seconds", "6"]),   # 1,000-source 1-core CPU sample (~50 s)
+    ("c1", ["--config", "c1", "--cpu-seconds", "4", "--cpu-sources", "0"]),
     ("c2fw", ["--config", "c2fw", "--steps", "1"]),   # the FW engine's whole C2 table
-    ("c5_on_c4", ["--config", "c5", "--c5-table", "c4", "--steps", "10", "--warmup", "2", "--no-cpu-baseline"]),
+    ("c5_on_c4", ["--config", "c5", "--c5-table", "c4", "--steps", "10", "--warmup", "2", "--cpu-seconds", "6"]),
 )
 
 
-def side_configs(timeout_s: float = 120.0):
+def side_configs(timeout_s: float = 240.0):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
@@ -586,6 +660,13 @@ def main():
     ap.add_argument("--groups", type=int, default=0, help="64-source blocks per build launch (0 = auto)")
     ap.add_argument("--engine", type=int, default=0, help="0 auto, 1 batch (64-lane HBM state), 2 LDS-resident rows")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-sources", type=int, default=1000,
+                    help="sources the 1-core CPU baseline times (BASELINE.md: 1,000; 0 = --cpu-seconds bound)")
+    ap.add_argument("--shared-frac", type=float, default=-1.0,
+                    help="N > 1: fraction of source blocks sharded + all-gathered, the rest built by every "
+                         "rank (-1 = from the measured build time and gather bandwidth, DESIGN 6)")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="N > 1: skip the C4 line measured after the C3 line in the same ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the all-gather (build only)")
@@ -626,10 +707,18 @@ def main():
         bench_lookup(args, rank, world, local, dist)
     else:
         line = bench_table(args, rank, world, local, dist)
+        import gc
+        import torch
+        if world > 1 and args.config == "c3" and not args.no_north_star and args.shares == 1:
+            # the north star's own target in the same ranks: the whole 200k-vertex /
+            # 100k-host table replicated on every GPU (C4), after the C3 table is freed
+            gc.collect()
+            torch.cuda.empty_cache()
+            c4 = bench_table(args, rank, world, local, dist, config="c4")
+            if line is not None:
+                line["side_configs"] = {"c4": c4}
         if line is not None:
             if world == 1 and args.config == "c3" and not args.no_side and args.shares == 1:
-                import gc
-                import torch
                 gc.collect()
                 torch.cuda.empty_cache()
                 line["side_configs"] = side_configs()

@@ -79,6 +79,8 @@ typedef struct spe_graph_desc {
     const double* vertex_packetloss;
     int32_t directed;
     int32_t prefer_direct;          /* graph attribute preferdirectpaths */
+    int32_t keep_pendants;          /* 1: relax over every vertex (no pendant pruning, so relaxation
+                                     * ids = vertex ids, e.g. for spe_fw_apsp's matrix); 0 = prune */
 } spe_graph_desc;
 
 typedef struct spe_graph_info {
@@ -119,10 +121,9 @@ typedef struct spe_table_opts {
                                      * either direction.  Needs a table owning all blocks; applied
                                      * by spe_table_build (not spe_table_build_blocks). */
     int32_t engine;                 /* SPE_ENGINE_* */
-    int32_t lanes_per_group;        /* sources sharing one relaxation frontier: 16, 32, 64, 128
-                                     * or 256 (128 / 256: each thread carries 2 / 4 sources);
-                                     * 0 = default: 128 when groups_per_launch is even (no
-                                     * padding lanes; C3 +2 % over 64), else 64 */
+    int32_t lanes_per_group;        /* sources sharing one relaxation frontier: 64 or 128 (each
+                                     * thread carries 2 sources); 0 = default: 128 when
+                                     * groups_per_launch is even (no padding lanes), else 64 */
     int32_t want_aux;               /* 1: also fold the graph's auxiliary edge attribute
                                      * (spe_graph_set_edge_aux) along every row's path, in path
                                      * order from 0.0 -- the offline completion tool's jitter sum
@@ -141,7 +142,31 @@ typedef struct spe_table_opts {
     const int32_t* devices;         /* n_devices device indices (NULL: the graph's device) */
     int32_t n_devices;              /* 0 or 1: single device */
     int32_t gather;                 /* SPE_GATHER_* */
+    /* Batch-engine tuning of 128-lane rows (64-lane rows ignore the first three); 0 everywhere =
+     * the measured defaults.  Tests and A/B experiments set these; the
+     * library reads no environment variables. */
+    int32_t relax_kernel;           /* SPE_RELAX_* (128-lane rows only) */
+    int32_t rows_in_flight;         /* neighbour rows per memory round trip (0 = default) */
+    int32_t waves_per_simd;         /* occupancy the relaxation kernel is held to (0 = the shape's
+                                     * default, 1 = the compiler's choice) */
+    int32_t no_overlap;             /* 1: batch i's rows do not overlap batch i+1's relaxation */
+    double delta_ms;                /* > 0: Delta-stepping schedule (measured slower) */
+    int32_t trace;                  /* 1: per-launch kernel times to stderr while profiling */
+    /* Multi-device compute-versus-gather split: the first S source blocks
+     * are sharded (contiguous shares, built in chunks whose records are broadcast to
+     * every device while the next chunk builds), the remaining blocks are built by
+     * every device itself.  S / nblk = shared_fraction when in (0, 1]; 0 = from the
+     * model x* = T1 N / ((N - 1)(span / B + T1)) with T1 = build_seconds_hint (or the
+     * library's estimate) and B = gather_gbps (or 300 GB/s). */
+    double shared_fraction;
+    double gather_gbps;
+    double build_seconds_hint;      /* one-device whole-table build time, if the caller measured it */
 } spe_table_opts;
+
+#define SPE_RELAX_AUTO 0            /* the default below */
+#define SPE_RELAX_REGISTER 1        /* k_relax_m: neighbour rows staged in registers */
+#define SPE_RELAX_LDS_RING 2        /* k_relax_s: neighbour rows gathered into a per-wave LDS ring by
+                                     * LDS-DMA, in-CSR bounds prefetched with the frontier word */
 
 #define SPE_GATHER_AUTO 0           /* RCCL when the devices are distinct and librccl loads, else PEER */
 #define SPE_GATHER_RCCL 1           /* ncclAllGather, in place, one communicator per device */
@@ -152,6 +177,13 @@ typedef struct spe_table_opts {
  * ceil(blocks / n_devices) (the all-gather's equal counts; a share past the end is
  * empty).  Host-only. */
 int spe_device_shares(int32_t n_attached, int32_t n_devices, int32_t* block_begin, int32_t* block_end);
+/* The multi-device split for shared_fraction x in [0, 1]: x = 1 is
+ * spe_device_shares (every block sharded, local_begin = the block count); x < 1
+ * gives every device an equal share of floor(x nblk / N) blocks of [0, S),
+ * S = N floor(x nblk / N), and *local_begin = S: blocks [S, nblk) are built by
+ * every device itself.  Host-only. */
+int spe_device_split(int32_t n_attached, int32_t n_devices, double shared_fraction, int32_t* block_begin,
+                     int32_t* block_end, int32_t* local_begin);
 
 /* Where a table keeps its rows.  Element (s_slot, t_slot) of a field lives at
  *   ((s_slot / 64 - block_begin) * n_attached + t_slot) * 64 + s_slot % 64
@@ -174,6 +206,7 @@ typedef struct spe_table_layout {
                                      * next_hop / hops are NULL (they stay with each share's device) */
     int32_t device;                 /* the device latrel lives on */
     int32_t lanes_per_group;        /* batch engine: sources per relaxation row (64 or 128 by default) */
+    int32_t relax_kernel;           /* batch engine: the SPE_RELAX_* kernel it runs */
 } spe_table_layout;
 
 typedef struct spe_entry {
@@ -191,6 +224,9 @@ typedef struct spe_build_stats {
     double gather_seconds;          /* multi-device: the all-gather of the records */
     int32_t n_devices;
     int32_t gather;                 /* the SPE_GATHER_* mode used */
+    int32_t shared_blocks;          /* multi-device: blocks sharded and gathered (the rest built on every device) */
+    int32_t local_blocks;
+    double build_wait_seconds;      /* multi-device: slowest device's build time (shares + local part) */
 } spe_build_stats;
 
 const char* spe_last_error(void);
@@ -240,6 +276,15 @@ int spe_table_build(spe_table* t, void* stream);
 /* Compute only source blocks [block_begin, block_end) (absolute block ids, a
  * sub-range of the owned ones): incremental / stepped builds. */
 int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end, void* stream);
+/* Build blocks [block_begin, block_end) of the owned range into caller device
+ * buffers instead of the table's storage: latrel / next_hop / hops address block
+ * block_begin's first element, in the SB64 layout of (block_end - block_begin)
+ * blocks.  The table's own rows are untouched and not marked built.  For
+ * schedules that place the records and the next hops / hop counts apart (a rank
+ * keeping the next hops of its own blocks only, beside a replicated record
+ * span).  Not for owner-replay or want_aux tables. */
+int spe_table_build_blocks_into(spe_table* t, int32_t block_begin, int32_t block_end, void* latrel,
+                                void* next_hop, void* hops, void* stream);
 
 /* Per-kernel device time, from HIP events recorded around every launch on the
  * build stream while profiling is enabled (costs one event pair per launch). */
@@ -296,6 +341,14 @@ int spe_table_download_aux(const spe_table* t, int32_t row_begin, int32_t row_en
  * owned by this table return ok = 0, latency = reliability = -1. */
 int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, double* d_latency,
                      double* d_reliability, uint8_t* d_ok, void* stream);
+/* The same against replica `replica` of a multi-device table (0 = the home
+ * device; for a single-device table only 0): pairs and outputs live on that
+ * replica's device (spe_table_replica_device), so every device answers its own
+ * batch from its own HBM (the C5 replicas; shd-worker.c:235-247 is
+ * the per-packet lookup it batches).  The stream, if given, is on that device. */
+int spe_lookup_batch_replica(const spe_table* t, int32_t replica, const int32_t* d_pairs, int64_t q,
+                             double* d_latency, double* d_reliability, uint8_t* d_ok, void* stream);
+int spe_table_replica_device(const spe_table* t, int32_t replica, int32_t* device);
 /* Minimum latency over every owned routable entry (minimumPathLatency). */
 /* On-disk path-table cache (the reference recomputes its paths
  * every run).  The key hashes everything that determines the rows: the graph

@@ -960,6 +960,162 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_relax_m(int32_t total, int32_t n
     if (__ballot(wrote) && lane == 0) *fl.any_changed = 1;
 }
 
+// ---- k_relax_s: the 128-lane relaxation with LDS-staged neighbour rows.
+// k_relax_m's item is a chain of dependent memory round trips (frontier word ->
+// in-CSR bounds -> in-list chunk and flags -> neighbour rows INFL at a time ->
+// parent routes), and the kernel spends ~80 % of its wave cycles waiting on
+// them.  Two of those trips go here:
+//  * the in-CSR bounds of a frontier unit's eight vertices are fetched with the
+//    unit's frontier word, one unit ahead, so an item issues its own distance
+//    row, its in-list chunk and its in-edge flags in ONE round trip;
+//  * the flagged neighbours' distance rows (1 KB each: 128 lanes x f64) are
+//    gathered straight into a per-wave LDS ring by LDS-DMA
+//    (global_load_lds_dwordx4: one wave instruction per row, no VGPR
+//    destination), NS rows per round trip instead of INFL register-staged rows,
+//    so a light vertex's flagged in-neighbours (4-5 on C3) arrive together and
+//    the kernel holds fewer live registers.
+// Offers, finish and marks are k_relax_m's (same canonical keys, same routes):
+// the relaxation order changes nothing in the fixpoint.
+template <int NS>
+struct RelaxRing {
+    double row[NS][2 * WAVE];   // one wave's LDS slots: 128 lanes of one neighbour row each
+};
+
+template <int NS>
+__device__ __forceinline__ bool relax_item_s(int64_t e, int32_t k0, int32_t k1, int32_t n, int32_t lane,
+                                             const int32_t* __restrict__ srcv, const DevGraph& G, const State& st,
+                                             const Flags& fl, RelaxRing<NS>* ring) {
+    constexpr int M = 2, L = WAVE * M;
+    int32_t g = 0, v = 0;
+    if (e >= 0) {
+        g = (int32_t)(e / n);
+        v = (int32_t)(e - (int64_t)g * n);
+    } else {
+        k0 = k1 = 0;
+    }
+    // round trip 1: sources, own row, in-list chunk, in-edge flags (all independent)
+    const int32_t k = k0 + lane;
+    const bool ok = k < k1;   // light vertex: in-degree <= 64, one chunk
+    const int4 pk = ok ? G.ipack[k] : make_int4(0, 0, 0, 0);
+    const size_t fo = (size_t)g * G.nrel + k;
+    const bool f = ok && fl.in_cur[fo] != 0;
+    Best b[M];
+    int32_t s[M];
+    double d_old[M];
+    bool active[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const int32_t j = lane + m * WAVE;
+        s[m] = e >= 0 ? srcv[g * L + j] : -1;
+        const size_t rv = sidx<L>(g, n, v, j);
+        d_old[m] = e >= 0 ? st.D[rv] : INF;
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const int32_t p = d_old[m] < INF ? PK_UNREAD : -1;
+        b[m] = Best{d_old[m], p, -1, -1.0, false, p, sidx<L>(g, n, v, lane + m * WAVE)};
+        active[m] = (e >= 0) && (s[m] != -1) && (s[m] != v);
+    }
+    const int32_t u_j = pk.x;
+    const double w_j = __hiloint2double(pk.w, pk.z);
+    if (f) fl.in_cur[fo] = 0;   // consumed
+    uint64_t sm = __ballot(f);
+    // round trip 2..: the flagged rows, NS per trip, into this wave's LDS ring
+    const double* gbase = st.D + (size_t)g * (size_t)n * L;
+    while (sm) {
+        int32_t bs[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            bs[q] = -1;
+            if (sm) {
+                bs[q] = __builtin_ctzll(sm);
+                sm &= sm - 1;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous trip's LDS reads are done
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+            if (bs[q] >= 0) {
+                const int32_t u = __builtin_amdgcn_readlane(u_j, bs[q]);
+                const double* src = gbase + (size_t)u * L + 2 * lane;   // 16 B per lane: the whole 1-KB row
+                __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)&ring->row[q][0], 16, 0, 0);
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            if (bs[q] < 0) continue;
+            const int32_t u = __builtin_amdgcn_readlane(u_j, bs[q]);
+            const double w = sub_get_d<WAVE>(w_j, bs[q]);
+            const int32_t kk = k0 + bs[q];
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                const double du = ring->row[q][lane + m * WAVE];
+                const double alt = du + w;
+                if (active[m] && alt > du) offer<L>(b[m], G, st, g, n, lane + m * WAVE, kk, u, du, alt);
+            }
+        }
+    }
+    bool changed = false;
+    if (e >= 0) changed = finish_vertex_m<M>(b, G, st, g, n, lane, v, s, d_old);
+    if (__ballot(changed)) {
+        if (G.undirected) {   // the out-list IS the in-list: marks from registers
+            if (ok) {
+                const int32_t orev = pk.y & 0x7FFFFFFF;
+                (pk.y < 0 ? fl.hmark_next : fl.mark_next)[(size_t)g * n + u_j] = 1;
+                fl.in_next[(size_t)g * G.nrel + orev] = 1;
+            }
+        } else {
+            mark_out<WAVE>(G, g, n, v, lane, fl);
+        }
+    }
+    return changed;
+}
+
+// in-CSR bounds (iptr[v], iptr[v + 1]) of item e = unit * 8 + lane, lanes 0..7
+__device__ __forceinline__ int2 unit_bounds(int64_t unit, int32_t lane, int32_t total, int32_t n, const int32_t* iptr) {
+    const int64_t e = unit * 8 + lane;
+    if (lane >= 8 || e >= total) return make_int2(0, 0);
+    const int32_t v = (int32_t)(e % n);
+    return make_int2(iptr[v], iptr[v + 1]);
+}
+
+template <int NS, int OCC = 1>
+__global__ __launch_bounds__(BLOCK, OCC) void k_relax_s(int32_t total, int32_t n, const int32_t* __restrict__ srcv,
+                                                      DevGraph G, State st, Flags fl) {
+    __shared__ RelaxRing<NS> rings[BLOCK / WAVE];
+    if (*fl.prev_changed == 0) return;
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    RelaxRing<NS>* ring = &rings[threadIdx.x >> 6];
+    uint64_t* words = reinterpret_cast<uint64_t*>(fl.mark_cur);
+    const int64_t all_units = ((int64_t)total + 7) >> 3;
+    const int32_t xcd = blockIdx.x & 7;
+    const int64_t waves_per_xcd = ((int64_t)(gridDim.x >> 3) * BLOCK) >> 6;
+    const int64_t wave = ((int64_t)(blockIdx.x >> 3) * BLOCK + threadIdx.x) >> 6;
+    const int64_t lo = all_units * xcd / 8, hi = all_units * (xcd + 1) / 8;
+    bool wrote = false;
+    int64_t u8 = lo + wave;
+    uint64_t w_ahead = u8 < hi ? words[u8] : 0;
+    int2 b_ahead = u8 < hi ? unit_bounds(u8, lane, total, n, G.iptr) : make_int2(0, 0);
+    for (; u8 < hi; u8 += waves_per_xcd) {
+        const uint64_t w = uniform_u64(w_ahead);
+        const int2 bnd = b_ahead;
+        const int64_t nx = u8 + waves_per_xcd;
+        w_ahead = nx < hi ? words[nx] : 0;
+        b_ahead = nx < hi ? unit_bounds(nx, lane, total, n, G.iptr) : make_int2(0, 0);
+        if (!w) continue;
+        if (lane == 0) words[u8] = 0;   // taken
+        for (uint32_t bm = byte_mask(w); bm; bm &= bm - 1) {
+            const int32_t bit = __builtin_ctz(bm);
+            int64_t e = u8 * 8 + bit;
+            if (e >= total) e = -1;
+            const int32_t k0 = __builtin_amdgcn_readlane(bnd.x, bit);
+            const int32_t k1 = __builtin_amdgcn_readlane(bnd.y, bit);
+            wrote |= relax_item_s<NS>(e, k0, k1, n, lane, srcv, G, st, fl, ring);
+        }
+    }
+    if (__ballot(wrote) && lane == 0) *fl.any_changed = 1;
+}
+
 template <int M, int INFL>
 __global__ __launch_bounds__(BLOCK) void k_heavy_partial_m(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
                                                            DevGraph G, State st, HeavyPlan hp, Partial pp, Flags fl) {
@@ -2479,13 +2635,20 @@ struct spe_table {
     uint64_t key = 0;              // on-disk cache key (spe_table_key)
     int32_t A = 0;
     int32_t blk0 = 0, blk1 = 0;
+    int32_t row_base = 0;          // the block tb's pointers start at (blk0; spe_table_build_blocks_into moves it)
     int32_t groups = 8;            // 64-source blocks per batch
     int32_t lanes = 16;            // sources per lane group (L)
     int32_t engine = SPE_ENGINE_BATCH;   // resolved engine
-    int32_t infl = 8;              // neighbour rows in flight per subgroup (2, 3, 4, 6 or 8)
-    bool trace = getenv("SPE_TRACE") != nullptr;   // diagnostic: per-launch times to stderr
+    int32_t relax_kernel = SPE_RELAX_REGISTER;   // resolved SPE_RELAX_* (batch engine)
+    int32_t infl = 8;              // neighbour rows per round trip (register: in flight per wave; ring: LDS slots)
+    bool trace = false;            // per-launch times to stderr while profiling (spe_table_opts.trace)
     unsigned long long* d_lds_dbg = nullptr;       // diagnostic (SPE_LDS_DEBUG): LDS engine phase clocks
-    int32_t occ = 0;               // forced waves/SIMD of k_relax (0 = compiler's choice; 6 at 128 lanes)
+#ifdef SPE_DIAGNOSTICS
+    bool lds_debug = getenv("SPE_LDS_DEBUG") != nullptr;   // diagnostic builds only
+#else
+    static constexpr bool lds_debug = false;
+#endif
+    int32_t occ = 0;               // waves/SIMD the relaxation kernel is held to (0 = compiler's choice)
     RowMode md{};
     bool ext = false;
     bool built = false;              // every owned block holds its rows
@@ -2583,6 +2746,17 @@ int check_device(int32_t device) {
     return SPE_OK;
 }
 
+// The relaxation shapes instantiated in relax_to_convergence (keep in sync).
+#define RELAX_DEFAULT_128 SPE_RELAX_LDS_RING
+#define RELAX_RING_NS 4
+bool relax_shape_supported(int32_t lanes, int32_t kernel, int32_t infl, int32_t occ, bool delta) {
+    if (delta) return true;   // fixed shapes
+    if (lanes == 64) return infl == 8 && occ <= 1;
+    if (kernel == SPE_RELAX_LDS_RING)
+        return (infl == 4 && (occ <= 1 || occ == 8)) || (infl == 6 && (occ <= 1 || occ == 6)) || (infl == 8 && occ <= 1);
+    return (infl == 4 && occ <= 1) || (infl == 2 && (occ <= 1 || occ == 6));
+}
+
 int grid_for(int64_t work_items, int64_t per_block, int cap = 8192) {
     int64_t b = (work_items + per_block - 1) / per_block;
     if (b < 1) b = 1;
@@ -2639,7 +2813,7 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
         f.val(desc->prefer_direct);
         g->key = f.h;
     }
-    spe::prune_pendants(&g->hg, getenv("SPE_NO_PRUNE") == nullptr);
+    spe::prune_pendants(&g->hg, desc->keep_pendants == 0);
     r = graph_upload(g);
     if (r) {
         spe_graph_free(g);
@@ -2917,8 +3091,7 @@ int spe_order_sources(const spe_graph* g, const int32_t* attached, int32_t n_att
     // Voronoi cells of ceil(A / 64) seeded-random centres over the relaxation
     // graph (multi-source Dijkstra on the in-CSR): a 64-source block then holds
     // sources that are close to one another, whose lanes advance in similar rounds
-    int32_t per_cell = WAVE;
-    if (getenv("SPE_ORDER_CELL")) per_cell = std::max(1, atoi(getenv("SPE_ORDER_CELL")));   // diagnostic
+    const int32_t per_cell = WAVE;   // cells of 16..512 sources measured flat within +-4 %
     const size_t K = std::min(distinct.size(), (size_t)((n_attached + per_cell - 1) / per_cell));
     std::vector<int32_t> cell((size_t)h.nc, INT32_MAX);
     std::vector<double> dist((size_t)h.nc, INF);
@@ -3014,6 +3187,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         t->blk0 = o.block_begin;
         t->blk1 = o.block_end;
     }
+    t->row_base = t->blk0;
     const bool force = o.force_sssp != 0;
     {   // table cache key: graph, attached set, and every option that changes a row
         Fnv f;
@@ -3098,38 +3272,26 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     t->groups = std::max(1, std::min(groups, owned));
     // sources per lane group (shared frontier); 64/L groups per 64-source block
     int32_t lanes = o.lanes_per_group;
-    if (lanes <= 0 && getenv("SPE_LANES")) lanes = atoi(getenv("SPE_LANES"));
     // default: 128 sources per relaxation row (2 per thread) when every full build
     // launch covers an even or a large block count, else 64.
     // Same-box A/B, three pairs: C3 +1.4..2.1 %, C4 within +-0.5 %.
     // (an odd launch pads one block of empty lanes: 1 / (groups + 1) extra work)
     if (lanes <= 0) lanes = (t->groups >= 2 && (t->groups % 2 == 0 || t->groups >= 32)) ? 128 : 64;
-    if (lanes != 16 && lanes != 32 && lanes != 64 && lanes != 128 && lanes != 256) {
+    if (lanes != 64 && lanes != 128) {
         delete t;
-        return fail(SPE_EINVAL, "lanes_per_group must be 16, 32, 64, 128 or 256");
+        return fail(SPE_EINVAL, "lanes_per_group must be 64 or 128");
     }
     t->lanes = lanes;
     {
         const bool fits = lds_bytes(g->hg.nc) <= (size_t)LDS_MAX_BYTES && g->hg.nc <= LDS_VPT * LDS_T;
         int32_t e = o.engine;
-        bool from_env = false;
-        if (e == SPE_ENGINE_AUTO && !o.want_aux && getenv("SPE_ENGINE")) {   // test / diagnostic override
-            e = atoi(getenv("SPE_ENGINE"));
-            from_env = true;
-        }
         if (e == SPE_ENGINE_FW && !t->md.complete && (int64_t)g->hg.nc > FW_MAX_N) {
-            if (!from_env) {
-                delete t;
-                return fail(SPE_EUNSUPPORTED, "relaxation graph too large for the FW engine (n^2 closure)");
-            }
-            e = SPE_ENGINE_BATCH;
+            delete t;
+            return fail(SPE_EUNSUPPORTED, "relaxation graph too large for the FW engine (n^2 closure)");
         }
         if (e == SPE_ENGINE_LDS && !fits) {
-            if (!from_env) {
-                delete t;
-                return fail(SPE_EUNSUPPORTED, "relaxation graph too large for the LDS engine");
-            }
-            e = SPE_ENGINE_BATCH;
+            delete t;
+            return fail(SPE_EUNSUPPORTED, "relaxation graph too large for the LDS engine");
         }
         t->engine = (e == SPE_ENGINE_AUTO) ? (fits ? SPE_ENGINE_LDS : SPE_ENGINE_BATCH) : e;
         if (t->engine == SPE_ENGINE_LDS && !t->md.complete) {
@@ -3145,15 +3307,39 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         }
     }
     if (t->engine == SPE_ENGINE_FW) t->lanes = lanes = WAVE;   // its state walk writes 64-lane rows
-    // rows in flight per k_relax wave: 8 at 64 lanes; at 128 lanes 2, with the
-    // kernel held to 6 waves / SIMD (80 VGPRs, a few spilled) — more waves beat
-    // deeper per-wave gathers there
-    t->infl = lanes == 64 ? 8 : lanes == 128 ? 2 : 4;
-    if (getenv("SPE_INFL")) {
-        const int want = atoi(getenv("SPE_INFL"));
-        if (want == 4 || want == 8 || (lanes == 64 && want == 6) || (lanes == 256 && want == 2) || (lanes == 128 && (want == 2 || want == 3))) t->infl = want;
+    // relaxation kernel and its shape.  64 lanes: k_relax, 8 rows in flight.  128
+    // lanes: k_relax_s (LDS ring, RELAX_RING_NS rows per trip) or k_relax_m (2 rows
+    // in flight held to 6 waves / SIMD).  Unsupported shapes are refused.
+    // (the kernel / rows / waves tuning applies to 128-lane rows; 64-lane rows run k_relax as measured)
+    t->delta = o.delta_ms > 0.0 ? o.delta_ms : 0.0;
+    const bool wide = lanes == 128;
+    t->relax_kernel = !wide ? SPE_RELAX_REGISTER
+                            : (o.relax_kernel != SPE_RELAX_AUTO ? o.relax_kernel
+                                                                : (t->delta == 0.0 ? RELAX_DEFAULT_128 : SPE_RELAX_REGISTER));
+    if (t->relax_kernel == SPE_RELAX_LDS_RING && t->delta > 0.0) {
+        delete t;
+        return fail(SPE_EUNSUPPORTED, "the LDS-ring relaxation runs 128-lane rows without the Delta schedule");
     }
-    t->occ = getenv("SPE_OCC") ? atoi(getenv("SPE_OCC")) : (lanes == 128 && t->infl == 2 ? 6 : 0);
+    // waves_per_simd 0 = the default for the shape, 1 = the compiler's choice
+    if (t->relax_kernel == SPE_RELAX_LDS_RING) {
+        t->infl = o.rows_in_flight > 0 ? o.rows_in_flight : RELAX_RING_NS;
+        t->occ = o.waves_per_simd > 0 ? o.waves_per_simd : (t->infl == 4 ? 8 : t->infl == 6 ? 6 : 1);
+    } else if (!wide) {
+        t->infl = 8;
+        t->occ = 1;
+    } else {
+        t->infl = o.rows_in_flight > 0 ? o.rows_in_flight : 2;
+        t->occ = o.waves_per_simd > 0 ? o.waves_per_simd : (t->infl == 2 ? 6 : 1);
+        if (t->delta > 0.0) {   // the Delta schedule's own instantiations
+            t->infl = lanes == 64 ? 8 : 4;
+            t->occ = 0;
+        }
+    }
+    if (!relax_shape_supported(t->lanes, t->relax_kernel, t->infl, t->occ, t->delta > 0.0)) {
+        delete t;
+        return fail(SPE_EUNSUPPORTED, "relaxation shape (rows_in_flight, waves_per_simd) not built");
+    }
+    t->trace = o.trace != 0;
     t->tb.A = n_attached;
     const size_t elems = (size_t)(t->blk1 - t->blk0) * n_attached * WAVE;
     int r = SPE_OK;
@@ -3230,7 +3416,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     const size_t GW = GL * (size_t)t->lanes;   // source entries per batch (>= G * 64: padding lanes)
     if (!t->md.complete && t->engine == SPE_ENGINE_BATCH) {
         const size_t se = GW * n;
-        t->overlap = !getenv("SPE_NO_OVERLAP");
+        t->overlap = o.no_overlap == 0;
         for (int i = 0; i < (t->overlap ? 2 : 1); ++i) {
             TRY(dev_alloc(t->allocs, &t->st_buf[i].D, se));
             TRY(dev_alloc(t->allocs, &t->st_buf[i].P, se));
@@ -3250,8 +3436,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         TRY(dev_alloc(t->allocs, &t->pp.uk, pe));
         t->max_iters = 4 * n + 64;
         TRY(dev_alloc(t->allocs, &t->counts, (size_t)t->max_iters + 2));
-        if (getenv("SPE_DELTA") && atof(getenv("SPE_DELTA")) > 0.0 && (t->lanes == 64 || t->lanes == 128)) {
-            t->delta = atof(getenv("SPE_DELTA"));
+        if (t->delta > 0.0) {
             t->max_iters = 64 * n + 4096;   // buckets add rounds
             TRY(dev_alloc(t->allocs, &t->counts, (size_t)t->max_iters + 2));
             TRY(dev_alloc(t->allocs, &t->ds.bound, GL));
@@ -3422,8 +3607,9 @@ int fw_pivot_rows(const FwPart& p, int32_t kb, int32_t rb0, int32_t rb1) {
 }
 }  // namespace spe
 
-template <int L, int INFL, int OCC = 1, bool DELTA = false>
+template <int L, int INFL, int OCC = 1, bool DELTA = false, bool RING = false>
 static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
+    static_assert(!RING || (L == 2 * WAVE && !DELTA), "the LDS-ring kernel runs 128-lane rows, no Delta schedule");
     constexpr int M = L > WAVE ? L / WAVE : 1;    // lanes per thread
     const spe_graph* g = t->g;
     const int32_t n = g->hg.nc;
@@ -3433,7 +3619,8 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     // one resident wave per hardware slot (no second wave of late blocks), multiple of 8 (XCD split)
     int per_cu = 0, cus = 0;
     const void* kfn;
-    if constexpr (M > 1) kfn = (const void*)k_relax_m<M, INFL, OCC, DELTA>;
+    if constexpr (RING) kfn = (const void*)k_relax_s<INFL, OCC>;
+    else if constexpr (M > 1) kfn = (const void*)k_relax_m<M, INFL, OCC, DELTA>;
     else kfn = (const void*)k_relax<L, INFL, OCC, DELTA>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, BLOCK, 0) != hipSuccess || per_cu < 1)
         per_cu = 4;
@@ -3477,7 +3664,9 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
             if constexpr (DELTA) fl.hmark_next = fl.mark_next;   // heavy rows relaxed by k_relax too
             {
                 LaunchTimer lt(t, s, SPE_K_RELAX);
-                if constexpr (M > 1)
+                if constexpr (RING)
+                    k_relax_s<INFL, OCC><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev, t->st, fl);
+                else if constexpr (M > 1)
                     k_relax_m<M, INFL, OCC, DELTA><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev,
                                                                                 t->st, fl, t->ds);
                 else
@@ -3520,29 +3709,19 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
 }
 
 static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
-    const bool deep = t->infl == 8;
-    if (t->delta > 0.0)   // experimental schedule
+    if (t->delta > 0.0)   // measured slower
         return t->lanes == 128 ? relax_to_convergence_l<128, 4, 1, true>(t, blocks, s)
                                : relax_to_convergence_l<64, 8, 1, true>(t, blocks, s);
-    switch (t->lanes) {
-        case 128:
-            if (t->infl == 3) return t->occ == 6 ? relax_to_convergence_l<128, 3, 6>(t, blocks, s) : relax_to_convergence_l<128, 3>(t, blocks, s);
-            if (t->occ == 6 && t->infl == 4) return relax_to_convergence_l<128, 4, 6>(t, blocks, s);
-            if (t->infl == 2) {
-                if (t->occ == 7) return relax_to_convergence_l<128, 2, 7>(t, blocks, s);
-                return t->occ == 6 ? relax_to_convergence_l<128, 2, 6>(t, blocks, s) : relax_to_convergence_l<128, 2>(t, blocks, s);
-            }
-            return deep ? relax_to_convergence_l<128, 8>(t, blocks, s) : relax_to_convergence_l<128, 4>(t, blocks, s);
-        case 256:
-            return t->infl == 2 ? relax_to_convergence_l<256, 2>(t, blocks, s) : relax_to_convergence_l<256, 4>(t, blocks, s);
-        case 16: return deep ? relax_to_convergence_l<16, 8>(t, blocks, s) : relax_to_convergence_l<16, 4>(t, blocks, s);
-        case 32: return deep ? relax_to_convergence_l<32, 8>(t, blocks, s) : relax_to_convergence_l<32, 4>(t, blocks, s);
-        default:
-            if (t->occ == 7) return relax_to_convergence_l<64, 8, 7>(t, blocks, s);
-            if (t->occ == 8) return relax_to_convergence_l<64, 8, 8>(t, blocks, s);
-            if (t->infl == 6) return relax_to_convergence_l<64, 6>(t, blocks, s);
-            return deep ? relax_to_convergence_l<64, 8>(t, blocks, s) : relax_to_convergence_l<64, 4>(t, blocks, s);
+    if (t->lanes == 64) return relax_to_convergence_l<64, 8>(t, blocks, s);
+    if (t->relax_kernel == SPE_RELAX_LDS_RING) {
+        if (t->infl == 4) return t->occ == 8 ? relax_to_convergence_l<128, 4, 8, false, true>(t, blocks, s)
+                                             : relax_to_convergence_l<128, 4, 1, false, true>(t, blocks, s);
+        if (t->infl == 6) return t->occ == 6 ? relax_to_convergence_l<128, 6, 6, false, true>(t, blocks, s)
+                                             : relax_to_convergence_l<128, 6, 1, false, true>(t, blocks, s);
+        return relax_to_convergence_l<128, 8, 1, false, true>(t, blocks, s);
     }
+    if (t->infl == 4) return relax_to_convergence_l<128, 4>(t, blocks, s);
+    return t->occ == 6 ? relax_to_convergence_l<128, 2, 6>(t, blocks, s) : relax_to_convergence_l<128, 2>(t, blocks, s);
 }
 
 static void launch_rows_sssp(spe_table* t, int grid, int32_t blocks, int32_t sb0, hipStream_t s) {
@@ -3557,10 +3736,7 @@ static void launch_rows_sssp(spe_table* t, int grid, int32_t blocks, int32_t sb0
                                                           g->dev, t->md, t->st, t->tb);                       \
     } while (0)
     switch (t->lanes) {
-        case 16: ROWS(16); break;
-        case 32: ROWS(32); break;
         case 128: ROWS(128); break;
-        case 256: ROWS(256); break;
         default: ROWS(64); break;
     }
 #undef ROWS
@@ -3585,11 +3761,41 @@ int spe_table_build(spe_table* t, void* stream) {
     return SPE_OK;
 }
 
+static int build_blocks_impl(spe_table* t, int32_t block_begin, int32_t block_end, void* stream);
+
 int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end, void* stream) {
     if (!t) return fail(SPE_EINVAL, "NULL table");
     if (t->multi) return fail(SPE_EUNSUPPORTED, "a multi-device table builds whole (spe_table_build)");
     if (block_begin < t->blk0 || block_end > t->blk1 || block_begin > block_end)
         return fail(SPE_EINVAL, "block range not owned by this table");
+    const int r = build_blocks_impl(t, block_begin, block_end, stream);
+    if (r) return r;
+    for (int32_t b = block_begin; b < block_end; ++b) t->blk_built[(size_t)(b - t->blk0)] = 1;
+    t->built = std::all_of(t->blk_built.begin(), t->blk_built.end(), [](uint8_t x) { return x != 0; });
+    return SPE_OK;
+}
+
+int spe_table_build_blocks_into(spe_table* t, int32_t block_begin, int32_t block_end, void* latrel, void* next_hop,
+                                void* hops, void* stream) {
+    if (!t) return fail(SPE_EINVAL, "NULL table");
+    if (t->multi) return fail(SPE_EUNSUPPORTED, "a multi-device table builds whole (spe_table_build)");
+    if (block_begin < t->blk0 || block_end > t->blk1 || block_begin > block_end)
+        return fail(SPE_EINVAL, "block range not owned by this table");
+    if (!latrel || !next_hop || !hops) return fail(SPE_EINVAL, "spe_table_build_blocks_into needs all three fields");
+    if (t->tb.prev || t->tb.aux) return fail(SPE_EUNSUPPORTED, "owner-replay / want_aux tables build in place");
+    const Table keep = t->tb;
+    const int32_t keep_base = t->row_base;
+    t->tb.lr = (double2*)latrel;
+    t->tb.next = (int32_t*)next_hop;
+    t->tb.hops = (uint16_t*)hops;
+    t->row_base = block_begin;
+    const int r = build_blocks_impl(t, block_begin, block_end, stream);
+    t->tb = keep;
+    t->row_base = keep_base;
+    return r;   // the table's own storage is untouched: nothing is marked built
+}
+
+static int build_blocks_impl(spe_table* t, int32_t block_begin, int32_t block_end, void* stream) {
     HIP_TRY(hipSetDevice(t->g->device));
     hipStream_t s = stream ? (hipStream_t)stream : t->stream;
     const auto t0 = std::chrono::steady_clock::now();
@@ -3621,7 +3827,7 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
         HIP_TRY(hipMemcpyAsync(t->d_srcv, t->h_srcv, sizeof(int32_t) * pb * WAVE, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(t->d_srcc, t->h_srcv + pb * WAVE, sizeof(int32_t) * pb * WAVE,
                                hipMemcpyHostToDevice, s));
-        const int32_t sb0 = b - t->blk0;
+        const int32_t sb0 = b - t->row_base;
         const int64_t items = (int64_t)groups * t->A;
         const int row_grid = grid_for(items * WAVE, BLOCK, 8192);
         if (t->md.complete) {
@@ -3634,11 +3840,11 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
                 const size_t bytes = lds_bytes(g->hg.nc);
                 int grid = std::min(s1 - s0, t->lds_grid);
                 if (grid >= 8) grid -= grid % 8;   // whole XCD rounds (see k_sssp_lds's slot order)
-                if (getenv("SPE_LDS_DEBUG") && !t->d_lds_dbg) {
+                if (t->lds_debug && !t->d_lds_dbg) {
                     if (int r = dev_alloc(t->allocs, &t->d_lds_dbg, 16)) return r;
                     HIP_TRY(hipMemset(t->d_lds_dbg, 0, 16 * sizeof(unsigned long long)));
                 }
-                k_sssp_lds<<<std::max(1, grid), LDS_T, bytes, s>>>(s0, s1, t->d_slots, t->blk0, g->dev, t->md, t->tb,
+                k_sssp_lds<<<std::max(1, grid), LDS_T, bytes, s>>>(s0, s1, t->d_slots, t->row_base, g->dev, t->md, t->tb,
                                                                    t->lsc, t->d_lds_dbg);
                 if (t->d_lds_dbg) {
                     unsigned long long h[16];
@@ -3720,8 +3926,6 @@ int spe_table_build_blocks(spe_table* t, int32_t block_begin, int32_t block_end,
     HIP_TRY(hipStreamSynchronize(s));
     t->stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     t->stats.n_devices = 1;
-    for (int32_t b = block_begin; b < block_end; ++b) t->blk_built[(size_t)(b - t->blk0)] = 1;
-    t->built = std::all_of(t->blk_built.begin(), t->blk_built.end(), [](uint8_t x) { return x != 0; });
     return SPE_OK;
 }
 
@@ -3763,6 +3967,7 @@ int spe_table_layout_get(const spe_table* t, spe_table_layout* out) {
     out->groups_per_launch = t->groups;
     out->engine = t->engine;
     out->lanes_per_group = t->lanes;
+    out->relax_kernel = t->relax_kernel;
     return SPE_OK;
 }
 
@@ -3901,13 +4106,30 @@ int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, doub
     if (!t || (q > 0 && (!d_pairs || !d_latency || !d_reliability || !d_ok))) return fail(SPE_EINVAL, "bad arguments");
     if (!t->built) return fail(SPE_ESTATE, "table not built");
     if (q == 0) return SPE_OK;
-    if (t->multi) return spe::multi_lookup(t->multi, d_pairs, q, d_latency, d_reliability, d_ok, stream);
+    return spe_lookup_batch_replica(t, 0, d_pairs, q, d_latency, d_reliability, d_ok, stream);
+}
+
+int spe_lookup_batch_replica(const spe_table* t, int32_t replica, const int32_t* d_pairs, int64_t q,
+                             double* d_latency, double* d_reliability, uint8_t* d_ok, void* stream) {
+    if (!t || (q > 0 && (!d_pairs || !d_latency || !d_reliability || !d_ok))) return fail(SPE_EINVAL, "bad arguments");
+    if (!t->built) return fail(SPE_ESTATE, "table not built");
+    if (q == 0) return SPE_OK;
+    if (t->multi) return spe::multi_lookup(t->multi, replica, d_pairs, q, d_latency, d_reliability, d_ok, stream);
+    if (replica != 0) return fail(SPE_EINVAL, "a single-device table has one replica (0)");
     HIP_TRY(hipSetDevice(t->g->device));
     hipStream_t s = stream ? (hipStream_t)stream : t->stream;
     k_lookup<1><<<grid_for(q, BLOCK, 16384), BLOCK, 0, s>>>((const int2*)d_pairs, q, t->blk0, t->blk1, t->tb,
                                                            d_latency, d_reliability, d_ok);
     HIP_TRY(hipGetLastError());
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
+    return SPE_OK;
+}
+
+int spe_table_replica_device(const spe_table* t, int32_t replica, int32_t* device) {
+    if (!t || !device) return fail(SPE_EINVAL, "NULL argument");
+    if (t->multi) return spe::multi_replica_device(t->multi, replica, device);
+    if (replica != 0) return fail(SPE_EINVAL, "a single-device table has one replica (0)");
+    *device = t->g->device;
     return SPE_OK;
 }
 

@@ -72,8 +72,11 @@ bool multi_built(const MultiDev* m);
 int multi_get(const MultiDev* m, int32_t s_slot, int32_t t_slot, spe_entry* out);
 int multi_download(const MultiDev* m, int32_t row_begin, int32_t row_end, double* latency, double* reliability,
                    int32_t* next_hop, int32_t* hops);
-int multi_lookup(const MultiDev* m, const int32_t* d_pairs, int64_t q, double* d_latency, double* d_reliability,
-                 uint8_t* d_ok, void* stream);
+int multi_lookup(const MultiDev* m, int32_t replica, const int32_t* d_pairs, int64_t q, double* d_latency,
+                 double* d_reliability, uint8_t* d_ok, void* stream);
+int multi_replica_device(const MultiDev* m, int32_t replica, int32_t* device);
+// x* of the compute-versus-gather split
+double multi_shared_fraction(int32_t n_dev, double t1_s, double span_bytes, double gather_bps);
 int multi_min_latency(const MultiDev* m, double* out);
 int multi_layout(const MultiDev* m, spe_table_layout* out);
 int multi_profile_enable(MultiDev* m, int32_t enable);

@@ -21,7 +21,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -72,23 +74,44 @@ int hip_fail(const char* what, hipError_t e) { return set_error(SPE_EHIP, std::s
 }  // namespace
 
 struct MultiDev {
-    int32_t A = 0, nblk = 0, cb = 0, n = 0;
+    int32_t A = 0, nblk = 0, n = 0;
+    int32_t cb = 0;                        // blocks per share of the sharded region
+    int32_t S = 0;                         // sharded blocks [0, S); every device builds [S, nblk) itself
+    int32_t span = 0;                      // replica blocks: max(n * cb, nblk) (pure sharding pads the last share)
+    int32_t chunk = 1;                     // blocks a share sends per gather round (one build launch)
     int32_t gather = SPE_GATHER_PEER;
+    double shared_fraction = 1.0;
     std::vector<int32_t> devs;
-    std::vector<int32_t> b0, b1;           // share of each device
+    std::vector<int32_t> b0, b1;           // share of each device (clipped to S)
     spe_graph* home = nullptr;             // the caller's graph (not owned)
     std::vector<spe_graph*> graphs;        // per device: home, or a clone on that device
-    std::vector<spe_table*> parts;         // nullptr for an empty share
-    std::vector<void*> replica;            // full {lat, rel} span per device: n * cb blocks
+    std::vector<spe_table*> parts;         // the share's part table; nullptr for an empty share
+    std::vector<spe_table*> lparts;        // the local remainder's part table (nullptr: S == nblk)
+    std::vector<void*> replica;            // full {lat, rel} span per device
     std::vector<void*> next, hops;         // the device's own share
-    std::vector<hipStream_t> streams;
+    std::vector<void*> lnext, lhops;       // the device's own copy of the local remainder
+    std::vector<hipStream_t> streams;      // per device: the gather stream
     std::vector<ncclComm_t> comms;
     bool built = false;
     bool fw = false;                       // FW-engine parts: one closure across the devices
     spe_build_stats stats{};
 
     size_t blk_elems() const { return (size_t)A * kWave; }
+    size_t blk_bytes() const { return blk_elems() * 2 * sizeof(double); }
 };
+
+// The a-priori one-device build time the split model uses when the caller gives
+// none: relaxation ~1.5e-10 s per (source, relaxation vertex) and rows at ~3.4 TB/s
+// of 22-B entries (within ~25 % of the measured C3 / C4 tables).
+static double build_time_estimate(int32_t n_relax, int32_t A) {
+    return 1.5e-10 * (double)n_relax * (double)A + 22.0 * (double)A * (double)A / 3.4e12;
+}
+
+double multi_shared_fraction(int32_t n_dev, double t1_s, double span_bytes, double gather_bps) {
+    if (n_dev <= 1 || t1_s <= 0.0 || gather_bps <= 0.0) return 1.0;
+    const double x = t1_s * n_dev / ((n_dev - 1) * (span_bytes / gather_bps + t1_s));
+    return std::min(1.0, std::max(0.0, x));
+}
 
 int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_table_opts& o, MultiDev** out) {
     *out = nullptr;
@@ -96,6 +119,7 @@ int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_tab
         return set_error(SPE_EUNSUPPORTED, "a multi-device table owns every block and its own storage "
                                            "(no block range, external storage, owner replay or want_aux)");
     if (o.gather < SPE_GATHER_AUTO || o.gather > SPE_GATHER_PEER) return set_error(SPE_EINVAL, "unknown gather mode");
+    if (o.shared_fraction < 0.0 || o.shared_fraction > 1.0) return set_error(SPE_EINVAL, "shared_fraction must be in [0, 1]");
     spe_graph_info gi;
     spe_graph_info_get(g, &gi);
     auto* m = new MultiDev();
@@ -104,10 +128,24 @@ int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_tab
     m->n = o.n_devices;
     m->devs.assign(o.devices, o.devices + o.n_devices);
     m->nblk = (A + kWave - 1) / kWave;
+    // the split: FW parts share one closure over the shares, so they never split
+    double x = 1.0;
+    if (o.engine != SPE_ENGINE_FW) {
+        if (o.shared_fraction > 0.0) {
+            x = o.shared_fraction;
+        } else {
+            const double t1 = o.build_seconds_hint > 0.0 ? o.build_seconds_hint : build_time_estimate(gi.n_relax_vertices, A);
+            const double bps = (o.gather_gbps > 0.0 ? o.gather_gbps : 300.0) * 1e9;
+            x = multi_shared_fraction(m->n, t1, (double)m->nblk * m->blk_bytes(), bps);
+        }
+    }
+    m->shared_fraction = x;
     m->b0.resize(m->n);
     m->b1.resize(m->n);
-    spe_device_shares(A, m->n, m->b0.data(), m->b1.data());
-    m->cb = (m->nblk + m->n - 1) / m->n;
+    spe_device_split(A, m->n, x, m->b0.data(), m->b1.data(), &m->S);
+    m->cb = m->n > 0 ? std::max(0, m->b1[0] - m->b0[0]) : 0;
+    if (x >= 1.0) m->cb = (m->nblk + m->n - 1) / m->n;   // shares padded to equal size (the last one short)
+    m->span = std::max(m->n * m->cb, m->nblk);
     bool distinct = true;
     for (int i = 0; i < m->n; ++i)
         for (int j = 0; j < i; ++j) distinct &= m->devs[i] != m->devs[j];
@@ -121,16 +159,21 @@ int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_tab
         delete m;
         return set_error(SPE_EUNSUPPORTED, "librccl.so.1 could not be loaded");
     }
-    m->graphs.assign(m->n, nullptr);
-    m->parts.assign(m->n, nullptr);
-    m->replica.assign(m->n, nullptr);
-    m->next.assign(m->n, nullptr);
-    m->hops.assign(m->n, nullptr);
-    m->streams.assign(m->n, nullptr);
+    const int32_t nd = m->n;
+    m->graphs.assign(nd, nullptr);
+    m->parts.assign(nd, nullptr);
+    m->lparts.assign(nd, nullptr);
+    m->replica.assign(nd, nullptr);
+    m->next.assign(nd, nullptr);
+    m->hops.assign(nd, nullptr);
+    m->lnext.assign(nd, nullptr);
+    m->lhops.assign(nd, nullptr);
+    m->streams.assign(nd, nullptr);
     int r = SPE_OK;
-    const size_t rep_bytes = (size_t)m->n * m->cb * m->blk_elems() * 2 * sizeof(double);
+    const size_t rep_bytes = (size_t)m->span * m->blk_bytes();
     const size_t own = (size_t)m->cb * m->blk_elems();
-    for (int d = 0; d < m->n && !r; ++d) {
+    const size_t loc = (size_t)(m->nblk - std::min(m->nblk, m->S)) * m->blk_elems();
+    for (int d = 0; d < nd && !r; ++d) {
         if (m->devs[d] == gi.device) {
             m->graphs[d] = g;
         } else if ((r = graph_clone(g, m->devs[d], &m->graphs[d]))) {
@@ -141,31 +184,43 @@ int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_tab
         if (e == hipSuccess) e = hipMalloc(&m->replica[d], rep_bytes);
         if (e == hipSuccess) e = hipMalloc(&m->next[d], std::max<size_t>(1, own) * sizeof(int32_t));
         if (e == hipSuccess) e = hipMalloc(&m->hops[d], std::max<size_t>(1, own) * sizeof(uint16_t));
+        if (e == hipSuccess && loc) e = hipMalloc(&m->lnext[d], loc * sizeof(int32_t));
+        if (e == hipSuccess && loc) e = hipMalloc(&m->lhops[d], loc * sizeof(uint16_t));
         if (e != hipSuccess) {
             r = hip_fail("multi-device table storage", e);
             break;
         }
-        if (m->b1[d] <= m->b0[d]) continue;   // an empty share (more devices than blocks)
         spe_table_opts po = o;
         po.devices = nullptr;
         po.n_devices = 0;
-        po.block_begin = m->b0[d];
-        po.block_end = m->b1[d];
-        po.ext_latrel = (char*)m->replica[d] + (size_t)m->b0[d] * m->blk_elems() * 2 * sizeof(double);
-        po.ext_next_hop = m->next[d];
-        po.ext_hops = m->hops[d];
         po.ext_filled = 0;
-        r = spe_table_create(m->graphs[d], attached, A, &po, &m->parts[d]);
-        if (!r) {
-            spe_table_layout pl{};
-            spe_table_layout_get(m->parts[d], &pl);
-            FwPart fp;
-            m->fw = pl.engine == SPE_ENGINE_FW && fw_part(m->parts[d], &fp) == SPE_OK;   // not for DIRECT tables
+        if (m->b1[d] > m->b0[d]) {
+            po.block_begin = m->b0[d];
+            po.block_end = m->b1[d];
+            po.ext_latrel = (char*)m->replica[d] + (size_t)m->b0[d] * m->blk_bytes();
+            po.ext_next_hop = m->next[d];
+            po.ext_hops = m->hops[d];
+            r = spe_table_create(m->graphs[d], attached, A, &po, &m->parts[d]);
+            if (!r) {
+                spe_table_layout pl{};
+                spe_table_layout_get(m->parts[d], &pl);
+                FwPart fp;
+                m->fw = pl.engine == SPE_ENGINE_FW && fw_part(m->parts[d], &fp) == SPE_OK;   // not for DIRECT tables
+                m->chunk = std::max(1, pl.groups_per_launch);
+            }
+        }
+        if (!r && loc) {   // the local remainder, built in place on this device
+            po.block_begin = m->S;
+            po.block_end = m->nblk;
+            po.ext_latrel = (char*)m->replica[d] + (size_t)m->S * m->blk_bytes();
+            po.ext_next_hop = m->lnext[d];
+            po.ext_hops = m->lhops[d];
+            r = spe_table_create(m->graphs[d], attached, A, &po, &m->lparts[d]);
         }
     }
     if (!r && m->gather == SPE_GATHER_RCCL) {
-        m->comms.assign(m->n, nullptr);
-        const ncclResult_t nr = rccl_lib().comm_init_all(m->comms.data(), m->n, m->devs.data());
+        m->comms.assign(nd, nullptr);
+        const ncclResult_t nr = rccl_lib().comm_init_all(m->comms.data(), nd, m->devs.data());
         if (nr != ncclSuccess) {
             m->comms.clear();
             r = set_error(SPE_EHIP, std::string("ncclCommInitAll: ") + rccl_lib().error_string(nr));
@@ -185,50 +240,60 @@ void multi_free(MultiDev* m) {
         if (c) rccl_lib().comm_destroy(c);
     for (int d = 0; d < m->n; ++d) {
         if (m->parts[d]) spe_table_free(m->parts[d]);
+        if (m->lparts[d]) spe_table_free(m->lparts[d]);
         (void)hipSetDevice(m->devs[d]);
         if (m->streams[d]) (void)hipStreamSynchronize(m->streams[d]);
-        if (m->replica[d]) (void)hipFree(m->replica[d]);
-        if (m->next[d]) (void)hipFree(m->next[d]);
-        if (m->hops[d]) (void)hipFree(m->hops[d]);
+        for (void* p : {m->replica[d], m->next[d], m->hops[d], m->lnext[d], m->lhops[d]})
+            if (p) (void)hipFree(p);
         if (m->streams[d]) (void)hipStreamDestroy(m->streams[d]);
         if (m->graphs[d] && m->graphs[d] != m->home) spe_graph_free(m->graphs[d]);
     }
     delete m;
 }
 
-static int gather_records(MultiDev* m) {
-    const size_t share_bytes = (size_t)m->cb * m->blk_elems() * 2 * sizeof(double);
+// Round k of the gather: every share's chunk k -- blocks [b0 + k c, b0 + (k + 1) c)
+// clipped to the share -- to every other device.  RCCL: one group of ncclBroadcast,
+// one per root, in place on every replica (the chunks of a round are not
+// contiguous, so an all-gather does not fit); PEER: each device pulls the other
+// chunks on its gather stream.  The chunks were built synchronously before.
+static int gather_round(MultiDev* m, int32_t k) {
     if (m->gather == SPE_GATHER_RCCL) {
         Rccl& R = rccl_lib();
         R.group_start();
         ncclResult_t nr = ncclSuccess;
-        for (int d = 0; d < m->n && nr == ncclSuccess; ++d) {
-            if (hipSetDevice(m->devs[d]) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
-            const void* send = (const char*)m->replica[d] + (size_t)d * share_bytes;
-            nr = R.all_gather(send, m->replica[d], (size_t)m->cb * m->blk_elems() * 2, ncclDouble, m->comms[d],
-                              m->streams[d]);
+        for (int root = 0; root < m->n && nr == ncclSuccess; ++root) {
+            const int32_t c0 = std::min(m->b1[root], m->b0[root] + k * m->chunk);
+            const int32_t c1 = std::min(m->b1[root], c0 + m->chunk);
+            if (c1 <= c0) continue;
+            const size_t off = (size_t)c0 * m->blk_bytes();
+            const size_t cnt = (size_t)(c1 - c0) * m->blk_elems() * 2;
+            for (int d = 0; d < m->n && nr == ncclSuccess; ++d) {
+                if (hipSetDevice(m->devs[d]) != hipSuccess) {
+                    R.group_end();
+                    return set_error(SPE_EHIP, "hipSetDevice");
+                }
+                char* buf = (char*)m->replica[d] + off;
+                nr = R.broadcast(buf, buf, cnt, ncclDouble, root, m->comms[d], m->streams[d]);
+            }
         }
         const ncclResult_t ne = R.group_end();
         if (nr != ncclSuccess || ne != ncclSuccess)
-            return set_error(SPE_EHIP, std::string("ncclAllGather: ") + R.error_string(nr != ncclSuccess ? nr : ne));
-    } else {
-        for (int e = 0; e < m->n; ++e) {   // device e pulls every other share
-            if (hipSetDevice(m->devs[e]) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
-            for (int d = 0; d < m->n; ++d) {
-                if (d == e || m->b1[d] <= m->b0[d]) continue;
-                const size_t off = (size_t)m->b0[d] * m->blk_elems() * 2 * sizeof(double);
-                const size_t bytes = (size_t)(m->b1[d] - m->b0[d]) * m->blk_elems() * 2 * sizeof(double);
-                const hipError_t he = hipMemcpyPeerAsync((char*)m->replica[e] + off, m->devs[e],
-                                                         (const char*)m->replica[d] + off, m->devs[d], bytes,
-                                                         m->streams[e]);
-                if (he != hipSuccess) return hip_fail("hipMemcpyPeerAsync", he);
-            }
-        }
+            return set_error(SPE_EHIP, std::string("ncclBroadcast: ") + R.error_string(nr != ncclSuccess ? nr : ne));
+        return SPE_OK;
     }
-    for (int d = 0; d < m->n; ++d) {
-        if (hipSetDevice(m->devs[d]) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
-        const hipError_t he = hipStreamSynchronize(m->streams[d]);
-        if (he != hipSuccess) return hip_fail("gather sync", he);
+    for (int e = 0; e < m->n; ++e) {   // device e pulls every other share's chunk
+        if (hipSetDevice(m->devs[e]) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
+        for (int d = 0; d < m->n; ++d) {
+            if (d == e) continue;
+            const int32_t c0 = std::min(m->b1[d], m->b0[d] + k * m->chunk);
+            const int32_t c1 = std::min(m->b1[d], c0 + m->chunk);
+            if (c1 <= c0) continue;
+            const size_t off = (size_t)c0 * m->blk_bytes();
+            const hipError_t he = hipMemcpyPeerAsync((char*)m->replica[e] + off, m->devs[e],
+                                                     (const char*)m->replica[d] + off, m->devs[d],
+                                                     (size_t)(c1 - c0) * m->blk_bytes(), m->streams[e]);
+            if (he != hipSuccess) return hip_fail("hipMemcpyPeerAsync", he);
+        }
     }
     return SPE_OK;
 }
@@ -246,7 +311,8 @@ namespace {
 struct FwBcast {
     const MultiDev* m;
     std::vector<FwPart>& P;
-    std::vector<hipEvent_t>& ev;
+    std::vector<hipEvent_t>& ev;      // per device: its copies issued / its rows ready to read
+    std::vector<hipEvent_t>& ready;   // per device: every kernel it queued so far (destination side)
     bool rccl;
     // rows [r0, r1) of the arrays in `which` (bit 0 D, 1 R, 2 N) from device `root` to every other
     int rows(int root, int64_t r0, int64_t r1, int which) {
@@ -272,10 +338,24 @@ struct FwBcast {
             return SPE_OK;
         }
         // peer copies on the root's stream (its later kernels overwrite these rows),
-        // then every other device's stream waits for them
+        // ordered after everything each destination queued before (a destination's
+        // earlier kernels -- its init, or the column panel / rest of the previous
+        // pivot -- still read or write the rows the copy lands in), then every
+        // other device's stream waits for the copies
         const FwPart& o = P[root];
+        for (int d = 0; d < m->n; ++d) {
+            if (d == root) continue;
+            if (hipSetDevice(P[d].device) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
+            const hipError_t e = hipEventRecord(ready[d], (hipStream_t)P[d].stream);
+            if (e != hipSuccess) return hip_fail("hipEventRecord (FW destination)", e);
+        }
         if (hipSetDevice(o.device) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
         hipStream_t so = (hipStream_t)o.stream;
+        for (int d = 0; d < m->n; ++d) {
+            if (d == root) continue;
+            const hipError_t e = hipStreamWaitEvent(so, ready[d], 0);
+            if (e != hipSuccess) return hip_fail("hipStreamWaitEvent (FW destination)", e);
+        }
         for (int d = 0; d < m->n; ++d) {
             if (d == root) continue;
             hipError_t e = hipSuccess;
@@ -312,14 +392,15 @@ static int fw_closure_multi(MultiDev* m, double* seconds) {
     const auto t0 = std::chrono::steady_clock::now();
     const int32_t nb = (int32_t)(P[0].ld / 64);
     const int32_t rbs = (nb + m->n - 1) / m->n;   // closure row blocks per device
-    std::vector<hipEvent_t> ev(m->n, nullptr);
+    std::vector<hipEvent_t> ev(m->n, nullptr), ready(m->n, nullptr);
     int r = SPE_OK;
     for (int d = 0; d < m->n && !r; ++d) {
-        if (hipSetDevice(P[d].device) != hipSuccess || hipEventCreateWithFlags(&ev[d], hipEventDisableTiming) != hipSuccess)
+        if (hipSetDevice(P[d].device) != hipSuccess || hipEventCreateWithFlags(&ev[d], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ready[d], hipEventDisableTiming) != hipSuccess)
             r = set_error(SPE_EHIP, "FW closure events");
         if (!r) r = fw_init(m->graphs[d], P[d]);
     }
-    FwBcast bc{m, P, ev, m->gather == SPE_GATHER_RCCL};
+    FwBcast bc{m, P, ev, ready, m->gather == SPE_GATHER_RCCL};
     for (int32_t kb = 0; kb < nb && !r; ++kb) {
         const int own = kb / rbs;
         r = fw_pivot_owner(P[own], kb);
@@ -335,6 +416,7 @@ static int fw_closure_multi(MultiDev* m, double* seconds) {
             if (!r && e != hipSuccess) r = hip_fail("FW closure sync", e);
         }
         if (ev[d]) (void)hipEventDestroy(ev[d]);
+        if (ready[d]) (void)hipEventDestroy(ready[d]);
     }
     if (r) return r;
     for (auto& p : P) *p.done = true;
@@ -348,35 +430,71 @@ int multi_build(MultiDev* m, spe_build_stats* stats) {
     if (m->fw) {
         if (int r = fw_closure_multi(m, &fw_s)) return r;
     }
+    // Every device builds its share chunk by chunk; the device finishing chunk k
+    // last issues gather round k (the other devices are already building chunk
+    // k + 1: the gather runs on the gather streams under the builds), then each
+    // device builds the local remainder while the last rounds are in flight.
+    const int32_t rounds = m->cb > 0 ? (m->cb + m->chunk - 1) / m->chunk : 0;
     std::vector<int> rc(m->n, SPE_OK);
     std::vector<std::string> err(m->n);
+    std::vector<double> busy(m->n, 0.0);
+    std::vector<int32_t> arrived(std::max(1, rounds), 0);
+    std::mutex mu;
+    int gather_rc = SPE_OK;
+    std::string gather_err;
     std::vector<std::thread> th;
     for (int d = 0; d < m->n; ++d) {
-        if (!m->parts[d]) continue;
-        th.emplace_back([m, d, &rc, &err]() {
-            rc[d] = spe_table_build(m->parts[d], nullptr);
-            if (rc[d]) err[d] = spe_last_error();
+        th.emplace_back([&, d]() {
+            const auto s0 = std::chrono::steady_clock::now();
+            for (int32_t k = 0; k < rounds; ++k) {
+                const int32_t c0 = std::min(m->b1[d], m->b0[d] + k * m->chunk);
+                const int32_t c1 = std::min(m->b1[d], c0 + m->chunk);
+                if (c1 > c0 && rc[d] == SPE_OK) {
+                    rc[d] = spe_table_build_blocks(m->parts[d], c0, c1, nullptr);
+                    if (rc[d]) err[d] = spe_last_error();
+                }
+                std::lock_guard<std::mutex> lk(mu);
+                if (++arrived[k] == m->n && gather_rc == SPE_OK) {
+                    bool ok = true;
+                    for (int e = 0; e < m->n; ++e) ok &= rc[e] == SPE_OK;
+                    if (ok && (gather_rc = gather_round(m, k))) gather_err = spe_last_error();
+                }
+            }
+            if (m->lparts[d] && rc[d] == SPE_OK) {
+                rc[d] = spe_table_build(m->lparts[d], nullptr);
+                if (rc[d]) err[d] = spe_last_error();
+            }
+            busy[d] = std::chrono::duration<double>(std::chrono::steady_clock::now() - s0).count();
         });
     }
     for (auto& x : th) x.join();
     for (int d = 0; d < m->n; ++d)
         if (rc[d]) return set_error(rc[d], "device " + std::to_string(m->devs[d]) + ": " + err[d]);
+    if (gather_rc) return set_error(gather_rc, gather_err);
     const auto t1 = std::chrono::steady_clock::now();
-    if (int r = gather_records(m)) return r;
+    for (int d = 0; d < m->n; ++d) {
+        if (hipSetDevice(m->devs[d]) != hipSuccess) return set_error(SPE_EHIP, "hipSetDevice");
+        const hipError_t he = hipStreamSynchronize(m->streams[d]);
+        if (he != hipSuccess) return hip_fail("gather sync", he);
+    }
     const auto t2 = std::chrono::steady_clock::now();
     spe_build_stats s{};
-    for (int d = 0; d < m->n; ++d) {
-        if (!m->parts[d]) continue;
-        spe_build_stats p{};
-        spe_table_build_stats(m->parts[d], &p);
-        s.iterations += p.iterations;
-        s.active_rounds += p.active_rounds;
-        s.launches += p.launches;
-    }
+    for (int d = 0; d < m->n; ++d)
+        for (spe_table* p : {m->parts[d], m->lparts[d]}) {
+            if (!p) continue;
+            spe_build_stats q{};
+            spe_table_build_stats(p, &q);
+            s.iterations += q.iterations;
+            s.active_rounds += q.active_rounds;
+            s.launches += q.launches;
+        }
     s.seconds = std::chrono::duration<double>(t2 - t0).count();
-    s.gather_seconds = std::chrono::duration<double>(t2 - t1).count();
+    s.gather_seconds = std::chrono::duration<double>(t2 - t1).count();   // gather time not hidden by the builds
+    s.build_wait_seconds = *std::max_element(busy.begin(), busy.end());
     s.n_devices = m->n;
     s.gather = m->gather;
+    s.shared_blocks = std::min(m->S, m->nblk);
+    s.local_blocks = m->nblk - std::min(m->S, m->nblk);
     m->stats = s;
     if (stats) *stats = s;
     m->built = true;
@@ -385,31 +503,39 @@ int multi_build(MultiDev* m, spe_build_stats* stats) {
 
 bool multi_built(const MultiDev* m) { return m->built; }
 
-static int owner_of(const MultiDev* m, int32_t s_slot) {
-    const int32_t b = s_slot / kWave;
-    for (int d = 0; d < m->n; ++d)
-        if (b >= m->b0[d] && b < m->b1[d]) return d;
-    return -1;
+// The part table holding row block b's next hops / hop counts, and the last
+// block of that table's run: a share's part, or the home device's local part.
+static spe_table* part_of(const MultiDev* m, int32_t b, int32_t* run_end) {
+    if (b >= m->S) {
+        *run_end = m->nblk;
+        return m->lparts[0];
+    }
+    const int d = b / m->cb;
+    *run_end = m->b1[d];
+    return m->parts[d];
 }
 
 int multi_get(const MultiDev* m, int32_t s_slot, int32_t t_slot, spe_entry* out) {
     if (s_slot < 0 || s_slot >= m->A || t_slot < 0 || t_slot >= m->A) return set_error(SPE_EINVAL, "slot out of range");
-    return spe_table_get(m->parts[owner_of(m, s_slot)], s_slot, t_slot, out);
+    int32_t e = 0;
+    return spe_table_get(part_of(m, s_slot / kWave, &e), s_slot, t_slot, out);
 }
 
 int multi_source_tree(MultiDev* m, int32_t s_slot, int32_t* parent) {
     if (s_slot < 0 || s_slot >= m->A) return set_error(SPE_EINVAL, "slot out of range");
-    return spe_table_source_tree(m->parts[owner_of(m, s_slot)], s_slot, parent);
+    int32_t e = 0;
+    return spe_table_source_tree(part_of(m, s_slot / kWave, &e), s_slot, parent);
 }
 
 int multi_download(const MultiDev* m, int32_t row_begin, int32_t row_end, double* latency, double* reliability,
                    int32_t* next_hop, int32_t* hops) {
     if (row_begin < 0 || row_end > m->A || row_begin > row_end) return set_error(SPE_EINVAL, "row range out of bounds");
     for (int32_t r0 = row_begin; r0 < row_end;) {
-        const int d = owner_of(m, r0);
-        const int32_t r1 = std::min(row_end, m->b1[d] * kWave);
+        int32_t be = 0;
+        spe_table* p = part_of(m, r0 / kWave, &be);
+        const int32_t r1 = std::min(row_end, be * kWave);
         const size_t off = (size_t)(r0 - row_begin) * m->A;
-        int rc = spe_table_download(m->parts[d], r0, r1, latency ? latency + off : nullptr,
+        int rc = spe_table_download(p, r0, r1, latency ? latency + off : nullptr,
                                     reliability ? reliability + off : nullptr, next_hop ? next_hop + off : nullptr,
                                     hops ? hops + off : nullptr);
         if (rc) return rc;
@@ -418,18 +544,27 @@ int multi_download(const MultiDev* m, int32_t row_begin, int32_t row_end, double
     return SPE_OK;
 }
 
-int multi_lookup(const MultiDev* m, const int32_t* d_pairs, int64_t q, double* d_latency, double* d_reliability,
-                 uint8_t* d_ok, void* stream) {
-    return lookup_on_replica(m->devs[0], m->replica[0], m->A, m->nblk, d_pairs, q, d_latency, d_reliability, d_ok,
-                             stream);
+int multi_lookup(const MultiDev* m, int32_t replica, const int32_t* d_pairs, int64_t q, double* d_latency,
+                 double* d_reliability, uint8_t* d_ok, void* stream) {
+    if (replica < 0 || replica >= m->n) return set_error(SPE_EINVAL, "replica out of range");
+    return lookup_on_replica(m->devs[replica], m->replica[replica], m->A, m->nblk, d_pairs, q, d_latency, d_reliability,
+                             d_ok, stream);
+}
+
+int multi_replica_device(const MultiDev* m, int32_t replica, int32_t* device) {
+    if (replica < 0 || replica >= m->n) return set_error(SPE_EINVAL, "replica out of range");
+    *device = m->devs[replica];
+    return SPE_OK;
 }
 
 int multi_min_latency(const MultiDev* m, double* out) {
     double best = 0.0;
-    for (int d = 0; d < m->n; ++d) {
-        if (!m->parts[d]) continue;
+    std::vector<spe_table*> ts(m->parts);
+    ts.push_back(m->lparts[0]);
+    for (spe_table* p : ts) {
+        if (!p) continue;
         double v = 0.0;
-        if (int r = spe_table_min_latency(m->parts[d], &v)) return r;
+        if (int r = spe_table_min_latency(p, &v)) return r;
         if (v > 0 && (best == 0.0 || v < best)) best = v;   // 0 = the reference's "unset"
     }
     *out = best;
@@ -438,48 +573,77 @@ int multi_min_latency(const MultiDev* m, double* out) {
 
 int multi_layout(const MultiDev* m, spe_table_layout* out) {
     spe_table_layout p{};
-    for (int d = 0; d < m->n; ++d)
-        if (m->parts[d]) {
-            spe_table_layout_get(m->parts[d], &p);
+    for (spe_table* x : {m->parts[0], m->lparts[0]})
+        if (x) {
+            spe_table_layout_get(x, &p);
             break;
         }
     out->n_attached = m->A;
     out->block_begin = 0;
     out->block_end = m->nblk;
-    out->elems = (int64_t)m->n * m->cb * m->A * kWave;
+    out->elems = (int64_t)m->span * m->A * kWave;
     out->latrel = m->replica[0];
     out->next_hop = nullptr;
     out->hops = nullptr;
     out->groups_per_launch = p.groups_per_launch;
     out->engine = p.engine;
     out->lanes_per_group = p.lanes_per_group;
+    out->relax_kernel = p.relax_kernel;
     out->n_devices = m->n;
     out->device = m->devs[0];
     return SPE_OK;
 }
 
 int multi_profile_enable(MultiDev* m, int32_t enable) {
-    for (spe_table* p : m->parts)
-        if (p)
-            if (int r = spe_table_profile_enable(p, enable)) return r;
+    for (int d = 0; d < m->n; ++d)
+        for (spe_table* p : {m->parts[d], m->lparts[d]})
+            if (p)
+                if (int r = spe_table_profile_enable(p, enable)) return r;
     return SPE_OK;
 }
 
 int multi_profile_get(const MultiDev* m, spe_kernel_profile* out) {
     *out = spe_kernel_profile{};
-    for (spe_table* p : m->parts) {
-        if (!p) continue;
-        spe_kernel_profile k{};
-        spe_table_profile_get(p, &k);
+    for (int d = 0; d < m->n; ++d) {
+        spe_kernel_profile dev{};   // one device: its parts run one after the other
+        for (spe_table* p : {m->parts[d], m->lparts[d]}) {
+            if (!p) continue;
+            spe_kernel_profile k{};
+            spe_table_profile_get(p, &k);
+            for (int i = 0; i < SPE_K_COUNT; ++i) {
+                dev.ms[i] += k.ms[i];
+                dev.launches[i] += k.launches[i];
+            }
+        }
         for (int i = 0; i < SPE_K_COUNT; ++i) {
-            out->ms[i] = std::max(out->ms[i], k.ms[i]);   // the parts run concurrently: the slowest
-            out->launches[i] += k.launches[i];
+            out->ms[i] = std::max(out->ms[i], dev.ms[i]);   // the devices run concurrently: the slowest
+            out->launches[i] += dev.launches[i];
         }
     }
     return SPE_OK;
 }
 
 }  // namespace spe
+
+extern "C" int spe_device_split(int32_t n_attached, int32_t n_devices, double shared_fraction, int32_t* block_begin,
+                                int32_t* block_end, int32_t* local_begin) {
+    if (n_attached < 0 || n_devices < 1 || !block_begin || !block_end || !local_begin || shared_fraction < 0.0 ||
+        shared_fraction > 1.0)
+        return spe::set_error(SPE_EINVAL, "spe_device_split: bad arguments");
+    const int32_t nblk = (n_attached + 63) / 64;
+    if (shared_fraction >= 1.0) {
+        *local_begin = nblk;
+        return spe_device_shares(n_attached, n_devices, block_begin, block_end);
+    }
+    const int32_t cb = (int32_t)std::floor(shared_fraction * nblk / n_devices);
+    const int32_t S = n_devices * cb;   // <= nblk: every share full, the remainder local
+    for (int32_t d = 0; d < n_devices; ++d) {
+        block_begin[d] = d * cb;
+        block_end[d] = (d + 1) * cb;
+    }
+    *local_begin = S;
+    return SPE_OK;
+}
 
 extern "C" int spe_device_shares(int32_t n_attached, int32_t n_devices, int32_t* block_begin, int32_t* block_end) {
     if (n_attached < 0 || n_devices < 1 || !block_begin || !block_end)

@@ -169,3 +169,61 @@ def allgather_round(lr, k: int, world: int, rank: int, chunk_elems: int, dist, a
             dst.copy_(p)
         return None
     return dist.all_gather_into_tensor(grp, own, async_op=async_op)
+
+
+# ---- compute-versus-gather split.  Gathering a share costs xGMI time,
+# recomputing it costs build time: with T1 the one-GPU whole-table build time and
+# S / B the time to receive the whole record span, sharding a fraction x of the
+# blocks (built once, all-gathered) and building the rest [S, nblk) on every rank
+# (no exchange) takes about max(T1 (x / N + 1 - x), x (N - 1) / N S / B) when the
+# gathers overlap the local builds.  The two terms meet at
+#   x* = T1 N / ((N - 1) (S / B + T1)),
+# clipped to [0, 1] (x = 1: pure sharding, the C3 regime; C4 at N = 8 with
+# S = 160 GB: x* ~ 0.4).
+
+def shared_fraction(world: int, t1_s: float, span_bytes: float, gather_bps: float) -> float:
+    """x*: the fraction of the source blocks to shard and all-gather (the rest is
+    built by every rank), from the one-GPU build time and the gather bandwidth."""
+    if world <= 1:
+        return 1.0
+    if gather_bps <= 0 or t1_s <= 0:
+        return 1.0
+    x = t1_s * world / ((world - 1) * (span_bytes / gather_bps + t1_s))
+    return float(min(1.0, max(0.0, x)))
+
+
+def split_schedule(nblk: int, world: int, groups: int, shared_frac: float, lead: int = 4):
+    """(sizes, S): chunk_schedule rounds over the first S blocks (every round holds
+    world equal parts, so S = world * sum(sizes) and no gathered part reaches past
+    S), and the local remainder [S, nblk) that every rank builds itself.
+    shared_frac >= 1 (or a world of 1): every block sharded, S may exceed nblk
+    (padding blocks, never read)."""
+    if world <= 1 or shared_frac >= 1.0:
+        sizes = chunk_schedule(nblk, world, groups, lead)
+        return sizes, world * sum(sizes)
+    want = int(math.floor(max(0.0, shared_frac) * nblk / world))   # blocks per rank
+    if want <= 0:
+        return [], 0
+    sizes = chunk_schedule(want * world, world, groups, lead)
+    return sizes, world * sum(sizes)
+
+
+def local_span(nblk: int, S: int) -> Tuple[int, int]:
+    """The blocks every rank builds itself under split_schedule."""
+    return min(nblk, S), nblk
+
+
+def rank_next_hop_slots(nblk: int, world: int, rank: int, sizes, S: int):
+    """Where a rank keeps next hop / hop count: its own sharded chunks, then the
+    local remainder, packed contiguously -> [(b0, b1, slot0)] with slot0 the first
+    packed block of [b0, b1), and the packed block count."""
+    out, slot = [], 0
+    for _, _, _, b0, b1 in rank_chunks_sched(nblk, world, rank, sizes):
+        if b1 > b0:
+            out.append((b0, b1, slot))
+            slot += b1 - b0
+    l0, l1 = local_span(nblk, S)
+    if l1 > l0:
+        out.append((l0, l1, slot))
+        slot += l1 - l0
+    return out, slot

@@ -1029,7 +1029,15 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, Snap** ou
         o.devices = devs;
         o.n_devices = ndev;
     }
+    /* SHADOW_SPE_ENGINE=1|2|3: ask for the batch / LDS / FW engine (SPE_ENGINE_*); an
+     * engine the graph does not fit falls back to the library's choice */
+    const char* eng = getenv("SHADOW_SPE_ENGINE");
+    if (eng && *eng) o.engine = (int32_t)strtol(eng, NULL, 10);
     int rc = spe_table_create(top->graph, s->attached, A, &o, &s->table);
+    if (rc == SPE_EUNSUPPORTED && o.engine != SPE_ENGINE_AUTO) {
+        o.engine = SPE_ENGINE_AUTO;
+        rc = spe_table_create(top->graph, s->attached, A, &o, &s->table);
+    }
     /* SHADOW_SPE_TABLE_CACHE=<dir>: reuse the rows of an earlier run on the same
      * graph / hosts (keyed file), else build and save them */
     const char* cdir = getenv("SHADOW_SPE_TABLE_CACHE");

@@ -23,7 +23,21 @@ SPE_SELF_ROW = 0
 SPE_SELF_RULE = 1
 SPE_ENGINE_AUTO, SPE_ENGINE_BATCH, SPE_ENGINE_LDS, SPE_ENGINE_FW = 0, 1, 2, 3
 SPE_GATHER_AUTO, SPE_GATHER_RCCL, SPE_GATHER_PEER = 0, 1, 2
+SPE_RELAX_AUTO, SPE_RELAX_REGISTER, SPE_RELAX_LDS_RING = 0, 1, 2
+SPE_EUNSUPPORTED = -4
 WAVE = 64
+
+# Test / experiment hooks of this mirror (libspe itself reads no environment):
+#   SPE_ENGINE=1|2|3   engine for tables that leave it AUTO (falls back to batch when
+#                      the graph does not fit the asked engine)
+#   SPE_LANES=64|128, SPE_RELAX=1|2, SPE_INFL=<rows per trip>, SPE_OCC=<waves/SIMD>,
+#   SPE_DELTA=<ms>, SPE_NO_OVERLAP=1, SPE_TRACE=1   batch-engine tuning (spe_table_opts)
+#   SPE_NO_PRUNE=1     graphs keep their pendant vertices (spe_graph_desc.keep_pendants)
+
+
+def _env_int(name: str, default: int = 0) -> int:
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
 
 
 class SpeError(RuntimeError):
@@ -34,7 +48,8 @@ class GraphDesc(C.Structure):
     _fields_ = [("n_vertices", C.c_int32), ("n_edges", C.c_int64),
                 ("edge_source", C.c_void_p), ("edge_target", C.c_void_p),
                 ("edge_latency", C.c_void_p), ("edge_packetloss", C.c_void_p),
-                ("vertex_packetloss", C.c_void_p), ("directed", C.c_int32), ("prefer_direct", C.c_int32)]
+                ("vertex_packetloss", C.c_void_p), ("directed", C.c_int32), ("prefer_direct", C.c_int32),
+                ("keep_pendants", C.c_int32)]
 
 
 class GraphInfo(C.Structure):
@@ -51,7 +66,10 @@ class TableOpts(C.Structure):
                 ("ext_next_hop", C.c_void_p), ("ext_hops", C.c_void_p), ("ext_filled", C.c_int32),
                 ("owner_rank", C.c_void_p), ("engine", C.c_int32), ("lanes_per_group", C.c_int32),
                 ("want_aux", C.c_int32), ("devices", C.c_void_p), ("n_devices", C.c_int32),
-                ("gather", C.c_int32)]
+                ("gather", C.c_int32), ("relax_kernel", C.c_int32), ("rows_in_flight", C.c_int32),
+                ("waves_per_simd", C.c_int32), ("no_overlap", C.c_int32), ("delta_ms", C.c_double),
+                ("trace", C.c_int32), ("shared_fraction", C.c_double), ("gather_gbps", C.c_double),
+                ("build_seconds_hint", C.c_double)]
 
 
 class TableLayout(C.Structure):
@@ -59,7 +77,7 @@ class TableLayout(C.Structure):
                 ("elems", C.c_int64), ("latrel", C.c_void_p),
                 ("next_hop", C.c_void_p), ("hops", C.c_void_p), ("groups_per_launch", C.c_int32),
                 ("engine", C.c_int32), ("n_devices", C.c_int32), ("device", C.c_int32),
-                ("lanes_per_group", C.c_int32)]
+                ("lanes_per_group", C.c_int32), ("relax_kernel", C.c_int32)]
 
 
 class Entry(C.Structure):
@@ -77,18 +95,21 @@ class KernelProfile(C.Structure):
 class BuildStats(C.Structure):
     _fields_ = [("iterations", C.c_int64), ("active_rounds", C.c_int64), ("launches", C.c_int64),
                 ("seconds", C.c_double), ("gather_seconds", C.c_double), ("n_devices", C.c_int32),
-                ("gather", C.c_int32)]
+                ("gather", C.c_int32), ("shared_blocks", C.c_int32), ("local_blocks", C.c_int32),
+                ("build_wait_seconds", C.c_double)]
 
 
 # every symbol include/spe.h declares (tests/test_abi.py checks the export table)
 EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_info_get", "spe_graph_free",
            "spe_order_sources",
-           "spe_table_create", "spe_table_build", "spe_table_build_blocks", "spe_table_profile_enable",
+           "spe_table_create", "spe_table_build", "spe_table_build_blocks", "spe_table_build_blocks_into",
+           "spe_table_profile_enable",
            "spe_table_profile_get", "spe_table_build_stats", "spe_table_layout_get",
            "spe_table_get", "spe_table_download", "spe_lookup_batch", "spe_table_min_latency",
            "spe_table_key", "spe_table_save", "spe_table_load", "spe_table_free",
            "spe_graph_set_edge_aux", "spe_table_download_aux", "spe_fw_apsp", "spe_fw_closure", "spe_graph_self_path",
-           "spe_graph_adjacent", "spe_device_shares", "spe_graph_edge", "spe_table_source_tree"]
+           "spe_graph_adjacent", "spe_device_shares", "spe_graph_edge", "spe_table_source_tree",
+           "spe_device_split", "spe_lookup_batch_replica", "spe_table_replica_device"]
 
 _lib = None
 
@@ -118,6 +139,7 @@ def lib():
         L.spe_table_create.argtypes = [P, P, C.c_int32, P, P]
         L.spe_table_build.argtypes = [P, P]
         L.spe_table_build_blocks.argtypes = [P, C.c_int32, C.c_int32, P]
+        L.spe_table_build_blocks_into.argtypes = [P, C.c_int32, C.c_int32, P, P, P, P]
         L.spe_table_profile_enable.argtypes = [P, C.c_int32]
         L.spe_table_profile_get.argtypes = [P, P]
         L.spe_table_build_stats.argtypes = [P, P]
@@ -125,6 +147,9 @@ def lib():
         L.spe_table_get.argtypes = [P, C.c_int32, C.c_int32, P]
         L.spe_table_download.argtypes = [P, C.c_int32, C.c_int32, P, P, P, P]
         L.spe_lookup_batch.argtypes = [P, P, C.c_int64, P, P, P, P]
+        L.spe_lookup_batch_replica.argtypes = [P, C.c_int32, P, C.c_int64, P, P, P, P]
+        L.spe_table_replica_device.argtypes = [P, C.c_int32, P]
+        L.spe_device_split.argtypes = [C.c_int32, C.c_int32, C.c_double, P, P, P]
         L.spe_table_min_latency.argtypes = [P, P]
         L.spe_table_key.argtypes = [P, P]
         L.spe_table_save.argtypes = [P, C.c_char_p]
@@ -163,6 +188,17 @@ def device_shares(n_attached: int, n_devices: int):
     return list(zip(b0.tolist(), b1.tolist()))
 
 
+def device_split(n_attached: int, n_devices: int, shared_fraction: float):
+    """spe_device_split: ([(begin, end)] shares of the sharded blocks, first block of
+    the local remainder every device builds) (host-only)."""
+    b0 = np.empty(n_devices, np.int32)
+    b1 = np.empty(n_devices, np.int32)
+    lb = C.c_int32(0)
+    _check(lib().spe_device_split(int(n_attached), int(n_devices), float(shared_fraction), _p(b0), _p(b1),
+                                  C.byref(lb)), "spe_device_split")
+    return list(zip(b0.tolist(), b1.tolist())), int(lb.value)
+
+
 def device_count() -> int:
     c = C.c_int32(0)
     lib().spe_device_count(C.byref(c))
@@ -172,13 +208,15 @@ def device_count() -> int:
 class Graph:
     """spe_graph: the topology uploaded to one device (topology_new's role)."""
 
-    def __init__(self, top: Topology, device: int = 0):
+    def __init__(self, top: Topology, device: int = 0, keep_pendants: Optional[bool] = None):
         self.top = top
+        if keep_pendants is None:
+            keep_pendants = _env_int("SPE_NO_PRUNE") != 0
         keep = [np.ascontiguousarray(top.esrc, np.int32), np.ascontiguousarray(top.edst, np.int32),
                 np.ascontiguousarray(top.elat, np.float64), np.ascontiguousarray(top.eloss, np.float64),
                 np.ascontiguousarray(top.vloss, np.float64)]
         d = GraphDesc(int(top.n), int(keep[0].shape[0]), _p(keep[0]), _p(keep[1]), _p(keep[2]), _p(keep[3]),
-                      _p(keep[4]), int(bool(top.directed)), int(bool(top.prefer_direct)))
+                      _p(keep[4]), int(bool(top.directed)), int(bool(top.prefer_direct)), int(bool(keep_pendants)))
         h = C.c_void_p()
         _check(lib().spe_graph_create(C.byref(d), int(device), C.byref(h)), "spe_graph_create")
         self.h = h
@@ -242,7 +280,9 @@ class PathTable:
     def __init__(self, graph: Graph, attached, self_mode: int = SPE_SELF_ROW, force_sssp: bool = False,
                  groups: int = 0, blocks=None, ext=None, ext_filled: bool = False, lanes: int = 0,
                  owner_order=None, engine: int = 0, want_aux: bool = False, devices=None,
-                 gather: int = SPE_GATHER_AUTO):
+                 gather: int = SPE_GATHER_AUTO, relax_kernel: int = 0, rows_in_flight: int = 0,
+                 waves_per_simd: int = 0, no_overlap: Optional[bool] = None, delta_ms: Optional[float] = None,
+                 shared_fraction: float = 0.0, gather_gbps: float = 0.0, build_seconds_hint: float = 0.0):
         self.graph = graph
         self.attached = np.ascontiguousarray(attached, np.int32)
         self.A = int(self.attached.shape[0])
@@ -250,9 +290,18 @@ class PathTable:
         o.self_mode = int(self_mode)
         o.force_sssp = int(bool(force_sssp))
         o.groups_per_launch = int(groups)
-        o.lanes_per_group = int(lanes)
+        o.lanes_per_group = int(lanes) or _env_int("SPE_LANES")
         o.engine = int(engine)
         o.want_aux = int(bool(want_aux))
+        o.relax_kernel = int(relax_kernel) or _env_int("SPE_RELAX")
+        o.rows_in_flight = int(rows_in_flight) or _env_int("SPE_INFL")
+        o.waves_per_simd = int(waves_per_simd) or _env_int("SPE_OCC")
+        o.no_overlap = int(bool(no_overlap if no_overlap is not None else _env_int("SPE_NO_OVERLAP")))
+        o.delta_ms = float(delta_ms if delta_ms is not None else (os.environ.get("SPE_DELTA") or 0.0))
+        o.trace = _env_int("SPE_TRACE")
+        env_engine = engine == SPE_ENGINE_AUTO and not want_aux and _env_int("SPE_ENGINE") != 0
+        if env_engine:
+            o.engine = _env_int("SPE_ENGINE")
         if owner_order is not None:   # source-run order (slots) -> rank of each slot
             self._rank = np.empty(self.A, np.int32)
             self._rank[np.asarray(owner_order, np.int64)] = np.arange(self.A, dtype=np.int32)
@@ -264,12 +313,18 @@ class PathTable:
             o.devices = self._devs.ctypes.data
             o.n_devices = int(self._devs.shape[0])
             o.gather = int(gather)
+            o.shared_fraction = float(shared_fraction)
+            o.gather_gbps = float(gather_gbps)
+            o.build_seconds_hint = float(build_seconds_hint)
         if ext is not None:  # three device pointers (ints): latrel (2 x f64), next_hop (i32), hops (u16)
             o.ext_latrel, o.ext_next_hop, o.ext_hops = [int(x) for x in ext]
             o.ext_filled = int(bool(ext_filled))
         h = C.c_void_p()
-        _check(lib().spe_table_create(graph.h, _p(self.attached), self.A, C.byref(o), C.byref(h)),
-               "spe_table_create")
+        rc = lib().spe_table_create(graph.h, _p(self.attached), self.A, C.byref(o), C.byref(h))
+        if rc == SPE_EUNSUPPORTED and env_engine and o.engine != SPE_ENGINE_BATCH:
+            o.engine = SPE_ENGINE_BATCH   # SPE_ENGINE asked for an engine the graph does not fit
+            rc = lib().spe_table_create(graph.h, _p(self.attached), self.A, C.byref(o), C.byref(h))
+        _check(rc, "spe_table_create")
         self.h = h
 
     @property
@@ -283,6 +338,15 @@ class PathTable:
     def build_blocks(self, b0: int, b1: int, stream: Optional[int] = None) -> dict:
         _check(lib().spe_table_build_blocks(self.h, int(b0), int(b1), C.c_void_p(stream) if stream else None),
                "spe_table_build_blocks")
+        return self.stats()
+
+    def build_blocks_into(self, b0: int, b1: int, latrel: int, next_hop: int, hops: int,
+                          stream: Optional[int] = None) -> dict:
+        """spe_table_build_blocks_into: rows of blocks [b0, b1) into caller device
+        buffers (pointers to where block b0's elements go)."""
+        _check(lib().spe_table_build_blocks_into(self.h, int(b0), int(b1), C.c_void_p(latrel), C.c_void_p(next_hop),
+                                                 C.c_void_p(hops), C.c_void_p(stream) if stream else None),
+               "spe_table_build_blocks_into")
         return self.stats()
 
     def profile(self, enable: bool = True):
@@ -336,6 +400,18 @@ class PathTable:
         _check(lib().spe_lookup_batch(self.h, C.c_void_p(d_pairs), int(q), C.c_void_p(d_lat), C.c_void_p(d_rel),
                                       C.c_void_p(d_ok), C.c_void_p(stream) if stream else None),
                "spe_lookup_batch")
+
+    def lookup_batch_replica(self, replica: int, d_pairs: int, q: int, d_lat: int, d_rel: int, d_ok: int,
+                             stream: Optional[int] = None):
+        """spe_lookup_batch_replica: queries on replica `replica`'s device, answered from its records."""
+        _check(lib().spe_lookup_batch_replica(self.h, int(replica), C.c_void_p(d_pairs), int(q), C.c_void_p(d_lat),
+                                              C.c_void_p(d_rel), C.c_void_p(d_ok),
+                                              C.c_void_p(stream) if stream else None), "spe_lookup_batch_replica")
+
+    def replica_device(self, replica: int) -> int:
+        d = C.c_int32(0)
+        _check(lib().spe_table_replica_device(self.h, int(replica), C.byref(d)), "spe_table_replica_device")
+        return int(d.value)
 
     def key(self) -> int:
         k = C.c_uint64(0)

@@ -107,7 +107,7 @@ def test_demo_on_shipped_topology(tmp_path, golden_dir):
 @pytest.mark.parametrize("engine", ["1", "2"], ids=["batch", "lds"])
 def test_demo_on_sparse_graph(tmp_path, monkeypatch, engine):
     """Not complete, no preferdirectpaths => every query is an SSSP row."""
-    monkeypatch.setenv("SPE_ENGINE", engine)
+    monkeypatch.setenv("SHADOW_SPE_ENGINE", engine)
     t = graphs.gen_random_small(1500, 4500, 11)
     p = tmp_path / "sparse.graphml"
     graphs.write_graphml(t, str(p))

@@ -219,3 +219,121 @@ def test_gloo_round_robin_chunks_allgather(world):
     for p in procs:
         p.join(timeout=60)
     assert res == {r: True for r in range(world)}
+
+
+def test_shared_fraction_model():
+    """dist.shared_fraction: x* = T1 N / ((N - 1)(S / B + T1)), clipped."""
+    assert sd.shared_fraction(1, 0.3, 160e9, 300e9) == 1.0
+    x4 = sd.shared_fraction(8, 0.28, 160e9, 300e9)     # C4 at N = 8: share ~40 %, recompute the rest
+    assert 0.35 < x4 < 0.45
+    x3 = sd.shared_fraction(8, 0.45, 40e9, 300e9)      # C3: mostly shared
+    assert x4 < x3 < 1.0
+    assert sd.shared_fraction(8, 5.0, 1e6, 300e9) == 1.0   # gathers are free: shard everything
+    # at x*, the build and the gather terms of the model meet
+    N, t1, S, B = 8, 0.28, 160e9, 300e9
+    x = sd.shared_fraction(N, t1, S, B)
+    assert abs(t1 * (x / N + 1 - x) - x * (N - 1) / N * S / B) < 1e-9
+
+
+def test_split_schedule_covers_every_block_once():
+    """Sharded rounds (every gathered part inside [0, S)) plus the local remainder
+    [S, nblk) every rank builds: each block is built by exactly one rank or by all
+    ranks, and a rank's packed next-hop slots cover exactly what it built."""
+    for nblk in (1, 9, 157, 782, 1563):
+        for world in (2, 3, 8):
+            for groups in (1, 26, 391):
+                for frac in (0.0, 0.1, 0.39, 0.88, 1.0):
+                    sizes, S = sd.split_schedule(nblk, world, groups, frac)
+                    l0, l1 = sd.local_span(nblk, S)
+                    if frac < 1.0:
+                        assert S <= nblk and S == world * sum(sizes)
+                    else:
+                        assert S >= nblk and l1 == l0
+                    shared = []
+                    for r in range(world):
+                        built = []
+                        for k, off, g, b0, b1 in sd.rank_chunks_sched(nblk, world, r, sizes):
+                            assert off + world * g <= max(S, nblk) or frac >= 1.0
+                            built += list(range(b0, b1))
+                        shared += built
+                        slots, nslot = sd.rank_next_hop_slots(nblk, world, r, sizes, S)
+                        packed = []
+                        for b0, b1, s0 in slots:
+                            assert s0 == len(packed)
+                            packed += list(range(b0, b1))
+                        assert packed == built + list(range(l0, l1)) and nslot == len(packed)
+                    assert sorted(shared) == list(range(min(S, nblk)))
+                    assert sorted(shared + list(range(l0, l1))) == list(range(nblk))
+
+
+def _split_worker(rank, world, port, out_q):
+    """bench.py's N > 1 step with the compute-versus-gather split on a reduced
+    C4-shaped workload (tiered graph, stub hosts): sharded rounds all-gathered in
+    place, the remainder built by every rank; every rank must end with the whole
+    record span, and its packed next hops / hop counts equal the oracle's for the
+    blocks it built."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys_path_oracle()
+    from oracle import Oracle
+    top = graphs.gen_tiered(n_core=300, n_stub=1200, n_attached=700, seed=9)
+    A = graphs.tiered_attached(top, n_core=300, n_attached=700)
+    nA = A.shape[0]
+    nblk = sd.nblocks(nA)
+    sizes, S = sd.split_schedule(nblk, world, 2, 0.45)
+    l0, l1 = sd.local_span(nblk, S)
+    blk = nA * 64
+    lr = torch.full((max(S, nblk) * blk, 2), float("nan"), dtype=torch.float64)
+    slots, nslot = sd.rank_next_hop_slots(nblk, world, rank, sizes, S)
+    nx = np.full(nslot * blk, -7, dtype=np.int32)
+    hp = np.zeros(nslot * blk, dtype=np.uint16)
+    slot_of = {(b0, b1): s0 for b0, b1, s0 in slots}
+    o = Oracle(top)
+
+    def build(b0, b1):
+        rows = o.rows(A[b0 * 64:min(nA, b1 * 64)], A)
+        rows["hops"] = rows["hops"].astype(np.uint16)
+        f = sd.rows_to_sb64(rows, b0 * 64, nA, b1 - b0)
+        lr[b0 * blk:b1 * blk] = torch.from_numpy(f["lr"])
+        s0 = slot_of[(b0, b1)]
+        nx[s0 * blk:(s0 + b1 - b0) * blk] = f["next"]
+        hp[s0 * blk:(s0 + b1 - b0) * blk] = f["hops"]
+
+    for k, off, g, b0, b1 in sd.rank_chunks_sched(nblk, world, rank, sizes):
+        if b1 > b0:
+            build(b0, b1)
+        sd.allgather_span(lr, off, g, world, rank, blk, dist)
+    if l1 > l0:
+        build(l0, l1)
+    ref = o.rows(A, A)
+    e = sd.sb64_index(np.repeat(np.arange(nA), nA), np.tile(np.arange(nA), nA), nA)
+    got = lr.numpy()[e]
+    ok = np.array_equal(got[:, 0], ref["lat"].ravel()) and np.array_equal(got[:, 1], ref["rel"].ravel())
+    for b0, b1, s0 in slots:
+        for s in range(b0 * 64, min(nA, b1 * 64)):
+            idx = sd.sb64_index(s, np.arange(nA), nA, b0) + s0 * blk
+            ok &= np.array_equal(nx[idx], ref["next"][s]) and np.array_equal(hp[idx].astype(np.int32), ref["hops"][s])
+    out_q.put((rank, bool(ok), S, l1 - l0))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_split_schedule_c4_shaped(world):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] for r in res), res
+    assert all(r[2] > 0 and r[3] > 0 for r in res)   # both parts of the split ran

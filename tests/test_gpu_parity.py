@@ -314,23 +314,43 @@ def test_partially_built_table_refuses_unbuilt_rows(spe):
     assert t.get(200, 3)["latency"] > 0 and t.min_latency() > 0
 
 
+# every relaxation shape libspe instantiates (spe.hip relax_to_convergence):
+# (lanes, SPE_RELAX_*, rows per round trip, waves per SIMD)
+RELAX_SHAPES = [(64, 0, 0, 0), (128, 1, 2, 6), (128, 1, 4, 1), (128, 2, 4, 8), (128, 2, 4, 1), (128, 2, 6, 6),
+                (128, 2, 6, 1), (128, 2, 8, 0)]
+
+
 @pytest.mark.engine_fixed
-@pytest.mark.parametrize("lanes", [16, 32, 64, 128, 256])
-def test_lane_group_widths(spe, lanes):
-    """Every lane-group width of the batch engine (L = 128 / 256: each thread
-    carries 2 / 4 sources; an odd block count pads the last group) on a BA graph
-    whose hubs take the heavy-vertex kernels, and on a tiered graph whose stub
-    sources are pruned pendants."""
+@pytest.mark.parametrize("shape", RELAX_SHAPES, ids=lambda s: f"L{s[0]}-k{s[1]}-r{s[2]}-w{s[3]}")
+def test_lane_group_widths(spe, shape):
+    """Every relaxation shape of the batch engine (64-lane rows: k_relax; 128:
+    k_relax_m with register-staged neighbour rows or k_relax_s with the LDS ring,
+    each thread carrying 2 sources; an odd block count pads the last group) on a
+    BA graph whose hubs take the heavy-vertex kernels, and on a tiered graph whose
+    stub sources are pruned pendants."""
+    lanes, kern, infl, occ = shape
+    kw = dict(lanes=lanes, relax_kernel=kern, rows_in_flight=infl, waves_per_simd=occ, engine=spe.SPE_ENGINE_BATCH)
     ba = graphs.gen_ba(3000, 3, seed=11)
     A = np.arange(0, ba.n, 7, dtype=np.int32)[:5 * 64 + 13]     # 6 blocks, ragged
     ora = Oracle(ba).rows(A, A)
     for groups in (1, 3):
-        out, _, _ = run_gpu(spe, ba, A, groups=groups, lanes=lanes, engine=spe.SPE_ENGINE_BATCH)
-        compare(out, ora, label=f"ba L={lanes} groups={groups}")
+        out, _, _ = run_gpu(spe, ba, A, groups=groups, **kw)
+        compare(out, ora, label=f"ba {shape} groups={groups}")
     tt = graphs.gen_tiered(n_core=1500, n_stub=3000, n_attached=200, seed=5)
     At = graphs.tiered_attached(tt, n_core=1500, n_attached=200)
-    out, _, _ = run_gpu(spe, tt, At, groups=2, lanes=lanes, engine=spe.SPE_ENGINE_BATCH)
-    compare(out, Oracle(tt).rows(At, At), label=f"tiered L={lanes}")
+    out, _, _ = run_gpu(spe, tt, At, groups=2, **kw)
+    compare(out, Oracle(tt).rows(At, At), label=f"tiered {shape}")
+
+
+def test_unbuilt_relaxation_shapes_are_refused(spe):
+    """A tuning request libspe has no kernel for fails at spe_table_create."""
+    top = graphs.gen_random_small(200, 600, 3)
+    g = spe.Graph(top)
+    A = np.arange(top.n, dtype=np.int32)
+    for kw in (dict(lanes=32), dict(lanes=128, relax_kernel=2, rows_in_flight=5),
+               dict(lanes=128, relax_kernel=1, rows_in_flight=3), dict(lanes=128, relax_kernel=2, delta_ms=5.0)):
+        with pytest.raises(spe.SpeError):
+            spe.PathTable(g, A, engine=spe.SPE_ENGINE_BATCH, **kw)
 
 
 K3_GRAPHML = """<graphml xmlns="http://graphml.graphdrawing.org/xmlns">

@@ -1,8 +1,10 @@
 """Multi-device tables in one process (spe_table_opts.devices, spe_multi.cpp):
 Shadow is single-process (shd-master.c:390-394), so the library drives every
 GPU itself -- contiguous source-block shares, one host thread and stream per
-device, then an all-gather of the {latency, reliability} records (RCCL
-ncclAllGather, or peer copies).  CPU: the share / gather-offset arithmetic.
+device, chunk-wise broadcasts of the {latency, reliability} records while the
+next chunk builds (RCCL ncclBroadcast groups, or peer copies), and optionally a
+local remainder every device builds itself (the compute-versus-gather split,
+DESIGN §6).  CPU: the share / split / gather-offset arithmetic.
 GPU: the single-device path through the API with RCCL, and a 3-way split on one
 GPU (peer gather: RCCL refuses a repeated device) against the oracle."""
 import numpy as np
@@ -27,10 +29,31 @@ def test_device_shares_contiguous_and_padded(A, N):
             assert b0 == sh[d - 1][1]
 
 
+@pytest.mark.parametrize("A,N,x", [(100000, 8, 0.39), (50000, 8, 0.88), (700, 3, 0.5), (64, 2, 0.3), (50000, 8, 0.0),
+                                   (6400, 7, 1.0)])
+def test_device_split_arithmetic(A, N, x):
+    """spe_device_split: equal contiguous shares of [0, S), S = N floor(x nblk / N),
+    the local remainder [S, nblk); x = 1 is spe_device_shares."""
+    from shadow_amd import spe
+    sh, S = spe.device_split(A, N, x)
+    nblk = -(-A // 64)
+    if x >= 1.0:
+        assert sh == spe.device_shares(A, N) and S == nblk
+        return
+    cb = int(np.floor(x * nblk / N))
+    assert S == N * cb <= nblk
+    assert sh == [(d * cb, (d + 1) * cb) for d in range(N)]
+    # the model's x* lands C4 at N = 8 near 40 % shared (DESIGN §6)
+    from shadow_amd import dist as sd
+    assert abs(sd.shared_fraction(8, 0.28, 160e9, 300e9) - 0.393) < 0.01
+
+
 def test_device_shares_rejects_bad_arguments():
     from shadow_amd import spe
     with pytest.raises(spe.SpeError):
         spe.device_shares(10, 0)
+    with pytest.raises(spe.SpeError):
+        spe.device_split(10, 2, 1.5)
 
 
 def _check_table(t, top, att, label):
@@ -150,3 +173,45 @@ def test_fw_engine_c2_four_shares_equals_lds_engine():
         for k in ("ok", "lat", "rel", "next", "hops"):
             bad = np.count_nonzero(a[k] != b[k])
             assert bad == 0, f"rows {r0}:{r1} {k}: {bad} entries differ"
+
+
+@pytest.mark.gpu
+@pytest.mark.engine_fixed
+@pytest.mark.parametrize("frac", [0.5, 0.0], ids=["half-shared", "all-local"])
+def test_split_three_shares_overlap_on_one_gpu(frac):
+    """The compute-versus-gather split on three shares of one GPU (peer copies):
+    the first S blocks are built share by share in chunks whose records are copied
+    to the other replicas while the next chunk builds, the rest built by every
+    part itself.  Every replica then answers lookups from its own records
+    (spe_lookup_batch_replica) equal to the oracle, and download / get / min
+    latency route to the part that built each row."""
+    import torch
+    from shadow_amd import spe
+    top = graphs.gen_random_small(1200, 3600, 64)
+    att = np.arange(top.n, dtype=np.int32)
+    g = spe.Graph(top)
+    t = spe.PathTable(g, att, devices=[0, 0, 0], engine=spe.SPE_ENGINE_BATCH, groups=1, shared_fraction=frac)
+    st = t.build()
+    nblk = t.nblocks
+    sh, S = spe.device_split(top.n, 3, frac) if frac > 0 else ([(0, 0)] * 3, 0)
+    assert st["shared_blocks"] == min(S, nblk) and st["local_blocks"] == nblk - min(S, nblk)
+    assert st["gather"] == spe.SPE_GATHER_PEER
+    ref = _check_table(t, top, att, f"split {frac}")
+    for s_slot, t_slot in ((5, 900), (700, 3), (1199, 1199)):
+        e = t.get(s_slot, t_slot)
+        assert e["latency"] == ref["lat"][s_slot, t_slot] and e["hops"] == ref["hops"][s_slot, t_slot]
+    q = 100_000
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    pairs = torch.randint(0, t.A, (q, 2), dtype=torch.int32, device="cuda", generator=gen)
+    p = pairs.cpu().numpy()
+    for rep in range(3):
+        assert t.replica_device(rep) == 0
+        lat = torch.empty(q, dtype=torch.float64, device="cuda")
+        rel = torch.empty(q, dtype=torch.float64, device="cuda")
+        ok = torch.empty(q, dtype=torch.uint8, device="cuda")
+        t.lookup_batch_replica(rep, pairs.data_ptr(), q, lat.data_ptr(), rel.data_ptr(), ok.data_ptr())
+        np.testing.assert_array_equal(lat.cpu().numpy(), ref["lat"][p[:, 0], p[:, 1]], err_msg=f"replica {rep}")
+        np.testing.assert_array_equal(rel.cpu().numpy(), ref["rel"][p[:, 0], p[:, 1]], err_msg=f"replica {rep}")
+    assert t.min_latency() == ref["lat"][ref["kind"] != 0].min()
+    with pytest.raises(spe.SpeError):
+        t.replica_device(3)
