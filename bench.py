@@ -150,13 +150,23 @@ def bench_lookup(args, rank=0, world=1, local=0, dist=None):
     its own 100M queries per step (weak scaling)."""
     import torch
     from shadow_amd import spe
-    top, att, desc = workload(args.c5_table)
     dev = torch.device("cuda", local)
-    g = spe.Graph(top, device=local)
-    if args.c5_table != "c3":
-        att = g.order_sources(att)
-    t = spe.PathTable(g, att)
-    t.build()
+    if world > 1:
+        # the replicated table the N > 1 table build leaves on every GPU (sharded +
+        # all-gathered records, the remainder recomputed): each rank's lookups read
+        # its own replica
+        rep = bench_table(args, rank, world, local, dist, config=args.c5_table, replica_only=True)
+        g, att, desc = rep["graph"], rep["attached"], rep["desc"]
+        lr = rep["lr"]
+        t = spe.PathTable(g, att, blocks=(0, rep["nblk"]), ext=[lr.data_ptr(), lr.data_ptr(), lr.data_ptr()],
+                          ext_filled=True)
+    else:
+        top, att, desc = workload(args.c5_table)
+        g = spe.Graph(top, device=local)
+        if args.c5_table != "c3":
+            att = g.order_sources(att)
+        t = spe.PathTable(g, att)
+        t.build()
     q = args.queries
     gen = torch.Generator(device=dev).manual_seed(5 + rank)
     pairs = torch.randint(0, t.A, (q, 2), dtype=torch.int32, device=dev, generator=gen)
@@ -411,7 +421,7 @@ def calibrate_split(t, lr, blk_elems, nblk, world, rank, dev, dist, span_blocks)
     return float(x[0].item()), float(-x[1].item())
 
 
-def bench_table(args, rank, world, local, dist, config=None):
+def bench_table(args, rank, world, local, dist, config=None, replica_only=False):
     """The default measurement: a step is one WHOLE path table (every source
     row) of the config -- BASELINE's "full path-table time".  At N > 1 (one rank
     per GPU, torchrun) the table is replicated on every GPU at the end of a step,
@@ -494,6 +504,10 @@ def bench_table(args, rank, world, local, dist, config=None):
         torch.cuda.synchronize(dev)
         tg += time.perf_counter() - t1
         return tb, tg, its
+
+    if replica_only:   # C5 at N > 1: one build of the replicated records, then lookups read them
+        one_table()
+        return {"graph": g, "attached": att, "lr": lr, "desc": desc, "table": t, "nblk": nblk}
 
     def barrier():
         if dist is not None:

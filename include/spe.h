@@ -349,6 +349,31 @@ int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, doub
 int spe_lookup_batch_replica(const spe_table* t, int32_t replica, const int32_t* d_pairs, int64_t q,
                              double* d_latency, double* d_reliability, uint8_t* d_ok, void* stream);
 int spe_table_replica_device(const spe_table* t, int32_t replica, int32_t* device);
+
+/* Whole-table self-check on the device (every (s, t) entry, s != t, of a built
+ * single-device table owning every row): the consequences of the reference's
+ * per-target path walk (shd-topology.c:1790-1849) that hold entry by entry --
+ * routable entries have latency > 0, reliability in (0, 1] and hops >= 1; the
+ * next hop is an out-neighbour of s (get_eid(s, next) exists, :1473-1480); where
+ * the next hop is an attached vertex other than t, hops(s, t) = 1 + hops(next, t)
+ * (unique shortest paths: the rest of s's path is next's path); and on an
+ * undirected graph lat / rel of (s, t) and (t, s) agree within 1e-12 relative
+ * (the same edges summed / multiplied in opposite orders).  Counts only: which
+ * of them must be zero depends on the graph (unroutable pairs, ties). */
+typedef struct spe_check_report {
+    int64_t pairs;
+    int64_t unroutable;
+    int64_t bad_values;
+    int64_t next_not_adjacent;
+    int64_t hop_checked;
+    int64_t hop_mismatch;
+    int64_t sym_checked;
+    int64_t sym_mismatch;
+    double max_sym_rel_err;
+    int32_t first_bad_s;            /* one offending (s, t) slot pair, -1 if none */
+    int32_t first_bad_t;
+} spe_check_report;
+int spe_table_check(const spe_table* t, spe_check_report* out);
 /* Minimum latency over every owned routable entry (minimumPathLatency). */
 /* On-disk path-table cache (the reference recomputes its paths
  * every run).  The key hashes everything that determines the rows: the graph

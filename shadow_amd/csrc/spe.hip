@@ -2150,6 +2150,82 @@ __global__ __launch_bounds__(BLOCK) void k_owner_replay(int32_t A, const int32_t
 }
 
 
+// Whole-table self-check (spe_table_check): one thread per SB64 entry (s, t),
+// s != t.  Counters: [0] pairs, [1] unroutable, [2] bad values, [3] next hop not
+// adjacent to s, [4] hop checks, [5] hop mismatches, [6] symmetry checks, [7]
+// symmetry mismatches, [8] max relative asymmetry (f64 bits), [9] first bad pair
+// (s << 32 | t, ~0 = none).  The checks are the per-target walk's consequences
+// (shd-topology.c:1790-1849): the next hop is the path's second vertex, so it is
+// adjacent to s, and on unique shortest paths hops(s, t) = 1 + hops(next, t);
+// on an undirected graph lat(s, t) and lat(t, s) sum the same edges in opposite
+// orders.
+__device__ __forceinline__ void check_bad(unsigned long long* c, int32_t s, int32_t t) {
+    atomicCAS(&c[9], ~0ull, ((unsigned long long)(uint32_t)s << 32) | (uint32_t)t);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_table_check(int32_t A, const int32_t* __restrict__ slot_vertex,
+                                                       const int32_t* __restrict__ vertex_slot, DevGraph G,
+                                                       int32_t undirected, int32_t hop_rule, Table tb,
+                                                       unsigned long long* __restrict__ c) {
+    const int64_t total = (int64_t)((A + WAVE - 1) / WAVE) * A * WAVE;
+    unsigned long long n[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double worst = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLOCK) {
+        const int32_t b = (int32_t)(i / ((int64_t)A * WAVE));
+        const int64_t rem = i - (int64_t)b * A * WAVE;
+        const int32_t ts = (int32_t)(rem / WAVE), ss = b * WAVE + (int32_t)(rem % WAVE);
+        if (ss >= A || ss == ts) continue;
+        ++n[0];
+        const double2 e = tb.lr[i];
+        if (!(e.x > -1.0)) {
+            ++n[1];
+            continue;
+        }
+        const int32_t sv = slot_vertex[ss], tv = slot_vertex[ts];
+        const int32_t nx = tb.next[i];
+        const int32_t h = tb.hops[i];
+        bool bad = false;
+        if (!(e.x > 0.0) || !(e.y > 0.0 && e.y <= 1.0) || h < 1 || nx < 0 || nx >= G.n_full) {
+            ++n[2];
+            bad = true;
+        } else {
+            if (!has_edge(G, sv, nx)) {
+                ++n[3];
+                bad = true;
+            }
+            const int32_t xs = vertex_slot[nx];
+            if (hop_rule && xs >= 0 && nx != tv) {
+                ++n[4];
+                const int32_t h2 = tb.hops[tidx(xs / WAVE, A, ts, xs % WAVE)];
+                if (h != 1 + h2) {
+                    ++n[5];
+                    bad = true;
+                }
+            }
+            if (undirected) {
+                ++n[6];
+                const double2 r = tb.lr[tidx(ts / WAVE, A, ss, ts % WAVE)];
+                const double dl = fabs(e.x - r.x) / e.x, dr = fabs(e.y - r.y) / e.y;
+                const double d = fmax(dl, dr);
+                worst = fmax(worst, d);
+                if (!(d <= 1e-12)) {
+                    ++n[7];
+                    bad = true;
+                }
+            }
+        }
+        if (bad) check_bad(c, ss, ts);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        unsigned long long v = n[k];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if ((threadIdx.x & (WAVE - 1)) == 0 && v) atomicAdd(&c[k], v);
+    }
+    for (int o = 32; o > 0; o >>= 1) worst = fmax(worst, __shfl_xor(worst, o));
+    if ((threadIdx.x & (WAVE - 1)) == 0 && worst > 0.0) atomicMax(&c[8], (unsigned long long)__double_as_longlong(worst));
+}
+
 template <int NT>
 __global__ __launch_bounds__(BLOCK) void k_lookup(const int2* __restrict__ pairs, int64_t q, int32_t blk0,
                                                   int32_t blk1, Table tb, double* __restrict__ lat,
@@ -2748,12 +2824,13 @@ int check_device(int32_t device) {
 
 // The relaxation shapes instantiated in relax_to_convergence (keep in sync).
 #define RELAX_DEFAULT_128 SPE_RELAX_LDS_RING
-#define RELAX_RING_NS 4
+#define RELAX_RING_NS 6
 bool relax_shape_supported(int32_t lanes, int32_t kernel, int32_t infl, int32_t occ, bool delta) {
     if (delta) return true;   // fixed shapes
     if (lanes == 64) return infl == 8 && occ <= 1;
     if (kernel == SPE_RELAX_LDS_RING)
-        return (infl == 4 && (occ <= 1 || occ == 8)) || (infl == 6 && (occ <= 1 || occ == 6)) || (infl == 8 && occ <= 1);
+        return (infl == 4 && (occ <= 1 || occ == 7 || occ == 8)) || (infl == 5 && occ == 7) ||
+               (infl == 6 && (occ <= 1 || occ == 6)) || (infl == 8 && occ <= 1);
     return (infl == 4 && occ <= 1) || (infl == 2 && (occ <= 1 || occ == 6));
 }
 
@@ -3323,7 +3400,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     // waves_per_simd 0 = the default for the shape, 1 = the compiler's choice
     if (t->relax_kernel == SPE_RELAX_LDS_RING) {
         t->infl = o.rows_in_flight > 0 ? o.rows_in_flight : RELAX_RING_NS;
-        t->occ = o.waves_per_simd > 0 ? o.waves_per_simd : (t->infl == 4 ? 8 : t->infl == 6 ? 6 : 1);
+        t->occ = o.waves_per_simd > 0 ? o.waves_per_simd : (t->infl == 4 ? 8 : t->infl == 5 ? 7 : t->infl == 6 ? 6 : 1);
     } else if (!wide) {
         t->infl = 8;
         t->occ = 1;
@@ -3714,8 +3791,10 @@ static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
                                : relax_to_convergence_l<64, 8, 1, true>(t, blocks, s);
     if (t->lanes == 64) return relax_to_convergence_l<64, 8>(t, blocks, s);
     if (t->relax_kernel == SPE_RELAX_LDS_RING) {
-        if (t->infl == 4) return t->occ == 8 ? relax_to_convergence_l<128, 4, 8, false, true>(t, blocks, s)
-                                             : relax_to_convergence_l<128, 4, 1, false, true>(t, blocks, s);
+        if (t->infl == 4) return t->occ == 8   ? relax_to_convergence_l<128, 4, 8, false, true>(t, blocks, s)
+                                 : t->occ == 7 ? relax_to_convergence_l<128, 4, 7, false, true>(t, blocks, s)
+                                               : relax_to_convergence_l<128, 4, 1, false, true>(t, blocks, s);
+        if (t->infl == 5) return relax_to_convergence_l<128, 5, 7, false, true>(t, blocks, s);
         if (t->infl == 6) return t->occ == 6 ? relax_to_convergence_l<128, 6, 6, false, true>(t, blocks, s)
                                              : relax_to_convergence_l<128, 6, 1, false, true>(t, blocks, s);
         return relax_to_convergence_l<128, 8, 1, false, true>(t, blocks, s);
@@ -4122,6 +4201,47 @@ int spe_lookup_batch_replica(const spe_table* t, int32_t replica, const int32_t*
                                                            d_latency, d_reliability, d_ok);
     HIP_TRY(hipGetLastError());
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
+    return SPE_OK;
+}
+
+int spe_table_check(const spe_table* t, spe_check_report* out) {
+    if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
+    if (t->multi) return fail(SPE_EUNSUPPORTED, "spe_table_check runs on single-device tables");
+    if (t->blk0 != 0 || t->blk1 != (t->A + WAVE - 1) / WAVE) return fail(SPE_EUNSUPPORTED, "spe_table_check needs every source row");
+    if (!t->built) return fail(SPE_ESTATE, "table not built");
+    HIP_TRY(hipSetDevice(t->g->device));
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc(&d, 10 * sizeof(unsigned long long)));
+    unsigned long long h[10];
+    std::memset(h, 0, sizeof(h));
+    h[9] = ~0ull;
+    hipError_t e = hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice);
+    // hop rule: per-source rows (no owner replay) of an undirected graph or a directed one alike
+    const int32_t hop_rule = t->d_rank == nullptr;
+    const int32_t undirected = !t->g->hg.directed && t->d_rank == nullptr;
+    if (e == hipSuccess) {
+        const int64_t total = (int64_t)((t->A + WAVE - 1) / WAVE) * t->A * WAVE;
+        k_table_check<<<grid_for(total, BLOCK, 16384), BLOCK, 0, t->stream>>>(
+            t->A, t->d_slot_vertex, t->d_vertex_slot, t->g->dev, undirected, hop_rule, t->tb, d);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(t->stream);
+    if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(SPE_EHIP, std::string("spe_table_check: ") + hipGetErrorString(e));
+    out->pairs = (int64_t)h[0];
+    out->unroutable = (int64_t)h[1];
+    out->bad_values = (int64_t)h[2];
+    out->next_not_adjacent = (int64_t)h[3];
+    out->hop_checked = (int64_t)h[4];
+    out->hop_mismatch = (int64_t)h[5];
+    out->sym_checked = (int64_t)h[6];
+    out->sym_mismatch = (int64_t)h[7];
+    double w;
+    std::memcpy(&w, &h[8], sizeof(w));
+    out->max_sym_rel_err = w;
+    out->first_bad_s = h[9] == ~0ull ? -1 : (int32_t)(h[9] >> 32);
+    out->first_bad_t = h[9] == ~0ull ? -1 : (int32_t)(h[9] & 0xFFFFFFFFu);
     return SPE_OK;
 }
 

@@ -15,7 +15,7 @@ import numpy as np
 from .graphs import Topology
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# SPE_LIB: an alternative build of the library (same-box A/B experiments, tools/build_variant.sh)
+# SPE_LIB: an alternative build of the library (e.g. a -DSPE_DIAGNOSTICS build for ablations)
 LIB_PATH = os.environ.get("SPE_LIB") or os.path.join(_HERE, "libspe.so")
 
 SPE_OK = 0
@@ -88,6 +88,13 @@ class Entry(C.Structure):
 KERNELS = ["init", "seed", "heavy", "relax", "rows", "direct", "lds", "fw"]
 
 
+class CheckReport(C.Structure):
+    _fields_ = [("pairs", C.c_int64), ("unroutable", C.c_int64), ("bad_values", C.c_int64),
+                ("next_not_adjacent", C.c_int64), ("hop_checked", C.c_int64), ("hop_mismatch", C.c_int64),
+                ("sym_checked", C.c_int64), ("sym_mismatch", C.c_int64), ("max_sym_rel_err", C.c_double),
+                ("first_bad_s", C.c_int32), ("first_bad_t", C.c_int32)]
+
+
 class KernelProfile(C.Structure):
     _fields_ = [("ms", C.c_double * 8), ("launches", C.c_int64 * 8)]
 
@@ -109,7 +116,7 @@ EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_
            "spe_table_key", "spe_table_save", "spe_table_load", "spe_table_free",
            "spe_graph_set_edge_aux", "spe_table_download_aux", "spe_fw_apsp", "spe_fw_closure", "spe_graph_self_path",
            "spe_graph_adjacent", "spe_device_shares", "spe_graph_edge", "spe_table_source_tree",
-           "spe_device_split", "spe_lookup_batch_replica", "spe_table_replica_device"]
+           "spe_device_split", "spe_lookup_batch_replica", "spe_table_replica_device", "spe_table_check"]
 
 _lib = None
 
@@ -149,6 +156,7 @@ def lib():
         L.spe_lookup_batch.argtypes = [P, P, C.c_int64, P, P, P, P]
         L.spe_lookup_batch_replica.argtypes = [P, C.c_int32, P, C.c_int64, P, P, P, P]
         L.spe_table_replica_device.argtypes = [P, C.c_int32, P]
+        L.spe_table_check.argtypes = [P, P]
         L.spe_device_split.argtypes = [C.c_int32, C.c_int32, C.c_double, P, P, P]
         L.spe_table_min_latency.argtypes = [P, P]
         L.spe_table_key.argtypes = [P, P]
@@ -407,6 +415,12 @@ class PathTable:
         _check(lib().spe_lookup_batch_replica(self.h, int(replica), C.c_void_p(d_pairs), int(q), C.c_void_p(d_lat),
                                               C.c_void_p(d_rel), C.c_void_p(d_ok),
                                               C.c_void_p(stream) if stream else None), "spe_lookup_batch_replica")
+
+    def check(self) -> dict:
+        """spe_table_check: whole-table invariants counted on the device."""
+        r = CheckReport()
+        _check(lib().spe_table_check(self.h, C.byref(r)), "spe_table_check")
+        return {f: getattr(r, f) for f, _ in CheckReport._fields_}
 
     def replica_device(self, replica: int) -> int:
         d = C.c_int32(0)

@@ -76,17 +76,34 @@ def check_sampled_rows(t, top, order, slots, label):
     return ora
 
 
+def check_whole_table(t, A, label, hop_rule=True):
+    """spe_table_check over every entry: all routable with sane values, next hops
+    adjacent to their sources, hops(s, t) = 1 + hops(next, t) where the next hop is
+    attached (unique shortest paths), lat / rel symmetric within 1e-12 relative."""
+    r = t.check()
+    assert r["pairs"] == A * (A - 1), f"{label}: {r}"
+    assert r["unroutable"] == 0 and r["bad_values"] == 0 and r["next_not_adjacent"] == 0, f"{label}: {r}"
+    if hop_rule:
+        assert r["hop_checked"] > 0 and r["hop_mismatch"] == 0, f"{label}: {r}"
+    assert r["sym_checked"] == r["pairs"] and r["sym_mismatch"] == 0, f"{label}: {r}"
+    assert r["max_sym_rel_err"] < 1e-13, f"{label}: {r}"
+    return r
+
+
 def test_c3_bench_build_every_launch(spe):
-    """C3 (50k BA) full table, bench settings: two+ rows of every launch vs the oracle."""
+    """C3 (50k BA) full table, bench settings: 64 rows of every launch vs the
+    oracle, and the whole-table invariants over all 2.5e9 entries."""
     top = graphs.gen_ba(50000, 3, 3)
     att = np.arange(top.n, dtype=np.int32)
     g, t, order = bench_table(spe, top, att)
     lay = t.layout()
     assert lay["engine"] == spe.SPE_ENGINE_BATCH
-    slots = launch_sample_slots(t.A, lay["groups_per_launch"], extra_per_launch=1, seed=3)
+    slots = launch_sample_slots(t.A, lay["groups_per_launch"], extra_per_launch=62, seed=3)
     nlaunch = -(-t.nblocks // lay["groups_per_launch"])
-    assert len(slots) >= 2 * nlaunch
+    assert len(slots) >= 32 * nlaunch
     check_sampled_rows(t, top, order, slots, "C3")
+    r = check_whole_table(t, t.A, "C3")
+    assert r["hop_checked"] > 0.9 * r["pairs"]   # every vertex is attached: most next hops are too
 
 
 def test_c2_bench_build_lds_engine(spe):
@@ -109,8 +126,12 @@ def test_c4_one_gpu_full_table_every_launch(spe):
     g, t, order = bench_table(spe, top, att)
     lay = t.layout()
     assert lay["block_begin"] == 0 and lay["block_end"] == t.nblocks
-    slots = launch_sample_slots(t.A, lay["groups_per_launch"])
+    slots = launch_sample_slots(t.A, lay["groups_per_launch"], extra_per_launch=14, seed=4)
+    nlaunch = -(-t.nblocks // lay["groups_per_launch"])
+    assert len(slots) >= 8 * nlaunch
     check_sampled_rows(t, top, order, slots, "C4")
+    # next hops of stub sources are their (unattached) anchors: no hop rule here
+    check_whole_table(t, t.A, "C4", hop_rule=False)
 
 
 def test_c5_full_size_lookups(spe):

@@ -383,3 +383,37 @@ def test_k3_triangle_known_answers(spe, prefer):
     else:
         assert out["lat"][0, 2] == 20.0 and out["rel"][0, 2] == ((1.0 * 1.0) * 1.0) * 0.95 * 0.95
         assert out["next"][0, 2] == 1 and out["hops"][0, 2] == 2
+
+
+def test_table_check_counts(spe, golden_dir):
+    """spe_table_check on small tables: a tie-free undirected graph passes every
+    invariant; the shipped (complete, DIRECT) topology too (next hop = target,
+    one hop); and a corrupted entry is caught and named."""
+    top = graphs.gen_random_small(600, 1800, 71)
+    A = np.arange(top.n, dtype=np.int32)
+    out, t, g = run_gpu(spe, top, A)
+    r = t.check()
+    assert r["pairs"] == top.n * (top.n - 1) and r["unroutable"] == 0 and r["bad_values"] == 0
+    assert r["next_not_adjacent"] == 0 and r["hop_checked"] > 0 and r["hop_mismatch"] == 0
+    assert r["sym_checked"] == r["pairs"] and r["sym_mismatch"] == 0 and r["first_bad_s"] == -1
+    ship, z = shipped(golden_dir)
+    As = np.arange(ship.n, dtype=np.int32)
+    _, ts, _ = run_gpu(spe, ship, As)
+    rs = ts.check()
+    assert rs["pairs"] == ship.n * (ship.n - 1) and rs["next_not_adjacent"] == 0 and rs["bad_values"] == 0
+    assert rs["sym_mismatch"] == 0 and rs["hop_checked"] == 0   # DIRECT: the next hop is the target
+    # a table over caller-owned storage, one next hop corrupted: the check names it
+    import torch
+    nb = (top.n + 63) // 64
+    elems = nb * top.n * 64
+    lr = torch.empty((elems, 2), dtype=torch.float64, device="cuda")
+    nx = torch.empty(elems, dtype=torch.int32, device="cuda")
+    hp = torch.empty(elems, dtype=torch.int16, device="cuda")
+    t2 = spe.PathTable(g, A, ext=[lr.data_ptr(), nx.data_ptr(), hp.data_ptr()])
+    t2.build()
+    assert t2.check()["first_bad_s"] == -1
+    s_slot, t_slot = 77, 301
+    nx[((s_slot // 64) * top.n + t_slot) * 64 + s_slot % 64] = -5
+    torch.cuda.synchronize()
+    r2 = t2.check()
+    assert r2["bad_values"] == 1 and (r2["first_bad_s"], r2["first_bad_t"]) == (s_slot, t_slot)

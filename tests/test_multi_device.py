@@ -177,7 +177,7 @@ def test_fw_engine_c2_four_shares_equals_lds_engine():
 
 @pytest.mark.gpu
 @pytest.mark.engine_fixed
-@pytest.mark.parametrize("frac", [0.5, 0.0], ids=["half-shared", "all-local"])
+@pytest.mark.parametrize("frac", [0.5, 1e-6], ids=["half-shared", "all-local"])
 def test_split_three_shares_overlap_on_one_gpu(frac):
     """The compute-versus-gather split on three shares of one GPU (peer copies):
     the first S blocks are built share by share in chunks whose records are copied
@@ -193,7 +193,7 @@ def test_split_three_shares_overlap_on_one_gpu(frac):
     t = spe.PathTable(g, att, devices=[0, 0, 0], engine=spe.SPE_ENGINE_BATCH, groups=1, shared_fraction=frac)
     st = t.build()
     nblk = t.nblocks
-    sh, S = spe.device_split(top.n, 3, frac) if frac > 0 else ([(0, 0)] * 3, 0)
+    sh, S = spe.device_split(top.n, 3, frac)
     assert st["shared_blocks"] == min(S, nblk) and st["local_blocks"] == nblk - min(S, nblk)
     assert st["gather"] == spe.SPE_GATHER_PEER
     ref = _check_table(t, top, att, f"split {frac}")

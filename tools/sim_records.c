@@ -6,7 +6,9 @@
  *   REC  distance-only relaxation where a row that changes publishes a packed
  *        record {128-bit lane mask, the changed lanes' distances} for the next
  *        round (stale by one round), followed by a parent pass and a
- *        level-synchronous tree pass for (r, h, f).
+ *        level-synchronous tree pass for (r, h, f);
+ *   DIST distance-only relaxation with live rows (GS, no route records), then
+ *        the same parent pass and tree pass.
  *
  * Byte model: 128-B lines, per row visit; a 128-lane f64 row is 8 lines, i32
  * 4, u16 2.  Gathers count distinct (row, line) pairs.
@@ -65,7 +67,7 @@ static int gather_lines(const int32_t* rows, const mask128* lanes, int per_line)
     return c;
 }
 
-/* mode 0 = GS, 1 = REC */
+/* mode 0 = GS, 1 = REC, 2 = DIST */
 int sim_run(int32_t n, const int32_t* ptr, const int32_t* col, const double* w, const int32_t* src, int mode,
             sim_out* out) {
     memset(out, 0, sizeof(*out));
@@ -118,7 +120,7 @@ int sim_run(int32_t n, const int32_t* ptr, const int32_t* col, const double* w, 
                 if (!fl[cur][k]) continue;
                 fl[cur][k] = 0;
                 const int u = col[k];
-                if (mode == 0) {
+                if (mode != 1) {
                     out->nbr_lines += 8;
                     for (int l = 0; l < L; ++l) {
                         if (src[l] == v) continue;
@@ -146,13 +148,15 @@ int sim_run(int32_t n, const int32_t* ptr, const int32_t* col, const double* w, 
                     }
                 }
             }
-            out->own_lines += (mode == 0) ? 8 : lines_of(&offered, 16);
+            out->own_lines += (mode != 1) ? 8 : lines_of(&offered, 16);
             const int c = popc128(&ch);
             out->lane_updates += c;
             if (mode == 0) {
                 for (int l = 0; l < L; ++l) prow[l] = par[(size_t)v * L + l];
                 out->route_lines += gather_lines(prow, &ch, 8);               /* parent RT (16 B) */
                 out->wr_lines += lines_of(&ch, 16) + lines_of(&ch, 32) + lines_of(&ch, 8);   /* D, P, RT */
+            } else if (mode == 2) {
+                out->wr_lines += lines_of(&ch, 16);   /* D only */
             } else {
                 out->wr_lines += lines_of(&ch, 16) + (c ? 1 + (c * 8 + 127) / 128 : 0);   /* D + record */
                 rec[cur][v] = ch;
@@ -174,7 +178,7 @@ int sim_run(int32_t n, const int32_t* ptr, const int32_t* col, const double* w, 
         if (!any) break;
     }
     out->rd_lines = out->nbr_lines + out->own_lines + out->route_lines + out->visits * 2;   /* +2: CSR, flags */
-    if (mode == 1) {
+    if (mode != 0) {
         /* parent pass: every row reads all in-neighbour rows + own, writes P (i32) */
         for (int v = 0; v < n; ++v) {
             out->par_rd += 8 + 8 * (ptr[v + 1] - ptr[v]) + 2;
