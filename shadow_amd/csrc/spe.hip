@@ -2829,7 +2829,7 @@ bool relax_shape_supported(int32_t lanes, int32_t kernel, int32_t infl, int32_t 
     if (delta) return true;   // fixed shapes
     if (lanes == 64) return infl == 8 && occ <= 1;
     if (kernel == SPE_RELAX_LDS_RING)
-        return (infl == 4 && (occ <= 1 || occ == 7 || occ == 8)) || (infl == 5 && occ == 7) ||
+        return (infl == 4 && (occ <= 1 || occ == 8)) ||
                (infl == 6 && (occ <= 1 || occ == 6)) || (infl == 8 && occ <= 1);
     return (infl == 4 && occ <= 1) || (infl == 2 && (occ <= 1 || occ == 6));
 }
@@ -3400,7 +3400,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     // waves_per_simd 0 = the default for the shape, 1 = the compiler's choice
     if (t->relax_kernel == SPE_RELAX_LDS_RING) {
         t->infl = o.rows_in_flight > 0 ? o.rows_in_flight : RELAX_RING_NS;
-        t->occ = o.waves_per_simd > 0 ? o.waves_per_simd : (t->infl == 4 ? 8 : t->infl == 5 ? 7 : t->infl == 6 ? 6 : 1);
+        t->occ = o.waves_per_simd > 0 ? o.waves_per_simd : (t->infl == 4 ? 8 : t->infl == 6 ? 6 : 1);
     } else if (!wide) {
         t->infl = 8;
         t->occ = 1;
@@ -3792,9 +3792,7 @@ static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
     if (t->lanes == 64) return relax_to_convergence_l<64, 8>(t, blocks, s);
     if (t->relax_kernel == SPE_RELAX_LDS_RING) {
         if (t->infl == 4) return t->occ == 8   ? relax_to_convergence_l<128, 4, 8, false, true>(t, blocks, s)
-                                 : t->occ == 7 ? relax_to_convergence_l<128, 4, 7, false, true>(t, blocks, s)
                                                : relax_to_convergence_l<128, 4, 1, false, true>(t, blocks, s);
-        if (t->infl == 5) return relax_to_convergence_l<128, 5, 7, false, true>(t, blocks, s);
         if (t->infl == 6) return t->occ == 6 ? relax_to_convergence_l<128, 6, 6, false, true>(t, blocks, s)
                                              : relax_to_convergence_l<128, 6, 1, false, true>(t, blocks, s);
         return relax_to_convergence_l<128, 8, 1, false, true>(t, blocks, s);
