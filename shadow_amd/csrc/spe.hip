@@ -4351,20 +4351,48 @@ int spe_table_source_tree(spe_table* t, int32_t s_slot, int32_t* parent) {
     // unreached); -2 (batch / FW state) the pruned pendant source itself
     std::vector<int32_t> pk((size_t)std::max(1, nc), -1);
     HIP_TRY(hipSetDevice(t->g->device));
+    // The source is re-run into scratch rows of one block, never into the table itself:
+    // concurrent readers of a live table (the topology shim's queries) keep seeing its
+    // finished rows (a prefer-direct row would otherwise lack the DIRECT overlay for a while).
+    const size_t be = (size_t)t->A * WAVE;
+    const bool scratch = !t->tb.prev && !t->tb.aux;   // aux tables (offline tool only) rebuild in place
+    void* sbuf = nullptr;
+    if (scratch) HIP_TRY(hipMalloc(&sbuf, be * (sizeof(double2) + sizeof(int32_t) + sizeof(uint16_t))));
+    double2* s_lr = (double2*)sbuf;
+    int32_t* s_next = (int32_t*)(s_lr + (scratch ? be : 0));
+    uint16_t* s_hops = (uint16_t*)(s_next + (scratch ? be : 0));
+    int rc = SPE_OK;
     if (t->engine == SPE_ENGINE_LDS) {
-        // one workgroup re-runs this source (its row is rewritten with the same bits); the
-        // parent entries stay in that workgroup's scratch
-        k_sssp_lds<<<1, LDS_T, lds_bytes(nc), t->stream>>>(s_slot, s_slot + 1, t->d_slots, t->blk0, t->g->dev, t->md,
-                                                         t->tb, t->lsc, nullptr);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(pk.data(), t->lsc.par, sizeof(int32_t) * (size_t)nc, hipMemcpyDeviceToHost, t->stream));
-        HIP_TRY(hipStreamSynchronize(t->stream));
-        // preferdirectpaths: the row just rewritten lacks the DIRECT overlay; rebuild the block
-        if (t->md.prefer)
-            if (int r = spe_table_build_blocks(t, b, b + 1, nullptr)) return r;
+        // one workgroup re-runs this source; the parent entries stay in that workgroup's scratch
+        Table tb = t->tb;
+        int32_t blk0 = t->blk0;
+        if (scratch) {
+            tb.lr = s_lr;
+            tb.next = s_next;
+            tb.hops = s_hops;
+            blk0 = b;   // the scratch holds block b only
+        }
+        k_sssp_lds<<<1, LDS_T, lds_bytes(nc), t->stream>>>(s_slot, s_slot + 1, t->d_slots, blk0, t->g->dev, t->md, tb,
+                                                         t->lsc, nullptr);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(pk.data(), t->lsc.par, sizeof(int32_t) * (size_t)nc,
+                                                hipMemcpyDeviceToHost, t->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(t->stream);
+        if (e != hipSuccess) rc = fail(SPE_EHIP, hipGetErrorString(e));
+        // in place (aux tables): the row just rewritten lacks the DIRECT overlay; rebuild the block
+        if (!rc && !scratch && t->md.prefer) rc = spe_table_build_blocks(t, b, b + 1, nullptr);
     } else {
-        // rebuild the source's block (same rows); its state is left in the first buffer
-        if (int r = spe_table_build_blocks(t, b, b + 1, nullptr)) return r;
+        // re-run the source's block; its state is left in the first buffer
+        rc = scratch ? spe_table_build_blocks_into(t, b, b + 1, s_lr, s_next, s_hops, nullptr)
+                     : spe_table_build_blocks(t, b, b + 1, nullptr);
+        if (!rc) {
+            const hipError_t e = hipStreamSynchronize(t->stream);
+            if (e != hipSuccess) rc = fail(SPE_EHIP, hipGetErrorString(e));
+        }
+    }
+    if (sbuf) (void)hipFree(sbuf);
+    if (rc) return rc;
+    if (t->engine != SPE_ENGINE_LDS) {
         const int32_t L = t->lanes, j = s_slot % WAVE;
         const int32_t g = L <= WAVE ? j / L : 0, lane = L <= WAVE ? j % L : j;
         const int32_t* P = t->st_buf[0].P + ((size_t)g * nc) * (size_t)L + (size_t)lane;

@@ -100,6 +100,7 @@ typedef struct {
     double* mrel;
     _Atomic(double*)* blocks;      /* lazy mirror per 64-source block: lat[rows][A], rel[rows][A] */
     _Atomic int64_t row_budget;    /* bytes left for lazy blocks; beyond it: spe_table_get */
+    int64_t mirror_budget;         /* the budget this snapshot was given (full or lazy) */
     pthread_mutex_t row_mu;
     double min_latency;            /* over every routable entry */
 } Snap;
@@ -997,7 +998,35 @@ static int64_t env_bytes(const char* name, int64_t dflt) {
 }
 
 /* Build a table over `att` (A vertices) and its host-side view. */
-static int snap_build(Topology* top, const int32_t* att_in, int32_t A, Snap** out) {
+/* Host-mirror budget: SHADOW_SPE_MIRROR_BYTES, else min(8 GiB, a quarter of the
+ * host's available memory) -- a re-seal holds the old snapshot's mirror while the
+ * new one is filled, so the caller subtracts what the published snapshot holds. */
+static int64_t mem_available_bytes(void) {
+    FILE* f = fopen("/proc/meminfo", "r");
+    if (!f) return -1;
+    char line[256];
+    int64_t kb = -1;
+    while (fgets(line, sizeof line, f))
+        if (sscanf(line, "MemAvailable: %lld kB", (long long*)&kb) == 1) break;
+    fclose(f);
+    return kb < 0 ? -1 : kb * 1024;
+}
+
+static int64_t mirror_budget_default(void) {
+    int64_t b = (int64_t)8 << 30;
+    const int64_t avail = mem_available_bytes();
+    if (avail > 0 && avail / 4 < b) b = avail / 4;
+    return env_bytes("SHADOW_SPE_MIRROR_BYTES", b);
+}
+
+/* bytes of host mirror a snapshot holds */
+static int64_t snap_mirror_bytes(const Snap* s) {
+    if (!s) return 0;
+    if (s->mlat) return (int64_t)s->A * s->A * 16;
+    return s->blocks ? s->mirror_budget - atomic_load(&s->row_budget) : 0;
+}
+
+static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t budget, Snap** out) {
     *out = NULL;
     Snap* s = calloc(1, sizeof(Snap));
     pthread_mutex_init(&s->row_mu, NULL);
@@ -1055,10 +1084,11 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, Snap** ou
         if (rc == SPE_OK && cpath[0] && spe_table_save(s->table, cpath) != SPE_OK)
             tlog(top, LOG_WARNING, "could not save the path table cache: %s", spe_last_error());
     }
-    /* host view: the whole table when it fits SHADOW_SPE_MIRROR_BYTES (default
-     * 8 GiB: A <= 23k), else 64-source blocks mirrored on first use within that
+    /* host view: the whole table when it fits the mirror budget (mirror_budget_default:
+     * 8 GiB holds A <= 23k), else 64-source blocks mirrored on first use within that
      * budget, then single-entry device reads (spe_table_get) */
-    const int64_t budget = env_bytes("SHADOW_SPE_MIRROR_BYTES", (int64_t)8 << 30);
+    if (budget < 0) budget = 0;
+    s->mirror_budget = budget;
     const int64_t full = (int64_t)A * A * 16;
     if (rc == SPE_OK && full <= budget) {
         s->mlat = malloc((size_t)A * A * sizeof(double));
@@ -1096,7 +1126,11 @@ int32_t topology_seal(Topology* top) {
             rc = SPE_ESTATE;
         } else {
             const double t0 = now_s();
-            rc = snap_build(top, att, A, &s);   /* no lock held: queries on the old table go on */
+            /* the published snapshot's mirror stays allocated until the swap below */
+            pthread_rwlock_rdlock(&top->state_lock);
+            const int64_t held = snap_mirror_bytes(top->snap);
+            pthread_rwlock_unlock(&top->state_lock);
+            rc = snap_build(top, att, A, mirror_budget_default() - held, &s);   /* no lock held: queries on the old table go on */
             if (rc == SPE_OK) {
                 top->build_seconds += now_s() - t0;
                 top->build_rows += A;
