@@ -523,8 +523,11 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
     t0 = time.perf_counter()
     tb_sum = tg_sum = 0.0
     it_total = 0
+    step_s = []
     for _ in range(steps):
+        ts = time.perf_counter()
         tb, tg, its = one_table()
+        step_s.append(time.perf_counter() - ts)
         tb_sum += tb
         tg_sum += tg
         it_total += its
@@ -611,6 +614,7 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
             "gather_wait_s_per_step": round(tg_sum / steps, 4) if gather else None,
             "gather_bytes_per_gpu_per_step": gathered,
             "relax_rounds_per_step": round(it_total / max(1, steps), 1),
+            "rank0_step_s": [round(x, 4) for x in step_s],
             "roofline": roof, "cpu_baseline": cpu,
         }
         if gather:

@@ -607,7 +607,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_relax(int32_t total, int32_t n, 
     const int64_t all_units = ((int64_t)total + 7) >> 3;   // mark buffers padded to 8 bytes
     const int32_t xcd = blockIdx.x & 7;
     const int64_t waves_per_xcd = ((int64_t)(gridDim.x >> 3) * BLOCK) >> 6;
-    const int64_t wave = ((int64_t)(blockIdx.x >> 3) * BLOCK + threadIdx.x) >> 6;
+    const int64_t wave = (int64_t)(blockIdx.x >> 3) * (BLOCK / WAVE) +
+                         __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));   // uniform: SGPRs
     const int64_t lo = all_units * xcd / 8, hi = all_units * (xcd + 1) / 8;
     bool wrote = false;
     int64_t u8 = lo + wave;
@@ -940,7 +941,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_relax_m(int32_t total, int32_t n
     const int64_t all_units = ((int64_t)total + 7) >> 3;
     const int32_t xcd = blockIdx.x & 7;
     const int64_t waves_per_xcd = ((int64_t)(gridDim.x >> 3) * BLOCK) >> 6;
-    const int64_t wave = ((int64_t)(blockIdx.x >> 3) * BLOCK + threadIdx.x) >> 6;
+    const int64_t wave = (int64_t)(blockIdx.x >> 3) * (BLOCK / WAVE) +
+                         __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));   // uniform: SGPRs
     const int64_t lo = all_units * xcd / 8, hi = all_units * (xcd + 1) / 8;
     bool wrote = false;
     int64_t u8 = lo + wave;
@@ -976,6 +978,87 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_relax_m(int32_t total, int32_t n
 //    the kernel holds fewer live registers.
 // Offers, finish and marks are k_relax_m's (same canonical keys, same routes):
 // the relaxation order changes nothing in the fixpoint.
+// The ring kernel's per-lane relaxation state, leaner than Best: the lane's
+// state index is recomputed where needed and the stored distance is not kept --
+// whether the finish must write follows from two bits (the distance dropped; the
+// lane was unreached) and the stored parent, read lazily as before.
+struct Lean {
+    double bd;      // best distance so far (starts at the stored one)
+    double bdu;     // distance of the chosen parent (-1: not resolved yet)
+    int32_t bk;     // in-CSR entry of the parent edge (PK_UNREAD / -1 none / -2 pendant seed)
+    int32_t bu;     // parent vertex (-1: not resolved yet)
+    int32_t pold;   // the stored parent once read (PK_UNREAD until then)
+    uint32_t fl;    // LEAN_NEED | LEAN_DROP | LEAN_INF
+};
+constexpr uint32_t LEAN_NEED = 1u, LEAN_DROP = 2u, LEAN_INF = 4u;
+
+template <int L>
+__device__ __forceinline__ void offer_lean(Lean& b, const DevGraph& G, const State& st, int32_t g, int32_t n, int32_t v,
+                                           int32_t j, int32_t kk, int32_t u, double du, double alt) {
+    bool better = false;
+    if (alt < b.bd) {
+        better = true;
+        b.fl |= LEAN_DROP;
+    } else if (alt == b.bd) {
+        if (b.bk == PK_UNREAD) b.bk = b.pold = st.P[sidx<L>(g, n, v, j)];
+        if (kk == b.bk) {   // the current parent re-offers: refresh its route
+            b.fl |= LEAN_NEED;
+            b.bdu = du;
+            b.bu = u;
+        } else if (b.bk >= 0) {   // exact tie: canonical (d[u], u)
+            if (b.bu < 0) b.bu = G.icol[b.bk];
+            if (b.bdu < 0.0) b.bdu = st.D[sidx<L>(g, n, b.bu, j)];
+            better = (du < b.bdu) || (du == b.bdu && u < b.bu);
+        }
+    }
+    if (better) {
+        b.bd = alt;
+        b.bk = kk;
+        b.bu = u;
+        b.bdu = du;
+        b.fl |= LEAN_NEED;
+    }
+}
+
+// finish_vertex_m on Lean lanes (same routes, same writes)
+template <int M>
+__device__ __forceinline__ bool finish_lean(Lean (&b)[M], const DevGraph& G, const State& st, int32_t g, int32_t n,
+                                            int32_t lane, int32_t v, const int32_t (&s)[M]) {
+    constexpr int L = WAVE * M;
+    Route pu[M], old[M];
+    double ia[M];
+    bool same[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        same[m] = false;
+        if (b[m].fl & LEAN_NEED) {
+            pu[m] = st.RT[sidx<L>(g, n, b[m].bu, lane + m * WAVE)];
+            ia[m] = G.ia[b[m].bk];
+            // a refresh or a tie (no drop, reached before) read the stored parent
+            same[m] = !(b[m].fl & (LEAN_DROP | LEAN_INF)) && b[m].bk == b[m].pold;
+            if (same[m]) old[m] = st.RT[sidx<L>(g, n, v, lane + m * WAVE)];
+        }
+    }
+    bool changed = false;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        if (!(b[m].fl & LEAN_NEED)) continue;
+        Route nr;
+        nr.r = pu[m].r * ia[m];
+        nr.h = pu[m].h + 1;
+        nr.f = (b[m].bu == s[m]) ? G.corev[v] : pu[m].f;
+        const bool ch = !same[m] || nr.r != old[m].r || nr.h != old[m].h || nr.f != old[m].f;
+        if (ch) {
+            const size_t rv = sidx<L>(g, n, v, lane + m * WAVE);
+            st.D[rv] = b[m].bd;
+            st.P[rv] = b[m].bk;
+            st.RT[rv] = nr;
+        }
+        changed |= ch;
+    }
+    return changed;
+}
+
 template <int NS>
 struct RelaxRing {
     double row[NS][2 * WAVE];   // one wave's LDS slots: 128 lanes of one neighbour row each
@@ -999,22 +1082,21 @@ __device__ __forceinline__ bool relax_item_s(int64_t e, int32_t k0, int32_t k1, 
     const int4 pk = ok ? G.ipack[k] : make_int4(0, 0, 0, 0);
     const size_t fo = (size_t)g * G.nrel + k;
     const bool f = ok && fl.in_cur[fo] != 0;
-    Best b[M];
+    Lean b[M];
     int32_t s[M];
-    double d_old[M];
-    bool active[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
         const int32_t j = lane + m * WAVE;
         s[m] = e >= 0 ? srcv[g * L + j] : -1;
-        const size_t rv = sidx<L>(g, n, v, j);
-        d_old[m] = e >= 0 ? st.D[rv] : INF;
+        b[m].bd = e >= 0 ? st.D[sidx<L>(g, n, v, j)] : INF;
     }
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-        const int32_t p = d_old[m] < INF ? PK_UNREAD : -1;
-        b[m] = Best{d_old[m], p, -1, -1.0, false, p, sidx<L>(g, n, v, lane + m * WAVE)};
-        active[m] = (e >= 0) && (s[m] != -1) && (s[m] != v);
+        const bool reached = b[m].bd < INF;
+        b[m].bk = b[m].pold = reached ? PK_UNREAD : -1;
+        b[m].bu = -1;
+        b[m].bdu = -1.0;
+        b[m].fl = reached ? 0u : LEAN_INF;
     }
     const int32_t u_j = pk.x;
     const double w_j = __hiloint2double(pk.w, pk.z);
@@ -1051,12 +1133,16 @@ __device__ __forceinline__ bool relax_item_s(int64_t e, int32_t k0, int32_t k1, 
             for (int m = 0; m < M; ++m) {
                 const double du = ring->row[q][lane + m * WAVE];
                 const double alt = du + w;
-                if (active[m] && alt > du) offer<L>(b[m], G, st, g, n, lane + m * WAVE, kk, u, du, alt);
+                const bool active = s[m] != -1 && s[m] != v;   // (e < 0: s = -1)
+                if (active && alt > du) offer_lean<L>(b[m], G, st, g, n, v, lane + m * WAVE, kk, u, du, alt);
             }
+            // one slot's values live at a time: the next slot's LDS reads are not hoisted
+            // above these offers (holding all NS rows in VGPRs costs occupancy)
+            asm volatile("" ::: "memory");
         }
     }
     bool changed = false;
-    if (e >= 0) changed = finish_vertex_m<M>(b, G, st, g, n, lane, v, s, d_old);
+    if (e >= 0) changed = finish_lean<M>(b, G, st, g, n, lane, v, s);
     if (__ballot(changed)) {
         if (G.undirected) {   // the out-list IS the in-list: marks from registers
             if (ok) {
@@ -1085,12 +1171,15 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_relax_s(int32_t total, int32_t n
     __shared__ RelaxRing<NS> rings[BLOCK / WAVE];
     if (*fl.prev_changed == 0) return;
     const int32_t lane = threadIdx.x & (WAVE - 1);
-    RelaxRing<NS>* ring = &rings[threadIdx.x >> 6];
+    // wave-uniform values made provably uniform (readfirstlane): the ring base, the
+    // unit cursor and the (group, vertex) division then live in SGPRs, not VGPRs
+    const int32_t wib = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));
+    RelaxRing<NS>* ring = &rings[wib];
     uint64_t* words = reinterpret_cast<uint64_t*>(fl.mark_cur);
     const int64_t all_units = ((int64_t)total + 7) >> 3;
     const int32_t xcd = blockIdx.x & 7;
     const int64_t waves_per_xcd = ((int64_t)(gridDim.x >> 3) * BLOCK) >> 6;
-    const int64_t wave = ((int64_t)(blockIdx.x >> 3) * BLOCK + threadIdx.x) >> 6;
+    const int64_t wave = (int64_t)(blockIdx.x >> 3) * (BLOCK / WAVE) + wib;
     const int64_t lo = all_units * xcd / 8, hi = all_units * (xcd + 1) / 8;
     bool wrote = false;
     int64_t u8 = lo + wave;
@@ -2824,13 +2913,12 @@ int check_device(int32_t device) {
 
 // The relaxation shapes instantiated in relax_to_convergence (keep in sync).
 #define RELAX_DEFAULT_128 SPE_RELAX_LDS_RING
-#define RELAX_RING_NS 6
+#define RELAX_RING_NS 5   // 5 LDS slots per wave at 7 waves / SIMD
 bool relax_shape_supported(int32_t lanes, int32_t kernel, int32_t infl, int32_t occ, bool delta) {
     if (delta) return true;   // fixed shapes
     if (lanes == 64) return infl == 8 && occ <= 1;
     if (kernel == SPE_RELAX_LDS_RING)
-        return (infl == 4 && (occ <= 1 || occ == 8)) ||
-               (infl == 6 && (occ <= 1 || occ == 6)) || (infl == 8 && occ <= 1);
+        return (infl == 4 && occ == 8) || (infl == 5 && occ == 7) || (infl == 6 && occ == 6);
     return (infl == 4 && occ <= 1) || (infl == 2 && (occ <= 1 || occ == 6));
 }
 
@@ -3400,7 +3488,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     // waves_per_simd 0 = the default for the shape, 1 = the compiler's choice
     if (t->relax_kernel == SPE_RELAX_LDS_RING) {
         t->infl = o.rows_in_flight > 0 ? o.rows_in_flight : RELAX_RING_NS;
-        t->occ = o.waves_per_simd > 0 ? o.waves_per_simd : (t->infl == 4 ? 8 : t->infl == 6 ? 6 : 1);
+        t->occ = o.waves_per_simd > 0 ? o.waves_per_simd : (t->infl == 4 ? 8 : t->infl == 5 ? 7 : t->infl == 6 ? 6 : 1);
     } else if (!wide) {
         t->infl = 8;
         t->occ = 1;
@@ -3791,11 +3879,9 @@ static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
                                : relax_to_convergence_l<64, 8, 1, true>(t, blocks, s);
     if (t->lanes == 64) return relax_to_convergence_l<64, 8>(t, blocks, s);
     if (t->relax_kernel == SPE_RELAX_LDS_RING) {
-        if (t->infl == 4) return t->occ == 8   ? relax_to_convergence_l<128, 4, 8, false, true>(t, blocks, s)
-                                               : relax_to_convergence_l<128, 4, 1, false, true>(t, blocks, s);
-        if (t->infl == 6) return t->occ == 6 ? relax_to_convergence_l<128, 6, 6, false, true>(t, blocks, s)
-                                             : relax_to_convergence_l<128, 6, 1, false, true>(t, blocks, s);
-        return relax_to_convergence_l<128, 8, 1, false, true>(t, blocks, s);
+        if (t->infl == 4) return relax_to_convergence_l<128, 4, 8, false, true>(t, blocks, s);
+        if (t->infl == 6) return relax_to_convergence_l<128, 6, 6, false, true>(t, blocks, s);
+        return relax_to_convergence_l<128, 5, 7, false, true>(t, blocks, s);
     }
     if (t->infl == 4) return relax_to_convergence_l<128, 4>(t, blocks, s);
     return t->occ == 6 ? relax_to_convergence_l<128, 2, 6>(t, blocks, s) : relax_to_convergence_l<128, 2>(t, blocks, s);

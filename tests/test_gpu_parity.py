@@ -316,8 +316,8 @@ def test_partially_built_table_refuses_unbuilt_rows(spe):
 
 # every relaxation shape libspe instantiates (spe.hip relax_to_convergence):
 # (lanes, SPE_RELAX_*, rows per round trip, waves per SIMD)
-RELAX_SHAPES = [(64, 0, 0, 0), (128, 1, 2, 6), (128, 1, 4, 1), (128, 2, 4, 8), (128, 2, 4, 1), (128, 2, 6, 6),
-                (128, 2, 6, 1), (128, 2, 8, 0)]
+RELAX_SHAPES = [(64, 0, 0, 0), (128, 1, 2, 6), (128, 1, 4, 1), (128, 2, 4, 8), (128, 2, 5, 7), (128, 2, 6, 6),
+                (128, 2, 0, 0)]
 
 
 @pytest.mark.engine_fixed
@@ -347,7 +347,8 @@ def test_unbuilt_relaxation_shapes_are_refused(spe):
     top = graphs.gen_random_small(200, 600, 3)
     g = spe.Graph(top)
     A = np.arange(top.n, dtype=np.int32)
-    for kw in (dict(lanes=32), dict(lanes=128, relax_kernel=2, rows_in_flight=5),
+    for kw in (dict(lanes=32), dict(lanes=128, relax_kernel=2, rows_in_flight=3),
+               dict(lanes=128, relax_kernel=2, rows_in_flight=6, waves_per_simd=1),
                dict(lanes=128, relax_kernel=1, rows_in_flight=3), dict(lanes=128, relax_kernel=2, delta_ms=5.0)):
         with pytest.raises(spe.SpeError):
             spe.PathTable(g, A, engine=spe.SPE_ENGINE_BATCH, **kw)

@@ -29,6 +29,7 @@ typedef struct {
     int64_t par_rd, par_wr;           /* REC: parent pass */
     int64_t tree_visits, tree_rounds, tree_rd, tree_wr;
     int64_t max_hops;
+    int64_t prune_row, prune_line16, prune_line32, nbr_reads;   /* GS: min/max summary tests */
 } sim_out;
 
 typedef struct {
@@ -122,6 +123,32 @@ int sim_run(int32_t n, const int32_t* ptr, const int32_t* col, const double* w, 
                 const int u = col[k];
                 if (mode != 1) {
                     out->nbr_lines += 8;
+                    out->nbr_reads++;
+                    {   /* summary tests (conservative): line j of u can be skipped when
+                         * fl(min over the line's lanes of d_u + w) > max over them of d_v */
+                        double mn16[8], mx16[8];
+                        for (int j = 0; j < 8; ++j) {
+                            mn16[j] = INFINITY;
+                            mx16[j] = -INFINITY;
+                        }
+                        for (int l = 0; l < L; ++l) {
+                            const double du = d[(size_t)u * L + l], dv = d[(size_t)v * L + l];
+                            if (du < mn16[l / 16]) mn16[l / 16] = du;
+                            if (src[l] != v && dv > mx16[l / 16]) mx16[l / 16] = dv;
+                        }
+                        int all = 1;
+                        for (int j = 0; j < 8; ++j) {
+                            const int sk = mn16[j] + w[k] > mx16[j];
+                            out->prune_line16 += sk;
+                            all &= sk;
+                        }
+                        for (int j = 0; j < 4; ++j) {
+                            const double mn = fmin(mn16[2 * j], mn16[2 * j + 1]);
+                            const double mx = fmax(mx16[2 * j], mx16[2 * j + 1]);
+                            out->prune_line32 += 2 * (mn + w[k] > mx);
+                        }
+                        out->prune_row += 8 * all;
+                    }
                     for (int l = 0; l < L; ++l) {
                         if (src[l] == v) continue;
                         double a = d[(size_t)u * L + l] + w[k];

@@ -20,7 +20,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
 from shadow_amd import graphs  # noqa: E402
 
 FIELDS = ["rounds", "visits", "lane_updates", "rd_lines", "wr_lines", "nbr_lines", "own_lines", "route_lines",
-          "par_rd", "par_wr", "tree_visits", "tree_rounds", "tree_rd", "tree_wr", "max_hops"]
+          "par_rd", "par_wr", "tree_visits", "tree_rounds", "tree_rd", "tree_wr", "max_hops", "prune_row",
+          "prune_line16", "prune_line32", "nbr_reads"]
 
 
 class Out(C.Structure):
