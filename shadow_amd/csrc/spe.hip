@@ -380,9 +380,6 @@ __global__ __launch_bounds__(BLOCK) void k_seed(int32_t n, int32_t groups, const
 // current distance (a refresh from the parent, or a tie) needs it; most offers
 // are strictly better or worse, so most visits skip the 256-B P row.
 constexpr int32_t PK_UNREAD = -3;
-#ifndef SPE_NT_MODE
-#define SPE_NT_MODE 0
-#endif
 
 struct Best {
     double bd;     // best alt (= distance)
@@ -1091,11 +1088,7 @@ __device__ __forceinline__ bool relax_item_s(int64_t e, int32_t k0, int32_t k1, 
     for (int m = 0; m < M; ++m) {
         const int32_t j = lane + m * WAVE;
         s[m] = e >= 0 ? srcv[g * L + j] : -1;
-#if SPE_NT_MODE & 1   // experiment: the own row streams past L2 (read once per visit)
-        b[m].bd = e >= 0 ? __builtin_nontemporal_load(&st.D[sidx<L>(g, n, v, j)]) : INF;
-#else
         b[m].bd = e >= 0 ? st.D[sidx<L>(g, n, v, j)] : INF;
-#endif
     }
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -1127,14 +1120,7 @@ __device__ __forceinline__ bool relax_item_s(int64_t e, int32_t k0, int32_t k1, 
             if (bs[q] >= 0) {
                 const int32_t u = __builtin_amdgcn_readlane(u_j, bs[q]);
                 const double* src = gbase + (size_t)u * L + 2 * lane;   // 16 B per lane: the whole 1-KB row
-#if SPE_NT_MODE & 2   // experiment: light neighbours' rows non-temporal, heavy (hub) rows kept in L2
-                if (__builtin_amdgcn_readlane(pk.y, bs[q]) < 0)
-                    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)&ring->row[q][0], 16, 0, 0);
-                else
-                    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)&ring->row[q][0], 16, 0, 2);
-#else
                 __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)&ring->row[q][0], 16, 0, 0);
-#endif
             }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -3974,6 +3960,10 @@ int spe_table_build_blocks_into(spe_table* t, int32_t block_begin, int32_t block
 
 static int build_blocks_impl(spe_table* t, int32_t block_begin, int32_t block_end, void* stream) {
     HIP_TRY(hipSetDevice(t->g->device));
+    if (t->trace)   // where the relaxation state lives (run-to-run placement studies)
+        for (int i = 0; i < 2; ++i)
+            fprintf(stderr, "spe-trace-buf %d D %p P %p RT %p in %p mark %p\n", i, (void*)t->st_buf[i].D,
+                    (void*)t->st_buf[i].P, (void*)t->st_buf[i].RT, (void*)t->inflag[i], (void*)t->mark[i]);
     hipStream_t s = stream ? (hipStream_t)stream : t->stream;
     const auto t0 = std::chrono::steady_clock::now();
     const spe_graph* g = t->g;
