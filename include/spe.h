@@ -161,6 +161,9 @@ typedef struct spe_table_opts {
     double shared_fraction;
     double gather_gbps;
     double build_seconds_hint;      /* one-device whole-table build time, if the caller measured it */
+    /* 1: the batch engine relaxes the graph itself instead of its degree-3 contraction
+     * (same rows; the contraction is the default where it applies) */
+    int32_t no_contract;
 } spe_table_opts;
 
 #define SPE_RELAX_AUTO 0            /* the default below */
@@ -207,6 +210,8 @@ typedef struct spe_table_layout {
     int32_t device;                 /* the device latrel lives on */
     int32_t lanes_per_group;        /* batch engine: sources per relaxation row (64 or 128 by default) */
     int32_t relax_kernel;           /* batch engine: the SPE_RELAX_* kernel it runs */
+    int32_t contracted_vertices;    /* batch engine on the degree-3 contraction: its relaxation
+                                     * vertices (0: the table relaxes the graph itself) */
 } spe_table_layout;
 
 typedef struct spe_entry {

@@ -46,6 +46,7 @@
 #include <queue>
 #include <random>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "spe_internal.h"
@@ -129,6 +130,20 @@ struct DevGraph {
     const int32_t* dcol;
     const double* dwrep;
     const double* darep;
+    // Degree-3 contraction (spe_graph.devx, the batch engine's graph when the
+    // table runs on it; NULL in the plain graph).  Relaxation ids are then the kept
+    // vertices; entry k offers fl(fl(d[icol[k]] + iw[k]) + xw2[k]) (xw2 = 0 for a plain
+    // edge: the same bits as one add), its parent of record is core vertex xkey[k] (x
+    // for a shortcut), and the route multiplies ia[k] then xa2[k] and adds 1 + (xvia >= 0)
+    // hops.  A removed vertex's rows come from its three neighbours (rnb / rw / ra).
+    const double* xw2;
+    const double* xa2;
+    const int32_t* xkey;
+    const int32_t* xvia;         // original id of x, -1 for a plain edge
+    const int32_t* xrm;          // [n_full] removed index, -1 otherwise
+    const int32_t* rnb;          // [3 removed] kept ids of the neighbours (increasing)
+    const double* rw;
+    const double* ra;
 };
 
 struct RowMode {
@@ -215,7 +230,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_state(int32_t n, int32_t groups,
     const int64_t per = (int64_t)n * L;
     const int32_t j = threadIdx.x & (L - 1);
     const int32_t s = srcv[g * L + j];   // original id, -1 = padding lane
-    int32_t sc = -1, anc = -1, kx = -1;
+    int32_t sc = -1, anc = -1, kx = -1, rm = -1;
     double r0 = 1.0;
     if (s >= 0) {
         const double fs = vfac[s];
@@ -224,7 +239,14 @@ __global__ __launch_bounds__(BLOCK) void k_init_state(int32_t n, int32_t groups,
         if (sc < 0) {
             anc = G.anchor_core[s];
             kx = G.fiptr[s];
+            if (G.xrm) rm = G.xrm[s];   // a contracted source: its three edges seed the relaxation
         }
+    }
+    int32_t rn0 = -1, rn1 = -1, rn2 = -1;
+    if (rm >= 0) {
+        rn0 = G.rnb[3 * rm];
+        rn1 = G.rnb[3 * rm + 1];
+        rn2 = G.rnb[3 * rm + 2];
     }
     const size_t base = (size_t)g * (size_t)per;
     for (int64_t x = (int64_t)blockIdx.x * BLOCK + threadIdx.x; x < per; x += (int64_t)gridDim.x * BLOCK) {
@@ -246,6 +268,18 @@ __global__ __launch_bounds__(BLOCK) void k_init_state(int32_t n, int32_t groups,
             p = -2;
             Route rt;
             rt.r = r0 * G.fia[kx];
+            rt.h = 1;
+            rt.f = G.corev[v];
+            st.RT[i] = rt;
+        } else if (rm >= 0 && (v == rn0 || v == rn1 || v == rn2)) {
+            // contracted source: its first edge to each neighbour, an offer like any
+            // other (a shorter path through another neighbour replaces it); P = -2 as
+            // for a pendant source: the parent is the source itself, which wins ties
+            const int32_t q = v == rn0 ? 0 : (v == rn1 ? 1 : 2);
+            d = 0.0 + G.rw[3 * rm + q];
+            p = -2;
+            Route rt;
+            rt.r = r0 * G.ra[3 * rm + q];
             rt.h = 1;
             rt.f = G.corev[v];
             st.RT[i] = rt;
@@ -357,19 +391,26 @@ __global__ __launch_bounds__(BLOCK) void k_delta_advance(int32_t n, int32_t nrel
     if (threadIdx.x == 0) ds.minrej[g] = left;
 }
 
+// One wave per source entry (a hub source's out-list spreads over the lanes).
 template <int L>
 __global__ __launch_bounds__(BLOCK) void k_seed(int32_t n, int32_t groups, const int32_t* __restrict__ srcv,
                                                 DevGraph G, uint8_t* mark, uint8_t* hmark, uint8_t* in_flags) {
-    const int32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const int32_t i = __builtin_amdgcn_readfirstlane((int32_t)((blockIdx.x * BLOCK + threadIdx.x) >> 6));
+    const int32_t lane = threadIdx.x & (WAVE - 1);
     if (i >= groups * L) return;
     const int32_t s0 = srcv[i];
     if (s0 < 0) return;
     const int32_t sc = G.core_id[s0];
-    const int32_t s = sc >= 0 ? sc : G.anchor_core[s0];
     const int32_t g = i / L;
-    for (int32_t k = G.optr[s]; k < G.optr[s + 1]; ++k) {
-        (G.oheavy[k] ? hmark : mark)[(size_t)g * n + G.ocol[k]] = 1;
-        in_flags[(size_t)g * G.nrel + G.orev[k]] = 1;
+    const int32_t rm = (sc < 0 && G.xrm) ? G.xrm[s0] : -1;
+    // rows holding the source's first values: its own, its pendant anchor, or (a
+    // contracted source) its three neighbours
+    for (int32_t q = 0; q < (rm >= 0 ? 3 : 1); ++q) {
+        const int32_t s = rm >= 0 ? G.rnb[3 * rm + q] : (sc >= 0 ? sc : G.anchor_core[s0]);
+        for (int32_t k = G.optr[s] + lane; k < G.optr[s + 1]; k += WAVE) {
+            (G.oheavy[k] ? hmark : mark)[(size_t)g * n + G.ocol[k]] = 1;
+            in_flags[(size_t)g * G.nrel + G.orev[k]] = 1;
+        }
     }
 }
 
@@ -421,6 +462,45 @@ __device__ __forceinline__ void offer(Best& b, const DevGraph& G, const State& s
     }
 }
 
+// offer<L> on the contracted graph (the heavy combine): b.bu holds the parent-of-
+// record key (a core id), b.bdu its distance; two shortcuts through the same x
+// tie-break on their kept vertices (d[a], a).
+template <int L>
+__device__ __forceinline__ void offer_x(Best& b, const DevGraph& G, const State& st, int32_t g, int32_t n, int32_t j,
+                                        int32_t kk, int32_t key, double drec, double alt) {
+    bool better = false;
+    if (alt < b.bd) {
+        better = true;
+    } else if (alt == b.bd) {
+        if (b.bk == PK_UNREAD) b.bk = b.pold = st.P[b.rv];
+        if (kk == b.bk) {
+            b.need = true;
+            b.bdu = drec;
+            b.bu = key;
+        } else if (b.bk >= 0) {
+            const int4 po = G.ipack[b.bk];
+            if (b.bu < 0) b.bu = G.xkey[b.bk];
+            if (b.bdu < 0.0) {
+                const double da = st.D[sidx<L>(g, n, po.x, j)];
+                b.bdu = (po.y & 0x40000000) ? da + __hiloint2double(po.w, po.z) : da;
+            }
+            better = drec < b.bdu || (drec == b.bdu && key < b.bu);
+            if (drec == b.bdu && key == b.bu) {   // same x: x's own canonical parent decides
+                const int32_t an = G.ipack[kk].x, ao = po.x;
+                const double dn = st.D[sidx<L>(g, n, an, j)], dd = st.D[sidx<L>(g, n, ao, j)];
+                better = dn < dd || (dn == dd && an < ao);
+            }
+        }
+    }
+    if (better) {
+        b.bd = alt;
+        b.bk = kk;
+        b.bu = key;
+        b.bdu = drec;
+        b.need = true;
+    }
+}
+
 // Flagged candidates of one L-entry chunk [c0, c0+L) of a vertex's in-list.
 // `sm` = subgroup-relative mask of flagged entries (subgroup-uniform); rows of
 // the flagged neighbours are gathered INFL at a time; f(kk, u, du, alt) is
@@ -464,6 +544,27 @@ __device__ __forceinline__ bool finish_vertex(Best& b, const DevGraph& G, const 
     bool changed = false;
     // need with b.bd == d_old implies an equal offer, which read the stored parent
     const int32_t p_old = b.pold;
+    if (b.need && G.xw2) {   // contracted graph (heavy combine): route from the entry's kept vertex
+        const int32_t ga = G.icol[b.bk];
+        const int32_t via = G.xvia[b.bk];
+        const Route pu = st.RT[sidx<L>(g, n, ga, j)];
+        Route nr;
+        nr.r = (pu.r * G.ia[b.bk]) * G.xa2[b.bk];
+        nr.h = pu.h + (via >= 0 ? 2 : 1);
+        nr.f = (ga == s) ? (via >= 0 ? via : G.corev[v]) : pu.f;
+        if (d_old == INF || b.bd != d_old || b.bk != p_old) {
+            changed = true;
+        } else {
+            const Route old = st.RT[rv];
+            changed = (nr.r != old.r) || (nr.h != old.h) || (nr.f != old.f);
+        }
+        if (changed) {
+            st.D[rv] = b.bd;
+            st.P[rv] = b.bk;
+            st.RT[rv] = nr;
+        }
+        return changed;
+    }
     if (b.need) {
         if (b.bu < 0) b.bu = G.icol[b.bk];
         if (G.ablate & 1) {   // diagnostic only: distances + parents, no route records
@@ -1059,16 +1160,108 @@ __device__ __forceinline__ bool finish_lean(Lean (&b)[M], const DevGraph& G, con
     return changed;
 }
 
+// Lean lanes on the degree-3 contracted graph (DevGraph.xw2 != NULL): an entry's
+// parent of record (the canonical key) is core vertex xkey[k] -- x for a shortcut a ->
+// v via x, whose distance is fl(d[a] + w1) -- while its route is gathered from the
+// kept vertex a = icol[k].  Two shortcuts through the same x tie-break on x's own
+// canonical parent: (d[a], a).
+struct LeanX {
+    double bd;
+    double bdu;     // distance of the parent of record (-1: not resolved yet)
+    int32_t bk;
+    int32_t bu;     // kept vertex the route is gathered from (-1: not resolved yet)
+    int32_t bkey;   // core id of the parent of record
+    int32_t pold;
+    uint32_t fl;
+};
+
+template <int L>
+__device__ __forceinline__ void offer_leanx(LeanX& b, const DevGraph& G, const State& st, int32_t g, int32_t n,
+                                            int32_t v, int32_t j, int32_t kk, int32_t u, int32_t key, double du,
+                                            double drec, double alt) {
+    bool better = false;
+    if (alt < b.bd) {
+        better = true;
+        b.fl |= LEAN_DROP;
+    } else if (alt == b.bd) {
+        if (b.bk == PK_UNREAD) b.bk = b.pold = st.P[sidx<L>(g, n, v, j)];
+        if (kk == b.bk) {
+            b.fl |= LEAN_NEED;
+            b.bdu = drec;
+            b.bu = u;
+            b.bkey = key;
+        } else if (b.bk >= 0) {
+            const int4 pb = G.ipack[b.bk];
+            if (b.bu < 0) {
+                b.bu = pb.x;
+                b.bkey = G.xkey[b.bk];
+            }
+            const double da = st.D[sidx<L>(g, n, b.bu, j)];
+            if (b.bdu < 0.0) b.bdu = (pb.y & 0x40000000) ? da + __hiloint2double(pb.w, pb.z) : da;
+            better = (drec < b.bdu) || (drec == b.bdu && (key < b.bkey || (key == b.bkey && (du < da || (du == da && u < b.bu)))));
+        }
+    }
+    if (better) {
+        b.bd = alt;
+        b.bk = kk;
+        b.bu = u;
+        b.bkey = key;
+        b.bdu = drec;
+        b.fl |= LEAN_NEED;
+    }
+}
+
+template <int M>
+__device__ __forceinline__ bool finish_leanx(LeanX (&b)[M], const DevGraph& G, const State& st, int32_t g, int32_t n,
+                                             int32_t lane, int32_t v, const int32_t (&s)[M]) {
+    constexpr int L = WAVE * M;
+    Route pu[M], old[M];
+    double a1[M], a2[M];
+    int32_t via[M];
+    bool same[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        same[m] = false;
+        if (b[m].fl & LEAN_NEED) {
+            pu[m] = st.RT[sidx<L>(g, n, b[m].bu, lane + m * WAVE)];
+            a1[m] = G.ia[b[m].bk];
+            a2[m] = G.xa2[b[m].bk];
+            via[m] = G.xvia[b[m].bk];
+            same[m] = !(b[m].fl & (LEAN_DROP | LEAN_INF)) && b[m].bk == b[m].pold;
+            if (same[m]) old[m] = st.RT[sidx<L>(g, n, v, lane + m * WAVE)];
+        }
+    }
+    bool changed = false;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        if (!(b[m].fl & LEAN_NEED)) continue;
+        Route nr;
+        nr.r = (pu[m].r * a1[m]) * a2[m];   // the path order: edge a -> x, then x -> v
+        nr.h = pu[m].h + (via[m] >= 0 ? 2 : 1);
+        nr.f = (b[m].bu == s[m]) ? (via[m] >= 0 ? via[m] : G.corev[v]) : pu[m].f;
+        const bool ch = !same[m] || nr.r != old[m].r || nr.h != old[m].h || nr.f != old[m].f;
+        if (ch) {
+            const size_t rv = sidx<L>(g, n, v, lane + m * WAVE);
+            st.D[rv] = b[m].bd;
+            st.P[rv] = b[m].bk;
+            st.RT[rv] = nr;
+        }
+        changed |= ch;
+    }
+    return changed;
+}
+
 template <int NS>
 struct RelaxRing {
     double row[NS][2 * WAVE];   // one wave's LDS slots: 128 lanes of one neighbour row each
 };
 
-template <int NS>
+template <int NS, bool CX = false>
 __device__ __forceinline__ bool relax_item_s(int64_t e, int32_t k0, int32_t k1, int32_t n, int32_t lane,
                                              const int32_t* __restrict__ srcv, const DevGraph& G, const State& st,
                                              const Flags& fl, RelaxRing<NS>* ring) {
     constexpr int M = 2, L = WAVE * M;
+    using LaneT = typename std::conditional<CX, LeanX, Lean>::type;
     int32_t g = 0, v = 0;
     if (e >= 0) {
         g = (int32_t)(e / n);
@@ -1082,7 +1275,15 @@ __device__ __forceinline__ bool relax_item_s(int64_t e, int32_t k0, int32_t k1, 
     const int4 pk = ok ? G.ipack[k] : make_int4(0, 0, 0, 0);
     const size_t fo = (size_t)g * G.nrel + k;
     const bool f = ok && fl.in_cur[fo] != 0;
-    Lean b[M];
+    double w2_j = 0.0;   // CX: second weight and parent-of-record key of the lane's entry
+    int32_t key_j = 0;
+    if constexpr (CX) {
+        if (ok) {
+            w2_j = G.xw2[k];
+            key_j = G.xkey[k];
+        }
+    }
+    LaneT b[M];
     int32_t s[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -1097,6 +1298,7 @@ __device__ __forceinline__ bool relax_item_s(int64_t e, int32_t k0, int32_t k1, 
         b[m].bu = -1;
         b[m].bdu = -1.0;
         b[m].fl = reached ? 0u : LEAN_INF;
+        if constexpr (CX) b[m].bkey = -1;
     }
     const int32_t u_j = pk.x;
     const double w_j = __hiloint2double(pk.w, pk.z);
@@ -1129,12 +1331,27 @@ __device__ __forceinline__ bool relax_item_s(int64_t e, int32_t k0, int32_t k1, 
             const int32_t u = __builtin_amdgcn_readlane(u_j, bs[q]);
             const double w = sub_get_d<WAVE>(w_j, bs[q]);
             const int32_t kk = k0 + bs[q];
+            if constexpr (CX) {
+                const double w2 = sub_get_d<WAVE>(w2_j, bs[q]);
+                const int32_t key = __builtin_amdgcn_readlane(key_j, bs[q]);
+                const bool sc = (__builtin_amdgcn_readlane(pk.y, bs[q]) & 0x40000000) != 0;
 #pragma unroll
-            for (int m = 0; m < M; ++m) {
-                const double du = ring->row[q][lane + m * WAVE];
-                const double alt = du + w;
-                const bool active = s[m] != -1 && s[m] != v;   // (e < 0: s = -1)
-                if (active && alt > du) offer_lean<L>(b[m], G, st, g, n, v, lane + m * WAVE, kk, u, du, alt);
+                for (int m = 0; m < M; ++m) {
+                    const double du = ring->row[q][lane + m * WAVE];
+                    const double dx = du + w;           // the shortcut's x (a plain edge: the offer)
+                    const double alt = dx + w2;         // + 0.0 for a plain edge: the same bits
+                    const bool active = s[m] != -1 && s[m] != v;
+                    if (active && alt > du)
+                        offer_leanx<L>(b[m], G, st, g, n, v, lane + m * WAVE, kk, u, key, du, sc ? dx : du, alt);
+                }
+            } else {
+#pragma unroll
+                for (int m = 0; m < M; ++m) {
+                    const double du = ring->row[q][lane + m * WAVE];
+                    const double alt = du + w;
+                    const bool active = s[m] != -1 && s[m] != v;   // (e < 0: s = -1)
+                    if (active && alt > du) offer_lean<L>(b[m], G, st, g, n, v, lane + m * WAVE, kk, u, du, alt);
+                }
             }
             // one slot's values live at a time: the next slot's LDS reads are not hoisted
             // above these offers (holding all NS rows in VGPRs costs occupancy)
@@ -1142,11 +1359,15 @@ __device__ __forceinline__ bool relax_item_s(int64_t e, int32_t k0, int32_t k1, 
         }
     }
     bool changed = false;
-    if (e >= 0) changed = finish_lean<M>(b, G, st, g, n, lane, v, s);
+    if constexpr (CX) {
+        if (e >= 0) changed = finish_leanx<M>(b, G, st, g, n, lane, v, s);
+    } else {
+        if (e >= 0) changed = finish_lean<M>(b, G, st, g, n, lane, v, s);
+    }
     if (__ballot(changed)) {
         if (G.undirected) {   // the out-list IS the in-list: marks from registers
             if (ok) {
-                const int32_t orev = pk.y & 0x7FFFFFFF;
+                const int32_t orev = pk.y & (CX ? 0x3FFFFFFF : 0x7FFFFFFF);
                 (pk.y < 0 ? fl.hmark_next : fl.mark_next)[(size_t)g * n + u_j] = 1;
                 fl.in_next[(size_t)g * G.nrel + orev] = 1;
             }
@@ -1165,7 +1386,7 @@ __device__ __forceinline__ int2 unit_bounds(int64_t unit, int32_t lane, int32_t 
     return make_int2(iptr[v], iptr[v + 1]);
 }
 
-template <int NS, int OCC = 1>
+template <int NS, int OCC = 1, bool CX = false>
 __global__ __launch_bounds__(BLOCK, OCC) void k_relax_s(int32_t total, int32_t n, const int32_t* __restrict__ srcv,
                                                       DevGraph G, State st, Flags fl) {
     __shared__ RelaxRing<NS> rings[BLOCK / WAVE];
@@ -1199,13 +1420,13 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_relax_s(int32_t total, int32_t n
             if (e >= total) e = -1;
             const int32_t k0 = __builtin_amdgcn_readlane(bnd.x, bit);
             const int32_t k1 = __builtin_amdgcn_readlane(bnd.y, bit);
-            wrote |= relax_item_s<NS>(e, k0, k1, n, lane, srcv, G, st, fl, ring);
+            wrote |= relax_item_s<NS, CX>(e, k0, k1, n, lane, srcv, G, st, fl, ring);
         }
     }
     if (__ballot(wrote) && lane == 0) *fl.any_changed = 1;
 }
 
-template <int M, int INFL>
+template <int M, int INFL, bool CX = false>
 __global__ __launch_bounds__(BLOCK) void k_heavy_partial_m(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
                                                            DevGraph G, State st, HeavyPlan hp, Partial pp, Flags fl) {
     if (*fl.prev_changed == 0) return;
@@ -1239,15 +1460,75 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_partial_m(int32_t groups, int32
         const size_t fo = (size_t)g * G.nrel + k;
         const bool f = ok && fl.in_cur[fo] != 0;
         if (f) fl.in_cur[fo] = 0;
-        scan_chunk_m<M, INFL>(__ballot(f), kb, pk.x, __hiloint2double(pk.w, pk.z), g, n, lane, active, st,
-                              [&](int m, int32_t kk, int32_t u, double du, double alt) {
-                                  if (alt < ba[m] || (alt == ba[m] && (du < bdu[m] || (du == bdu[m] && u < bu[m])))) {
-                                      ba[m] = alt;
-                                      bdu[m] = du;
-                                      bu[m] = u;
-                                      bk[m] = kk;
-                                  }
-                              });
+        if constexpr (CX) {   // contracted graph: shortcut entries, keys (alt, d[parent], parent, d[a], a)
+            const double w2_j = ok ? G.xw2[k] : 0.0;
+            const int32_t key_j = ok ? G.xkey[k] : 0;
+            const double w1_j = __hiloint2double(pk.w, pk.z);
+            double bda[M];
+            int32_t bua[M];
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                bda[m] = INF;
+                bua[m] = -1;
+            }
+            for (uint64_t sm = __ballot(f); sm;) {
+                // INFL flagged rows per memory round trip (as scan_chunk_m)
+                int32_t bs[INFL];
+                double dus[INFL][M];
+#pragma unroll
+                for (int q = 0; q < INFL; ++q) {
+                    bs[q] = -1;
+                    if (sm) {
+                        bs[q] = __builtin_ctzll(sm);
+                        sm &= sm - 1;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < INFL; ++q)
+                    if (bs[q] >= 0) {
+                        const int32_t u = __builtin_amdgcn_readlane(pk.x, bs[q]);
+                        const double* row = st.D + ((size_t)g * (size_t)n + (size_t)u) * L;
+#pragma unroll
+                        for (int m = 0; m < M; ++m) dus[q][m] = row[lane + m * WAVE];
+                    }
+#pragma unroll
+                for (int q = 0; q < INFL; ++q) {
+                if (bs[q] < 0) continue;
+                const int32_t b = bs[q];
+                const int32_t u = __builtin_amdgcn_readlane(pk.x, b);
+                const double w1 = sub_get_d<WAVE>(w1_j, b), w2 = sub_get_d<WAVE>(w2_j, b);
+                const int32_t key = __builtin_amdgcn_readlane(key_j, b);
+                const bool sc = (__builtin_amdgcn_readlane(pk.y, b) & 0x40000000) != 0;
+#pragma unroll
+                for (int m = 0; m < M; ++m) {
+                    const double du = dus[q][m];
+                    const double dx = du + w1, alt = dx + w2, drec = sc ? dx : du;
+                    if (!(active[m] && alt > du)) continue;
+                    if (alt < ba[m] ||
+                        (alt == ba[m] &&
+                         (drec < bdu[m] ||
+                          (drec == bdu[m] && (key < bu[m] || (key == bu[m] && (du < bda[m] || (du == bda[m] && u < bua[m])))))))) {
+                        ba[m] = alt;
+                        bdu[m] = drec;
+                        bu[m] = key;
+                        bk[m] = kb + b;
+                        bda[m] = du;
+                        bua[m] = u;
+                    }
+                }
+                }
+            }
+        } else {
+            scan_chunk_m<M, INFL>(__ballot(f), kb, pk.x, __hiloint2double(pk.w, pk.z), g, n, lane, active, st,
+                                  [&](int m, int32_t kk, int32_t u, double du, double alt) {
+                                      if (alt < ba[m] || (alt == ba[m] && (du < bdu[m] || (du == bdu[m] && u < bu[m])))) {
+                                          ba[m] = alt;
+                                          bdu[m] = du;
+                                          bu[m] = u;
+                                          bk[m] = kk;
+                                      }
+                                  });
+        }
 #pragma unroll
         for (int m = 0; m < M; ++m) {
             const size_t o = ((size_t)g * hp.nseg + sgi) * L + lane + m * WAVE;
@@ -1258,7 +1539,7 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_partial_m(int32_t groups, int32
     }
 }
 
-template <int M>
+template <int M, bool CX = false>
 __global__ __launch_bounds__(BLOCK) void k_heavy_combine_m(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
                                                            DevGraph G, State st, HeavyPlan hp, Partial pp, Flags fl) {
     if (*fl.prev_changed == 0) return;
@@ -1285,7 +1566,9 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_combine_m(int32_t groups, int32
             for (int32_t sgi = hp.heavy_seg0[h]; sgi < hp.heavy_seg0[h + 1]; ++sgi) {
                 const size_t o = ((size_t)g * hp.nseg + sgi) * L + j;
                 const int2 uk = pp.uk[o];
-                if (uk.x >= 0) offer<L>(b, G, st, g, n, j, uk.y, uk.x, pp.du[o], pp.alt[o]);
+                if (uk.x < 0) continue;
+                if constexpr (CX) offer_x<L>(b, G, st, g, n, j, uk.y, uk.x, pp.du[o], pp.alt[o]);
+                else offer<L>(b, G, st, g, n, j, uk.y, uk.x, pp.du[o], pp.alt[o]);
             }
             changed |= finish_vertex<L>(b, G, st, g, n, j, v, s, rv, d_old);
         }
@@ -1457,9 +1740,36 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
             x.dc = INF;
             if (x.b >= 0 && x.s >= 0 && x.si.t != x.s) {
                 const int32_t g = (x.b * WAVE + lane) / L, j = (x.b * WAVE + lane) % L;
-                const size_t rt = sidx<L>(g, n, x.si.c, j);
-                x.dc = st.D[rt];
-                x.rc = st.RT[rt];
+                if (x.si.c >= 0) {
+                    const size_t rt = sidx<L>(g, n, x.si.c, j);
+                    x.dc = st.D[rt];
+                    x.rc = st.RT[rt];
+                } else {   // a contracted target: the best of its three neighbours (d, then d[u], then u)
+                    const int32_t r = -2 - x.si.c;
+                    const int32_t u0 = G.rnb[3 * r], u1 = G.rnb[3 * r + 1], u2 = G.rnb[3 * r + 2];
+                    const double d0 = st.D[sidx<L>(g, n, u0, j)], d1 = st.D[sidx<L>(g, n, u1, j)],
+                                 d2 = st.D[sidx<L>(g, n, u2, j)];
+                    const double a0 = d0 + G.rw[3 * r], a1 = d1 + G.rw[3 * r + 1], a2 = d2 + G.rw[3 * r + 2];
+                    int32_t q = d0 < INF ? 0 : -1;
+                    double bd = d0 < INF ? a0 : INF, bu = d0;
+                    if (d1 < INF && (a1 < bd || (a1 == bd && d1 < bu))) {
+                        q = 1;
+                        bd = a1;
+                        bu = d1;
+                    }
+                    if (d2 < INF && (a2 < bd || (a2 == bd && d2 < bu))) {
+                        q = 2;
+                        bd = a2;
+                        bu = d2;
+                    }
+                    if (q >= 0) {
+                        const Route rc = st.RT[sidx<L>(g, n, G.rnb[3 * r + q], j)];
+                        x.dc = bd;
+                        x.rc.r = rc.r * G.ra[3 * r + q];
+                        x.rc.h = rc.h + 1;
+                        x.rc.f = (rc.h == 0) ? x.si.t : rc.f;   // the neighbour is the source itself
+                    }
+                }
             }
         }
 #pragma unroll
@@ -2792,6 +3102,8 @@ struct spe_graph {
     DevGraph dev{};
     HeavyPlan hp{};
     const uint8_t* d_heavy = nullptr;
+    DevGraph devx{};               // degree-3 contracted relaxation graph (hg.cx.active), batch engine
+    HeavyPlan hpx{};
     std::vector<void*> allocs;
 };
 
@@ -2814,6 +3126,12 @@ struct spe_table {
     static constexpr bool lds_debug = false;
 #endif
     int32_t occ = 0;               // waves/SIMD the relaxation kernel is held to (0 = compiler's choice)
+    // the batch engine's relaxation graph: the core, or its degree-3 contraction (cx)
+    bool cx = false;
+    const DevGraph* bG = nullptr;
+    const HeavyPlan* bhp = nullptr;
+    int32_t bn = 0;                // relaxation vertices (state rows per lane group)
+    int32_t bm = 0;                // relaxation in-entries
     RowMode md{};
     bool ext = false;
     bool built = false;              // every owned block holds its rows
@@ -2979,6 +3297,7 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
         g->key = f.h;
     }
     spe::prune_pendants(&g->hg, desc->keep_pendants == 0);
+    spe::contract_degree3(&g->hg);
     r = graph_upload(g);
     if (r) {
         spe_graph_free(g);
@@ -3117,6 +3436,93 @@ static int graph_upload(spe_graph* g) {
         if (r) return r;
     }
 #undef UP
+    if (h.cx.active) {   // the batch engine's contracted relaxation graph (shares the rest of dev)
+        const spe::HostGraph::Contracted& cx = h.cx;
+        DevGraph& x = g->devx;
+        x = d;
+        x.n = cx.nk;
+        x.nrel = (int32_t)cx.col.size();
+        x.ipair = nullptr;
+        x.iaux = x.fiaux = nullptr;
+#define UPX(field, src)                                  \
+    do {                                                 \
+        r = dev_upload(g->allocs, src, &x.field);        \
+        if (r) return r;                                 \
+    } while (0)
+        UPX(iptr, cx.ptr);
+        UPX(icol, cx.col);
+        UPX(iw, cx.w1);
+        UPX(ia, cx.a1);
+        UPX(orev, cx.rev);
+        UPX(xw2, cx.w2);
+        UPX(xa2, cx.a2);
+        UPX(xkey, cx.key);
+        UPX(xvia, cx.via);
+        UPX(rnb, cx.rnb);
+        UPX(rw, cx.rw);
+        UPX(ra, cx.ra);
+        x.iwrep = x.iw;   // (contraction needs no multigraph representatives)
+        x.optr = x.iptr;
+        x.ocol = x.icol;
+        x.owrep = x.iw;
+        x.oarep = x.ia;
+        x.ow = x.iw;
+        {
+            std::vector<int32_t> irow(cx.col.size()), cid(h.n, -1), anc(h.n, -1), rm(h.n, -1);
+            for (int32_t v = 0; v < cx.nk; ++v)
+                for (int32_t k = cx.ptr[v]; k < cx.ptr[v + 1]; ++k) irow[k] = v;
+            std::vector<int32_t> corev(cx.nk);
+            for (int32_t k = 0; k < cx.nk; ++k) corev[k] = h.corev[cx.kcore[k]];
+            for (int32_t v = 0; v < h.n; ++v) {
+                const int32_t c = h.core_id[v];
+                if (c >= 0) {
+                    cid[v] = cx.kid[c];
+                    rm[v] = cx.rid[c];
+                } else if (h.anchor_core[v] >= 0) {
+                    anc[v] = cx.kid[h.anchor_core[v]];   // (no removed vertex anchors a pendant)
+                }
+            }
+            UPX(irow, irow);
+            UPX(corev, corev);
+            UPX(core_id, cid);
+            UPX(anchor_core, anc);
+            UPX(xrm, rm);
+        }
+#undef UPX
+        std::vector<uint8_t> heavy(cx.nk, 0);
+        std::vector<int32_t> seg_vertex, seg_begin, heavy_vertex, heavy_seg0;
+        for (int32_t v = 0; v < cx.nk; ++v) {
+            const int32_t k0 = cx.ptr[v], k1 = cx.ptr[v + 1];
+            if (k1 - k0 <= WAVE) continue;
+            heavy[v] = 1;
+            heavy_vertex.push_back(v);
+            heavy_seg0.push_back((int32_t)seg_vertex.size());
+            for (int32_t k = k0; k < k1; k += WAVE) {
+                seg_vertex.push_back(v);
+                seg_begin.push_back(k);
+            }
+        }
+        heavy_seg0.push_back((int32_t)seg_vertex.size());
+        g->hpx.nseg = (int32_t)seg_vertex.size();
+        g->hpx.nheavy = (int32_t)heavy_vertex.size();
+        if ((r = dev_upload(g->allocs, seg_vertex, &g->hpx.seg_vertex))) return r;
+        if ((r = dev_upload(g->allocs, seg_begin, &g->hpx.seg_begin))) return r;
+        if ((r = dev_upload(g->allocs, heavy_vertex, &g->hpx.heavy_vertex))) return r;
+        if ((r = dev_upload(g->allocs, heavy_seg0, &g->hpx.heavy_seg0))) return r;
+        if ((r = dev_upload(g->allocs, heavy, &x.heavy))) return r;
+        std::vector<uint8_t> oheavy(cx.col.size());
+        for (size_t k = 0; k < cx.col.size(); ++k) oheavy[k] = heavy[cx.col[k]];
+        if ((r = dev_upload(g->allocs, oheavy, &x.oheavy))) return r;
+        // bit 31: the target of the reverse entry is heavy; bit 30: a shortcut entry
+        std::vector<int4> pack(std::max<size_t>(1, cx.col.size()));
+        for (size_t k = 0; k < cx.col.size(); ++k) {
+            uint64_t wb;
+            std::memcpy(&wb, &cx.w1[k], sizeof wb);
+            const int32_t rev = cx.rev[k] | (cx.via[k] >= 0 ? 0x40000000 : 0) | (heavy[cx.col[k]] ? (int32_t)0x80000000 : 0);
+            pack[k] = make_int4(cx.col[k], rev, (int32_t)(uint32_t)wb, (int32_t)(uint32_t)(wb >> 32));
+        }
+        if ((r = dev_upload(g->allocs, pack, &x.ipack))) return r;
+    }
     if (!g->aux_edge.empty()) {   // the auxiliary attribute, if set (spe_graph_set_edge_aux)
         std::vector<double> ia(h.ieid.size()), fa(h.fieid.size());
         for (size_t k = 0; k < ia.size(); ++k) ia[k] = g->aux_edge[h.ieid[k]];
@@ -3504,6 +3910,15 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         delete t;
         return fail(SPE_EUNSUPPORTED, "relaxation shape (rows_in_flight, waves_per_simd) not built");
     }
+    // degree-3 contraction: the LDS-ring batch relaxation of SSSP rows,
+    // without the compat modes that walk parent edges (owner replay, aux fold)
+    t->cx = g->hg.cx.active && !o.no_contract && t->engine == SPE_ENGINE_BATCH && !t->md.complete &&
+            t->lanes == 128 && t->relax_kernel == SPE_RELAX_LDS_RING && t->infl == RELAX_RING_NS && t->occ == 7 &&
+            t->delta == 0.0 && !o.owner_rank && !o.want_aux;
+    t->bG = t->cx ? &g->devx : &g->dev;
+    t->bhp = t->cx ? &g->hpx : &g->hp;
+    t->bn = t->cx ? g->hg.cx.nk : g->hg.nc;
+    t->bm = t->cx ? (int32_t)g->hg.cx.col.size() : (int32_t)g->hg.icol.size();
     t->trace = o.trace != 0;
     t->tb.A = n_attached;
     const size_t elems = (size_t)(t->blk1 - t->blk0) * n_attached * WAVE;
@@ -3561,6 +3976,9 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
                 x.pw = h.fiw[x.kt];
                 x.pa = h.fia[x.kt];
             }
+            // contracted tables: kept ids; a removed target reads its three neighbours
+            // (c = -2 - removed index)
+            if (t->cx) x.c = h.cx.kid[x.c] >= 0 ? h.cx.kid[x.c] : -2 - h.cx.rid[x.c];
         }
         const SlotInfo* tsi = nullptr;
         TRY(dev_upload(t->allocs, si, &tsi));
@@ -3580,7 +3998,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     const size_t GL = t->lanes <= WAVE ? G * (WAVE / t->lanes) : (G * WAVE + t->lanes - 1) / t->lanes;
     const size_t GW = GL * (size_t)t->lanes;   // source entries per batch (>= G * 64: padding lanes)
     if (!t->md.complete && t->engine == SPE_ENGINE_BATCH) {
-        const size_t se = GW * n;
+        const size_t se = GW * (size_t)t->bn;
         t->overlap = o.no_overlap == 0;
         for (int i = 0; i < (t->overlap ? 2 : 1); ++i) {
             TRY(dev_alloc(t->allocs, &t->st_buf[i].D, se));
@@ -3588,26 +4006,26 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
             TRY(dev_alloc(t->allocs, &t->st_buf[i].RT, se));
         }
         t->st = t->st_buf[0];
-        const size_t nrel = std::max<size_t>(1, g->hg.icol.size());
+        const size_t nrel = std::max<size_t>(1, (size_t)t->bm);
         TRY(dev_alloc(t->allocs, &t->inflag[0], GL * nrel));
         TRY(dev_alloc(t->allocs, &t->inflag[1], GL * nrel));
-        TRY(dev_alloc(t->allocs, &t->mark[0], (GL * n + 8) & ~(size_t)7));
-        TRY(dev_alloc(t->allocs, &t->mark[1], (GL * n + 8) & ~(size_t)7));
-        TRY(dev_alloc(t->allocs, &t->hmark[0], GL * n));
-        TRY(dev_alloc(t->allocs, &t->hmark[1], GL * n));
-        const size_t pe = GW * std::max<size_t>(1, (size_t)g->hp.nseg);
+        TRY(dev_alloc(t->allocs, &t->mark[0], (GL * t->bn + 8) & ~(size_t)7));
+        TRY(dev_alloc(t->allocs, &t->mark[1], (GL * t->bn + 8) & ~(size_t)7));
+        TRY(dev_alloc(t->allocs, &t->hmark[0], GL * t->bn));
+        TRY(dev_alloc(t->allocs, &t->hmark[1], GL * t->bn));
+        const size_t pe = GW * std::max<size_t>(1, (size_t)t->bhp->nseg);
         TRY(dev_alloc(t->allocs, &t->pp.alt, pe));
         TRY(dev_alloc(t->allocs, &t->pp.du, pe));
         TRY(dev_alloc(t->allocs, &t->pp.uk, pe));
-        t->max_iters = 4 * n + 64;
+        t->max_iters = 4 * t->bn + 64;
         TRY(dev_alloc(t->allocs, &t->counts, (size_t)t->max_iters + 2));
         if (t->delta > 0.0) {
-            t->max_iters = 64 * n + 4096;   // buckets add rounds
+            t->max_iters = 64 * t->bn + 4096;   // buckets add rounds
             TRY(dev_alloc(t->allocs, &t->counts, (size_t)t->max_iters + 2));
             TRY(dev_alloc(t->allocs, &t->ds.bound, GL));
             TRY(dev_alloc(t->allocs, &t->ds.minrej, GL));
             TRY(dev_alloc(t->allocs, &t->ds.gchanged, GL));
-            TRY(dev_alloc(t->allocs, &t->ds.pending, GL * n));
+            TRY(dev_alloc(t->allocs, &t->ds.pending, GL * t->bn));
         }
     }
     if (!t->md.complete && t->engine == SPE_ENGINE_FW) {
@@ -3777,14 +4195,16 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     static_assert(!RING || (L == 2 * WAVE && !DELTA), "the LDS-ring kernel runs 128-lane rows, no Delta schedule");
     constexpr int M = L > WAVE ? L / WAVE : 1;    // lanes per thread
     const spe_graph* g = t->g;
-    const int32_t n = g->hg.nc;
-    const int32_t nrel = (int32_t)g->hg.icol.size();
+    const int32_t n = t->bn;      // the batch engine's relaxation graph (core or contracted)
+    const int32_t nrel = t->bm;
+    const DevGraph& G = *t->bG;
+    const HeavyPlan& HP = *t->bhp;
     const int32_t groups = M > 1 ? (blocks + M - 1) / M : blocks * (WAVE / L);    // lane groups
     const int64_t total = (int64_t)groups * n;
     // one resident wave per hardware slot (no second wave of late blocks), multiple of 8 (XCD split)
     int per_cu = 0, cus = 0;
     const void* kfn;
-    if constexpr (RING) kfn = (const void*)k_relax_s<INFL, OCC>;
+    if constexpr (RING) kfn = t->cx ? (const void*)k_relax_s<INFL, OCC, true> : (const void*)k_relax_s<INFL, OCC>;
     else if constexpr (M > 1) kfn = (const void*)k_relax_m<M, INFL, OCC, DELTA>;
     else kfn = (const void*)k_relax<L, INFL, OCC, DELTA>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, BLOCK, 0) != hipSuccess || per_cu < 1)
@@ -3801,7 +4221,7 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
     {
         LaunchTimer lt(t, s, SPE_K_INIT);
         const dim3 ig(grid_for((int64_t)n * L, BLOCK, std::max(8, 16384 / std::max(1, (int)groups))), groups);
-        k_init_state<L><<<ig, BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev.vfac, g->dev, t->st);
+        k_init_state<L><<<ig, BLOCK, 0, s>>>(n, groups, t->d_srcv, G.vfac, G, t->st);
     }
     if constexpr (DELTA) {
         HIP_TRY(hipMemsetAsync(t->ds.pending, 0x7F, sizeof(double) * (size_t)total, s));   // 1.4e306: none
@@ -3811,7 +4231,7 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
         LaunchTimer lt(t, s, SPE_K_SEED);
         // the sources "changed in round 0": their out-edges form round 1's frontier
         // (Delta: heavy vertices stay in the light frontier, relaxed by the same kernel)
-        k_seed<L><<<(groups * L + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(n, groups, t->d_srcv, g->dev, t->mark[1],
+        k_seed<L><<<(int)(((int64_t)groups * L * WAVE + BLOCK - 1) / BLOCK), BLOCK, 0, s>>>(n, groups, t->d_srcv, G, t->mark[1],
                                                                      DELTA ? t->mark[1] : t->hmark[1], t->inflag[1]);
     }
     const int64_t subs_per_wave = M > 1 ? 1 : WAVE / L;
@@ -3829,32 +4249,43 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
             if constexpr (DELTA) fl.hmark_next = fl.mark_next;   // heavy rows relaxed by k_relax too
             {
                 LaunchTimer lt(t, s, SPE_K_RELAX);
-                if constexpr (RING)
-                    k_relax_s<INFL, OCC><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev, t->st, fl);
+                if constexpr (RING) {
+                    if (t->cx)
+                        k_relax_s<INFL, OCC, true><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, G, t->st, fl);
+                    else
+                        k_relax_s<INFL, OCC><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, G, t->st, fl);
+                }
                 else if constexpr (M > 1)
-                    k_relax_m<M, INFL, OCC, DELTA><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev,
+                    k_relax_m<M, INFL, OCC, DELTA><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, G,
                                                                                 t->st, fl, t->ds);
                 else
-                    k_relax<L, INFL, OCC, DELTA><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, g->dev,
+                    k_relax<L, INFL, OCC, DELTA><<<relax_grid, BLOCK, 0, s>>>((int32_t)total, n, t->d_srcc, G,
                                                                               t->st, fl, t->ds);
             }
             if constexpr (DELTA) {
-                k_delta_advance<<<groups, BLOCK, 0, s>>>(n, nrel, t->delta, g->dev, t->ds, fl.mark_next, fl.in_next,
+                k_delta_advance<<<groups, BLOCK, 0, s>>>(n, nrel, t->delta, G, t->ds, fl.mark_next, fl.in_next,
                                                          t->counts + it);
-            } else if (g->hp.nheavy > 0) {
+            } else if (HP.nheavy > 0) {
                 LaunchTimer lt(t, s, SPE_K_HEAVY);
-                const int64_t pw = ((int64_t)groups * g->hp.nseg + subs_per_wave - 1) / subs_per_wave;
-                const int64_t cw = ((int64_t)groups * g->hp.nheavy + subs_per_wave - 1) / subs_per_wave;
+                const int64_t pw = ((int64_t)groups * HP.nseg + subs_per_wave - 1) / subs_per_wave;
+                const int64_t cw = ((int64_t)groups * HP.nheavy + subs_per_wave - 1) / subs_per_wave;
                 if constexpr (M > 1) {
-                    k_heavy_partial_m<M, INFL><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
-                        groups, n, t->d_srcc, g->dev, t->st, g->hp, t->pp, fl);
-                    k_heavy_combine_m<M><<<grid_for(cw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
-                        groups, n, t->d_srcc, g->dev, t->st, g->hp, t->pp, fl);
+                    if (t->cx) {
+                        k_heavy_partial_m<M, INFL, true><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
+                            groups, n, t->d_srcc, G, t->st, HP, t->pp, fl);
+                        k_heavy_combine_m<M, true><<<grid_for(cw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
+                            groups, n, t->d_srcc, G, t->st, HP, t->pp, fl);
+                    } else {
+                        k_heavy_partial_m<M, INFL><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
+                            groups, n, t->d_srcc, G, t->st, HP, t->pp, fl);
+                        k_heavy_combine_m<M><<<grid_for(cw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
+                            groups, n, t->d_srcc, G, t->st, HP, t->pp, fl);
+                    }
                 } else {
-                    k_heavy_partial<L><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcc, g->dev,
-                                                                                          t->st, g->hp, t->pp, fl);
-                    k_heavy_combine<L><<<grid_for(cw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcc, g->dev,
-                                                                                          t->st, g->hp, t->pp, fl);
+                    k_heavy_partial<L><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcc, G,
+                                                                                          t->st, HP, t->pp, fl);
+                    k_heavy_combine<L><<<grid_for(cw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(groups, n, t->d_srcc, G,
+                                                                                          t->st, HP, t->pp, fl);
                 }
             }
         }
@@ -3888,15 +4319,14 @@ static int relax_to_convergence(spe_table* t, int32_t blocks, hipStream_t s) {
 }
 
 static void launch_rows_sssp(spe_table* t, int grid, int32_t blocks, int32_t sb0, hipStream_t s) {
-    const spe_graph* g = t->g;
 #define ROWS(LL)                                                                                              \
     do {                                                                                                      \
         if (t->tb.aux)                                                                                        \
-            k_rows_sssp<LL, true><<<grid, BLOCK, 0, s>>>(g->hg.nc, blocks, sb0, t->d_srcv, t->d_slots, g->dev, \
+            k_rows_sssp<LL, true><<<grid, BLOCK, 0, s>>>(t->bn, blocks, sb0, t->d_srcv, t->d_slots, *t->bG,   \
                                                          t->md, t->st, t->tb);                                \
         else                                                                                                  \
-            k_rows_sssp<LL, false><<<grid, BLOCK, 0, s>>>(g->hg.nc, blocks, sb0, t->d_srcv, t->d_slots,       \
-                                                          g->dev, t->md, t->st, t->tb);                       \
+            k_rows_sssp<LL, false><<<grid, BLOCK, 0, s>>>(t->bn, blocks, sb0, t->d_srcv, t->d_slots,          \
+                                                          *t->bG, t->md, t->st, t->tb);                       \
     } while (0)
     switch (t->lanes) {
         case 128: ROWS(128); break;
@@ -3989,7 +4419,9 @@ static int build_blocks_impl(spe_table* t, int32_t block_begin, int32_t block_en
                 const int32_t slot = (b + gi) * WAVE + l;
                 const int32_t v = (gi < groups && slot < t->A) ? t->attached[slot] : -1;
                 t->h_srcv[gi * WAVE + l] = v;
-                t->h_srcv[(pb + gi) * WAVE + l] = v < 0 ? -1 : (g->hg.core_id[v] >= 0 ? g->hg.core_id[v] : -2);
+                int32_t c = v < 0 ? -1 : (g->hg.core_id[v] >= 0 ? g->hg.core_id[v] : -2);
+                if (t->cx && c >= 0) c = g->hg.cx.kid[c] >= 0 ? g->hg.cx.kid[c] : -2;   // (a contracted source: -2)
+                t->h_srcv[(pb + gi) * WAVE + l] = c;
             }
         HIP_TRY(hipMemcpyAsync(t->d_srcv, t->h_srcv, sizeof(int32_t) * pb * WAVE, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(t->d_srcc, t->h_srcv + pb * WAVE, sizeof(int32_t) * pb * WAVE,
@@ -4135,6 +4567,7 @@ int spe_table_layout_get(const spe_table* t, spe_table_layout* out) {
     out->engine = t->engine;
     out->lanes_per_group = t->lanes;
     out->relax_kernel = t->relax_kernel;
+    out->contracted_vertices = t->cx ? t->bn : 0;
     return SPE_OK;
 }
 
@@ -4482,6 +4915,53 @@ int spe_table_source_tree(spe_table* t, int32_t s_slot, int32_t* parent) {
     }
     if (sbuf) (void)hipFree(sbuf);
     if (rc) return rc;
+    if (t->engine != SPE_ENGINE_LDS && t->cx) {
+        // the contracted graph: kept rows carry entries of the contracted CSR (a shortcut
+        // entry's parent is its x); a removed vertex's parent is the best of its three
+        // neighbours, the rows kernel's rule
+        const spe::HostGraph::Contracted& cx = h.cx;
+        const int32_t nk = cx.nk, L = t->lanes, j = s_slot % WAVE;
+        const int32_t g = L <= WAVE ? j / L : 0, lane = L <= WAVE ? j % L : j;
+        std::vector<int32_t> kp((size_t)std::max(1, nk));
+        std::vector<double> kd((size_t)std::max(1, nk));
+        const size_t off = ((size_t)g * nk) * (size_t)L + (size_t)lane;
+        HIP_TRY(hipMemcpy2D(kp.data(), sizeof(int32_t), t->st_buf[0].P + off, sizeof(int32_t) * (size_t)L,
+                            sizeof(int32_t), (size_t)nk, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy2D(kd.data(), sizeof(double), t->st_buf[0].D + off, sizeof(double) * (size_t)L,
+                            sizeof(double), (size_t)nk, hipMemcpyDeviceToHost));
+        std::fill(parent, parent + h.n, -1);
+        auto orig = [&](int32_t kv) { return h.corev[(size_t)cx.kcore[(size_t)kv]]; };
+        for (int32_t v = 0; v < nk; ++v) {
+            const int32_t k = kp[(size_t)v];
+            if (k >= 0) parent[orig(v)] = cx.via[(size_t)k] >= 0 ? cx.via[(size_t)k] : orig(cx.col[(size_t)k]);
+            else if (k == -2) parent[orig(v)] = s;   // the source's first edge (pendant or contracted source)
+        }
+        for (size_t r = 0; r < cx.rcore.size(); ++r) {
+            const int32_t x = h.corev[(size_t)cx.rcore[r]];
+            if (x == s) continue;
+            int32_t bq = -1;
+            double bd = INF, bdu = INF;
+            for (int q = 0; q < 3; ++q) {
+                const double du = kd[(size_t)cx.rnb[3 * r + q]];
+                if (!(du < INF)) continue;
+                const double alt = du + cx.rw[3 * r + q];
+                if (bq < 0 || alt < bd || (alt == bd && du < bdu)) {
+                    bq = q;
+                    bd = alt;
+                    bdu = du;
+                }
+            }
+            if (bq >= 0) parent[x] = orig(cx.rnb[3 * r + bq]);
+        }
+        if (h.pruned)
+            for (int32_t v = 0; v < h.n; ++v) {
+                if (h.core_id[(size_t)v] >= 0 || v == s) continue;
+                const int32_t a = h.anchor_core[(size_t)v];   // (never a removed vertex)
+                if (a >= 0 && kd[(size_t)cx.kid[(size_t)a]] < INF) parent[v] = h.corev[(size_t)a];
+            }
+        parent[s] = -1;
+        return SPE_OK;
+    }
     if (t->engine != SPE_ENGINE_LDS) {
         const int32_t L = t->lanes, j = s_slot % WAVE;
         const int32_t g = L <= WAVE ? j / L : 0, lane = L <= WAVE ? j % L : j;

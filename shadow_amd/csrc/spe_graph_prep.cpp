@@ -288,4 +288,96 @@ void prune_pendants(HostGraph* hg, bool enable) {
         }
 }
 
+void contract_degree3(HostGraph* hg) {
+    HostGraph::Contracted& cx = hg->cx;
+    cx = HostGraph::Contracted{};
+    if (hg->directed || hg->multi_rep) return;
+    for (double f : hg->vfac)
+        if (has_attr(f) && f != 1.0) return;   // the rows' path-order re-fold walks plain entries only
+    const int32_t nc = hg->nc;
+    if (nc < 8) return;
+    std::vector<int32_t> pendants(nc, 0);
+    for (int32_t v = 0; v < hg->n; ++v)
+        if (hg->anchor_core[v] >= 0) pendants[hg->anchor_core[v]]++;
+    cx.kid.assign(nc, 0);
+    cx.rid.assign(nc, -1);
+    std::vector<uint8_t> blocked(nc, 0);
+    for (int32_t x = 0; x < nc; ++x) {   // greedy independent set in core order
+        if (blocked[x] || pendants[x] || hg->iptr[x + 1] - hg->iptr[x] != 3) continue;
+        bool ok = true;
+        for (int32_t k = hg->iptr[x]; k < hg->iptr[x + 1]; ++k) ok &= hg->icol[k] != x;
+        if (!ok) continue;
+        cx.rid[x] = (int32_t)cx.rcore.size();
+        cx.rcore.push_back(x);
+        blocked[x] = 1;
+        for (int32_t k = hg->iptr[x]; k < hg->iptr[x + 1]; ++k) blocked[hg->icol[k]] = 1;
+    }
+    // worth it only where it removes a good share of the rows: the contracted build
+    // pays a few extra loads per visit and longer hub lists (C4's core, whose
+    // degree-3 vertices nearly all anchor pendants, keeps 2 of 20k: not contracted)
+    if (cx.rcore.empty() || (int64_t)cx.rcore.size() * 10 < (int64_t)nc) {
+        cx = HostGraph::Contracted{};
+        return;
+    }
+    for (int32_t c = 0; c < nc; ++c) {
+        cx.kid[c] = cx.rid[c] >= 0 ? -1 : (int32_t)cx.kcore.size();
+        if (cx.rid[c] < 0) cx.kcore.push_back(c);
+    }
+    cx.nk = (int32_t)cx.kcore.size();
+    for (int32_t x : cx.rcore)
+        for (int32_t k = hg->iptr[x]; k < hg->iptr[x + 1]; ++k) {   // neighbours in core order = kept order
+            cx.rnb.push_back(cx.kid[hg->icol[k]]);
+            cx.rw.push_back(hg->iw[k]);
+            cx.ra.push_back(hg->ia[k]);
+        }
+    // in-CSR over kept vertices
+    auto find = [&](int32_t list_of, int32_t nb) {   // entry of nb in list_of's core list
+        const int32_t* b = hg->icol.data() + hg->iptr[list_of];
+        const int32_t* e = hg->icol.data() + hg->iptr[list_of + 1];
+        return (int32_t)(std::lower_bound(b, e, nb) - hg->icol.data());
+    };
+    cx.ptr.assign(1, 0);
+    for (int32_t kv = 0; kv < cx.nk; ++kv) {
+        const int32_t v = cx.kcore[kv];
+        for (int32_t k = hg->iptr[v]; k < hg->iptr[v + 1]; ++k) {
+            const int32_t u = hg->icol[k];
+            if (cx.rid[u] < 0) {   // plain edge u -> v
+                cx.col.push_back(cx.kid[u]);
+                cx.w1.push_back(hg->iw[k]);
+                cx.w2.push_back(0.0);
+                cx.a1.push_back(hg->ia[k]);
+                cx.a2.push_back(1.0);
+                cx.key.push_back(u);
+                cx.via.push_back(-1);
+            } else {               // u = x removed: a -> v via x for x's other neighbours a
+                for (int32_t q = hg->iptr[u]; q < hg->iptr[u + 1]; ++q) {
+                    const int32_t a = hg->icol[q];
+                    if (a == v) continue;
+                    const int32_t kax = find(u, a);   // edge a -> x is the entry of a in x's list
+                    cx.col.push_back(cx.kid[a]);
+                    cx.w1.push_back(hg->iw[kax]);
+                    cx.w2.push_back(hg->iw[k]);       // x -> v: the entry of x in v's list
+                    cx.a1.push_back(hg->ia[kax]);
+                    cx.a2.push_back(hg->ia[k]);
+                    cx.key.push_back(u);
+                    cx.via.push_back(hg->corev[u]);
+                }
+            }
+        }
+        cx.ptr.push_back((int32_t)cx.col.size());
+    }
+    // reverse entries: (a -> v via x) <-> (v -> a via x)
+    cx.rev.assign(cx.col.size(), -1);
+    for (int32_t kv = 0; kv < cx.nk; ++kv)
+        for (int32_t k = cx.ptr[kv]; k < cx.ptr[kv + 1]; ++k) {
+            const int32_t a = cx.col[k];
+            for (int32_t q = cx.ptr[a]; q < cx.ptr[a + 1]; ++q)
+                if (cx.col[q] == kv && cx.via[q] == cx.via[k]) {
+                    cx.rev[k] = q;
+                    break;
+                }
+        }
+    cx.active = true;
+}
+
 }  // namespace spe

@@ -49,6 +49,28 @@ struct HostGraph {
     std::vector<double> loop_w, loop_a;       // get_eid(v,v) self-loop, NaN when none
     std::vector<double> self_w2, self_a2;     // SELF rule: 2*min latency, r*r
     std::vector<int32_t> self_other;          // other endpoint of the SELF edge, -1 none
+
+    // Degree-3 contraction for the batch engine (contract_degree3): an independent
+    // set of relaxation vertices x with exactly three neighbours (no pendant anchored
+    // at x) is taken out of the batch engine's relaxation graph; each x is replaced by
+    // "shortcut" entries a -> b via x between its neighbours, offering the two-add
+    // path fold fl(fl(d[a] + w(a,x)) + w(x,b)), and x's rows are derived from its
+    // three neighbours' rows.  The kept vertices keep their relative (core) order.
+    struct Contracted {
+        bool active = false;
+        int32_t nk = 0;                    // kept relaxation vertices
+        std::vector<int32_t> kid;          // [nc] kept id of a core vertex, -1 = removed
+        std::vector<int32_t> kcore;        // [nk] core id of a kept vertex
+        std::vector<int32_t> rid;          // [nc] removed index of a core vertex, -1 = kept
+        std::vector<int32_t> rcore;        // [nr] core id of a removed vertex
+        std::vector<int32_t> rnb;          // [3 nr] kept ids of its neighbours (increasing)
+        std::vector<double> rw, ra;        // [3 nr] relaxation latency / 1 - p of the edge (nb, x)
+        // in-CSR over kept ids: entry k of v = a -> v, plain or via a removed x
+        std::vector<int32_t> ptr, col, rev;
+        std::vector<double> w1, w2, a1, a2;   // plain: (w, 0, a, 1); shortcut: (w(a,x), w(x,v), a(a,x), a(x,v))
+        std::vector<int32_t> key;          // core id of the entry's parent (x for a shortcut, a for a plain edge)
+        std::vector<int32_t> via;          // original id of x, -1 for a plain edge
+    } cx;
 };
 
 int prepare_graph(const spe_graph_desc* d, HostGraph* hg, std::string* err);
@@ -102,5 +124,8 @@ int fw_pivot_rows(const FwPart& p, int32_t kb, int32_t rb0, int32_t rb1);  // co
 // Restrict the relaxation CSR to the core (no-op for directed graphs or when
 // `enable` is false); keeps the full CSR in hg->f*.
 void prune_pendants(HostGraph* hg, bool enable);
+// Build hg->cx when the graph qualifies (undirected, no multigraph latency
+// representatives, no vertex factor other than 1 / absent, some eligible vertex).
+void contract_degree3(HostGraph* hg);
 
 }  // namespace spe

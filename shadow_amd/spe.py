@@ -30,7 +30,7 @@ WAVE = 64
 # Test / experiment hooks of this mirror (libspe itself reads no environment):
 #   SPE_ENGINE=1|2|3   engine for tables that leave it AUTO (falls back to batch when
 #                      the graph does not fit the asked engine)
-#   SPE_LANES=64|128, SPE_RELAX=1|2, SPE_INFL=<rows per trip>, SPE_OCC=<waves/SIMD>,
+#   SPE_LANES=64|128, SPE_RELAX=1|2, SPE_INFL=<rows per trip>, SPE_OCC=<waves/SIMD>, SPE_NO_CONTRACT=1,
 #   SPE_DELTA=<ms>, SPE_NO_OVERLAP=1, SPE_TRACE=1   batch-engine tuning (spe_table_opts)
 #   SPE_NO_PRUNE=1     graphs keep their pendant vertices (spe_graph_desc.keep_pendants)
 
@@ -69,7 +69,7 @@ class TableOpts(C.Structure):
                 ("gather", C.c_int32), ("relax_kernel", C.c_int32), ("rows_in_flight", C.c_int32),
                 ("waves_per_simd", C.c_int32), ("no_overlap", C.c_int32), ("delta_ms", C.c_double),
                 ("trace", C.c_int32), ("shared_fraction", C.c_double), ("gather_gbps", C.c_double),
-                ("build_seconds_hint", C.c_double)]
+                ("build_seconds_hint", C.c_double), ("no_contract", C.c_int32)]
 
 
 class TableLayout(C.Structure):
@@ -77,7 +77,7 @@ class TableLayout(C.Structure):
                 ("elems", C.c_int64), ("latrel", C.c_void_p),
                 ("next_hop", C.c_void_p), ("hops", C.c_void_p), ("groups_per_launch", C.c_int32),
                 ("engine", C.c_int32), ("n_devices", C.c_int32), ("device", C.c_int32),
-                ("lanes_per_group", C.c_int32), ("relax_kernel", C.c_int32)]
+                ("lanes_per_group", C.c_int32), ("relax_kernel", C.c_int32), ("contracted_vertices", C.c_int32)]
 
 
 class Entry(C.Structure):
@@ -290,7 +290,8 @@ class PathTable:
                  owner_order=None, engine: int = 0, want_aux: bool = False, devices=None,
                  gather: int = SPE_GATHER_AUTO, relax_kernel: int = 0, rows_in_flight: int = 0,
                  waves_per_simd: int = 0, no_overlap: Optional[bool] = None, delta_ms: Optional[float] = None,
-                 shared_fraction: float = 0.0, gather_gbps: float = 0.0, build_seconds_hint: float = 0.0):
+                 shared_fraction: float = 0.0, gather_gbps: float = 0.0, build_seconds_hint: float = 0.0,
+                 no_contract: Optional[bool] = None):
         self.graph = graph
         self.attached = np.ascontiguousarray(attached, np.int32)
         self.A = int(self.attached.shape[0])
@@ -307,6 +308,7 @@ class PathTable:
         o.no_overlap = int(bool(no_overlap if no_overlap is not None else _env_int("SPE_NO_OVERLAP")))
         o.delta_ms = float(delta_ms if delta_ms is not None else (os.environ.get("SPE_DELTA") or 0.0))
         o.trace = _env_int("SPE_TRACE")
+        o.no_contract = int(bool(no_contract if no_contract is not None else _env_int("SPE_NO_CONTRACT")))
         env_engine = engine == SPE_ENGINE_AUTO and not want_aux and _env_int("SPE_ENGINE") != 0
         if env_engine:
             o.engine = _env_int("SPE_ENGINE")

@@ -20,7 +20,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#ifndef L
 #define L 128
+#endif
 
 typedef struct {
     int64_t rounds, visits, lane_updates;
@@ -33,10 +35,14 @@ typedef struct {
 } sim_out;
 
 typedef struct {
-    uint64_t m[2];
+    uint64_t m[L / 64];
 } mask128;
 
-static int popc128(const mask128* a) { return __builtin_popcountll(a->m[0]) + __builtin_popcountll(a->m[1]); }
+static int popc128(const mask128* a) {
+    int c = 0;
+    for (int i = 0; i < L / 64; ++i) c += __builtin_popcountll(a->m[i]);
+    return c;
+}
 static int lines_of(const mask128* a, int per_line) { /* lines of a row touched by the lanes in a */
     int c = 0;
     for (int l0 = 0; l0 < L; l0 += per_line) {
@@ -115,19 +121,19 @@ int sim_run(int32_t n, const int32_t* ptr, const int32_t* col, const double* w, 
             if (!mark[cur][v]) continue;
             mark[cur][v] = 0;
             out->visits++;
-            mask128 ch = {{0, 0}}, offered = {{0, 0}};
+            mask128 ch = {{0}}, offered = {{0}};
             int32_t prow[L];
             for (int k = ptr[v]; k < ptr[v + 1]; ++k) {
                 if (!fl[cur][k]) continue;
                 fl[cur][k] = 0;
                 const int u = col[k];
                 if (mode != 1) {
-                    out->nbr_lines += 8;
+                    out->nbr_lines += L / 16;
                     out->nbr_reads++;
                     {   /* summary tests (conservative): line j of u can be skipped when
                          * fl(min over the line's lanes of d_u + w) > max over them of d_v */
-                        double mn16[8], mx16[8];
-                        for (int j = 0; j < 8; ++j) {
+                        double mn16[L / 16], mx16[L / 16];
+                        for (int j = 0; j < L / 16; ++j) {
                             mn16[j] = INFINITY;
                             mx16[j] = -INFINITY;
                         }
@@ -137,17 +143,17 @@ int sim_run(int32_t n, const int32_t* ptr, const int32_t* col, const double* w, 
                             if (src[l] != v && dv > mx16[l / 16]) mx16[l / 16] = dv;
                         }
                         int all = 1;
-                        for (int j = 0; j < 8; ++j) {
+                        for (int j = 0; j < L / 16; ++j) {
                             const int sk = mn16[j] + w[k] > mx16[j];
                             out->prune_line16 += sk;
                             all &= sk;
                         }
-                        for (int j = 0; j < 4; ++j) {
+                        for (int j = 0; j < L / 32; ++j) {
                             const double mn = fmin(mn16[2 * j], mn16[2 * j + 1]);
                             const double mx = fmax(mx16[2 * j], mx16[2 * j + 1]);
                             out->prune_line32 += 2 * (mn + w[k] > mx);
                         }
-                        out->prune_row += 8 * all;
+                        out->prune_row += (L / 16) * all;
                     }
                     for (int l = 0; l < L; ++l) {
                         if (src[l] == v) continue;
@@ -175,7 +181,7 @@ int sim_run(int32_t n, const int32_t* ptr, const int32_t* col, const double* w, 
                     }
                 }
             }
-            out->own_lines += (mode != 1) ? 8 : lines_of(&offered, 16);
+            out->own_lines += (mode != 1) ? L / 16 : lines_of(&offered, 16);
             const int c = popc128(&ch);
             out->lane_updates += c;
             if (mode == 0) {
@@ -199,7 +205,7 @@ int sim_run(int32_t n, const int32_t* ptr, const int32_t* col, const double* w, 
             }
         }
         if (mode == 1)   /* records of the round before last are dead: clear for reuse */
-            for (int v = 0; v < n; ++v) rec[nx][v].m[0] = rec[nx][v].m[1] = 0;
+            for (int v = 0; v < n; ++v) memset(&rec[nx][v], 0, sizeof(mask128));
         out->rounds++;
         cur ^= 1;
         if (!any) break;
@@ -251,7 +257,7 @@ int sim_run(int32_t n, const int32_t* ptr, const int32_t* col, const double* w, 
             out->tree_rounds++;
             for (int v = 0; v < n; ++v) {
                 if (!tm[v]) continue;
-                mask128 pend = {{0, 0}}, now = {{0, 0}};
+                mask128 pend = {{0}}, now = {{0}};
                 int32_t prow[L];
                 for (int l = 0; l < L; ++l) {
                     size_t i = (size_t)v * L + l;
