@@ -468,7 +468,10 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
     if gather and frac < 0:   # auto: measure T1 and B on this job, then plan
         calib = calibrate_split(t, lr, blk_elems, nblk, world, rank, dev, dist, pad_blocks)
         frac = sd.shared_fraction(world, calib[0], nblk * blk_elems * 16.0, calib[1])
-    sizes, S = sd.split_schedule(nblk, shares, gpl, max(0.0, frac) if gather else 1.0)
+    # one GPU with shared anchor trees: the whole table is one build call,
+    # so the library batches by anchor roots (its state holds `gpl` blocks of roots)
+    sched_gpl = nblk if (world == 1 and not emulated and t.layout()["shared_sources"]) else gpl
+    sizes, S = sd.split_schedule(nblk, shares, sched_gpl, max(0.0, frac) if gather else 1.0)
     slots, nslot = sd.rank_next_hop_slots(nblk, shares, args.share_index if emulated else rank, sizes, S)
     # next hop (i32) and hop count (u16) of this rank's own blocks only, packed
     nx = torch.empty(max(1, nslot) * blk_elems, dtype=torch.int32, device=dev)
@@ -483,12 +486,16 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
         return t.build_blocks_into(b0, b1, lr[b0 * blk_elems:].data_ptr(), nx_base + s0 * blk_elems * 4,
                                    hp_base + s0 * blk_elems * 2)
 
+    lanes_run = [0]   # relaxation lanes (sources, or shared anchor roots) of this rank's builds
+
     def one_table():
         works, tb, tg, its = [], 0.0, 0.0, 0
         for k, off, gk, b0, b1 in mine:
             t0 = time.perf_counter()
             if b1 > b0:
-                its += into(b0, b1)["iterations"]
+                st = into(b0, b1)
+                its += st["iterations"]
+                lanes_run[0] += st["relaxed_lanes"]
             tb += time.perf_counter() - t0
             if gather:   # overlaps the next round's build and the local part (RCCL runs on its own stream)
                 w = sd.allgather_span(lr, off, gk, world, rank, blk_elems, dist, async_op=True)
@@ -496,7 +503,9 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
                     works.append(w)
         if l1 > l0 and not emulated:   # built by every rank itself: no exchange
             t0 = time.perf_counter()
-            its += into(l0, l1)["iterations"]
+            st = into(l0, l1)
+            its += st["iterations"]
+            lanes_run[0] += st["relaxed_lanes"]
             tb += time.perf_counter() - t0
         t1 = time.perf_counter()
         for w in works:
@@ -520,6 +529,7 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
     steps = args.steps if args.steps > 0 else 3
     torch.cuda.synchronize(dev)
     barrier()
+    lanes_run[0] = 0
     t0 = time.perf_counter()
     tb_sum = tg_sum = 0.0
     it_total = 0
@@ -563,13 +573,18 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
         rl = kp["lds" if lds else ("direct" if direct else "relax")]
         relax_s = rl["ms"] / 1e3
         done = built * steps   # this rank's sources (the profile is this rank's launches)
-        ach = b_relax * done / relax_s / 1e9 if relax_s > 0 else 0.0
+        # the relaxation's own units: one lane per source, or per shared anchor root
+        #  -- the bytes the kernel is priced on are per relaxed lane
+        relaxed = lanes_run[0] if (not lds and not direct and lanes_run[0] > 0) else done
+        ach = b_relax * relaxed / relax_s / 1e9 if relax_s > 0 else 0.0
         roof = {"bound": "hbm", "kernel": kname + (" (SSSP + rows, LDS-resident state)" if lds else
                                                    (" (DIRECT rows)" if direct else " (SSSP stage)")),
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(args, kname, config), "launches": rl["launches"],
                 "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
                 "algorithmic_bytes_per_source": b_relax,
+                "relaxed_lanes_per_step": round(relaxed / steps),
+                "shared_anchor_trees": bool(lay.get("shared_sources", 0)),
                 "lanes_per_group": lay["lanes_per_group"],
                 "bytes_basis": "relaxation graph: 12 m_relax + 28 n_relax + 8 (SURVEY 8d B_s minus the row stage)"}
         rw = kp["rows"]

@@ -164,6 +164,14 @@ typedef struct spe_table_opts {
     /* 1: the batch engine relaxes the graph itself instead of its degree-3 contraction
      * (same rows; the contraction is the default where it applies) */
     int32_t no_contract;
+    /* 1: every pruned pendant source relaxes on its own lane, so its latencies are the
+     * path-order sums bit for bit.  Default 0: pendant sources sharing an anchor take
+     * the anchor's relaxation, their rows the anchor's with the pendant edge folded in
+     * front -- routes (next hop, hops, routability) identical, latency / reliability
+     * within a few ulps (the north star's 1e-9 relative), exact where every weight is
+     * integer-valued.  A source whose anchor's parent decisions are
+     * within rounding of a tie is rebuilt on its own lane. */
+    int32_t exact_sources;
 } spe_table_opts;
 
 #define SPE_RELAX_AUTO 0            /* the default below */
@@ -212,6 +220,8 @@ typedef struct spe_table_layout {
     int32_t relax_kernel;           /* batch engine: the SPE_RELAX_* kernel it runs */
     int32_t contracted_vertices;    /* batch engine on the degree-3 contraction: its relaxation
                                      * vertices (0: the table relaxes the graph itself) */
+    int32_t shared_sources;         /* 1: pendant sources take their anchor's relaxation
+                                     * (spe_table_opts.exact_sources) */
 } spe_table_layout;
 
 typedef struct spe_entry {
@@ -232,6 +242,9 @@ typedef struct spe_build_stats {
     int32_t shared_blocks;          /* multi-device: blocks sharded and gathered (the rest built on every device) */
     int32_t local_blocks;
     double build_wait_seconds;      /* multi-device: slowest device's build time (shares + local part) */
+    int64_t relaxed_lanes;          /* batch engine: relaxation lanes (sources, or shared anchor
+                                     * roots) the last build ran, padding excluded */
+    int32_t fallback_blocks;        /* shared anchor trees: source blocks rebuilt lane per source */
 } spe_build_stats;
 
 const char* spe_last_error(void);

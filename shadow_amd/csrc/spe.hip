@@ -1692,11 +1692,21 @@ __device__ double aux_fold(const DevGraph& G, const State& st, int32_t g, int32_
 #ifndef ROWS_ITEMS
 #define ROWS_ITEMS 2
 #endif
-template <int L, bool AUX>
+// SHARE (shared anchor trees): the state lanes are the batch's roots; rli[b * 64 + l]
+// = {state lane of source b * 64 + l's root, its first hop (the anchor) or -1 for a
+// core source} and rwa[.] = {pendant edge latency w, f_s * (1 - p)}: a pruned pendant
+// source's row is its anchor's with the edge folded in front (latency w + d,
+// reliability (f_s a) r, one more hop, first hop the anchor).
+#ifndef SPE_ROWS_CACHE
+#define SPE_ROWS_CACHE 1
+#endif
+template <int L, bool AUX, bool SHARE = false>
 __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, int32_t sb0,
                                                      const int32_t* __restrict__ srcv,
                                                      const SlotInfo* __restrict__ slots, DevGraph G,
-                                                     RowMode md, State st, Table tb) {
+                                                     RowMode md, State st, Table tb,
+                                                     const int2* __restrict__ rli = nullptr,
+                                                     const double2* __restrict__ rwa = nullptr) {
     const int32_t lane = threadIdx.x & (WAVE - 1);
     const int64_t items_all = (int64_t)blocks * tb.A;
     // XCD-contiguous slices (grid a multiple of 8; workgroups are dealt round-robin
@@ -1718,8 +1728,13 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
         SlotInfo si;
         double dc;
         Route rc;
+        int2 ri;       // SHARE: (root's state lane, first hop of a pendant source or -1)
     };
     constexpr int NI = ROWS_ITEMS;
+    // SHARE: a wave's items walk the targets of one source block for long stretches,
+    // so the block's per-lane source constants are loaded once per block
+    int32_t cb = -1, cs = -1;
+    int2 cri = make_int2(0, -1);
     for (int64_t it0 = lo + wave0; it0 < items; it0 += NI * nwaves) {
         In in[NI];
 #pragma unroll
@@ -1731,7 +1746,18 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
                 x.b = (int32_t)(it / tb.A);
                 x.jt = (int32_t)(it - (int64_t)x.b * tb.A);
                 x.si = slots[x.jt];
-                x.s = srcv[x.b * WAVE + lane];
+                if constexpr (SHARE && SPE_ROWS_CACHE) {
+                    if (x.b != cb) {   // (wave-uniform)
+                        cb = x.b;
+                        cs = srcv[x.b * WAVE + lane];
+                        cri = rli[x.b * WAVE + lane];
+                    }
+                    x.s = cs;
+                    x.ri = cri;
+                } else {
+                    x.s = srcv[x.b * WAVE + lane];
+                    if constexpr (SHARE) x.ri = rli[x.b * WAVE + lane];
+                }
             }
         }
 #pragma unroll
@@ -1739,7 +1765,8 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
             In& x = in[q];
             x.dc = INF;
             if (x.b >= 0 && x.s >= 0 && x.si.t != x.s) {
-                const int32_t g = (x.b * WAVE + lane) / L, j = (x.b * WAVE + lane) % L;
+                const int32_t sl = SHARE ? x.ri.x : x.b * WAVE + lane;   // state lane
+                const int32_t g = sl / L, j = sl % L;
                 if (x.si.c >= 0) {
                     const size_t rt = sidx<L>(g, n, x.si.c, j);
                     x.dc = st.D[rt];
@@ -1770,6 +1797,15 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
                         x.rc.f = (rc.h == 0) ? x.si.t : rc.f;   // the neighbour is the source itself
                     }
                 }
+                if constexpr (SHARE) {
+                    if (x.ri.y >= 0 && x.dc < INF) {   // a pruned pendant source: s -> anchor, then the root's path
+                        const double2 wa = rwa[x.b * WAVE + lane];
+                        x.dc = wa.x + x.dc;
+                        x.rc.r = wa.y * x.rc.r;
+                        x.rc.h = x.rc.h + 1;
+                        x.rc.f = x.ri.y;
+                    }
+                }
             }
         }
 #pragma unroll
@@ -1779,7 +1815,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
             const int32_t b = x.b, jt = x.jt, s = x.s;
             const SlotInfo& si = x.si;
             const int32_t t = si.t;
-            const int32_t g = (b * WAVE + lane) / L, j = (b * WAVE + lane) % L;
+            const int32_t g = (b * WAVE + lane) / L, j = (b * WAVE + lane) % L;   // (!SHARE: the re-fold walks)
             double Lt = -1.0, R = -1.0, AX = -1.0;
             int32_t N = -1, H = 0, PV = -1;
             if (s >= 0) {
@@ -1872,6 +1908,91 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
     }
 }
 
+
+// Shared anchor trees: after a batch's relaxation over its roots, flag every root
+// some of whose parent decisions a source offset could change.  A source s with
+// offset o (its pendant edge, o <= omax) sums every path in the same order as its
+// root but from o instead of 0; along a path of h edges each sum is within
+// h u (o + d) of o + the exact sum (u = 2^-53), so a vertex whose parent's offer
+// beats every other in-entry's offer alt by more than 4.5 H u (omax + alt) -- H
+// bounding the edge count, alt / wmin + 3 -- keeps that parent, without a
+// tie-break, for every such source; then every source's tree is the root's (DESIGN
+// §4.1).  The test is per entry (alt - d - bound(alt) grows with alt, so the
+// smallest competing offer fails it first), so in-lists split freely: one wave per
+// (lane group, light vertex) or (lane group, 64-entry segment of a heavy vertex),
+// four neighbour rows per round trip.
+template <int L>
+__global__ __launch_bounds__(BLOCK) void k_share_check(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
+                                                       DevGraph G, State st, HeavyPlan hp, double wmin, double omax,
+                                                       double hmax, uint8_t* __restrict__ unsafe) {
+    constexpr int M = L > WAVE ? L / WAVE : 1;
+    static_assert(L >= WAVE, "one lane group per wave");
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int64_t nw = ((int64_t)gridDim.x * BLOCK) >> 6;
+    const int64_t light = (int64_t)groups * n;
+    const int64_t items = light + (int64_t)groups * hp.nseg;
+    for (int64_t it = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it < items; it += nw) {   // wave-uniform
+        int32_t g, v, k0, k1;
+        if (it < light) {
+            g = (int32_t)(it / n);
+            v = (int32_t)(it - (int64_t)g * n);
+            k0 = G.iptr[v];
+            k1 = G.iptr[v + 1];
+            if (k1 - k0 > WAVE) continue;   // heavy: its segments below
+        } else {
+            const int64_t q = it - light;
+            g = (int32_t)(q / hp.nseg);
+            const int32_t sg = (int32_t)(q - (int64_t)g * hp.nseg);
+            v = hp.seg_vertex[sg];
+            k0 = hp.seg_begin[sg];
+            k1 = min(k0 + WAVE, G.iptr[v + 1]);
+        }
+        double d[M];
+        int32_t pk[M];
+        bool act[M], any = false, bad[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const int32_t j = lane + m * WAVE;
+            const size_t i = sidx<L>(g, n, v, j);
+            d[m] = st.D[i];
+            pk[m] = st.P[i];
+            act[m] = srcv[g * L + j] >= 0 && d[m] < INF && pk[m] != -1;   // (-1: the root itself)
+            bad[m] = false;
+            any |= act[m];
+        }
+        if (!__ballot(any)) continue;
+        const int32_t k = k0 + lane;
+        const bool ok = k < k1;
+        const int4 pkk = ok ? G.ipack[k] : make_int4(0, 0, 0, 0);
+        const double w_j = __hiloint2double(pkk.w, pkk.z);
+        const double w2_j = (G.xw2 && ok) ? G.xw2[k] : 0.0;
+        const int32_t cnt = k1 - k0;
+        for (int32_t q = 0; q < cnt; q += 4) {
+            double du[4][M];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int32_t u = __builtin_amdgcn_readlane(pkk.x, min(q + r, cnt - 1));
+#pragma unroll
+                for (int m = 0; m < M; ++m) du[r][m] = st.D[sidx<L>(g, n, u, lane + m * WAVE)];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (q + r >= cnt) break;
+                const double w = sub_get_d<WAVE>(w_j, q + r), w2 = sub_get_d<WAVE>(w2_j, q + r);
+#pragma unroll
+                for (int m = 0; m < M; ++m) {
+                    const double alt = (du[r][m] + w) + w2;   // the relaxation's fold (+ 0.0: one add)
+                    if (!act[m] || k0 + q + r == pk[m] || !(alt < INF)) continue;
+                    const double h = wmin > 0.0 ? fmin(hmax, alt / wmin + 3.0) : hmax;
+                    bad[m] |= alt - d[m] <= 4.5 * h * 0x1p-53 * (omax + alt);
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+            if (bad[m]) unsafe[(size_t)g * L + lane + m * WAVE] = 1;
+    }
+}
 
 __global__ __launch_bounds__(BLOCK) void k_rows_direct(int32_t groups, int32_t sb0,
                                                        const int32_t* __restrict__ srcv,
@@ -3191,6 +3312,16 @@ struct spe_table {
     // experimental Delta-stepping schedule of the batch engine (SPE_DELTA=<ms> at creation)
     double delta = 0.0;
     DeltaState ds{};
+    // shared anchor trees (batch engine): relaxation lanes = the batch's
+    // roots; rows per source through rlane
+    bool share = false;
+    bool share_off = false;        // this build runs one lane per source (fallback, source trees)
+    int32_t* rsrc_buf[2] = {nullptr, nullptr};    // per source slot of the batch: original id (-1 pad)
+    int2* rli_buf[2] = {nullptr, nullptr};        // per source slot: {root's state lane, first hop / -1}
+    double2* rwa_buf[2] = {nullptr, nullptr};     // per source slot: {pendant latency, f_s (1 - p)}
+    unsigned char* h_rows = nullptr;   // pinned staging for the three (owned blocks x 64 x 28 B)
+    uint8_t* d_unsafe = nullptr;   // per root lane: k_share_check's flag
+    uint8_t* h_unsafe = nullptr;
 };
 
 namespace {
@@ -3298,6 +3429,7 @@ int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out
     }
     spe::prune_pendants(&g->hg, desc->keep_pendants == 0);
     spe::contract_degree3(&g->hg);
+    spe::share_prep(&g->hg);
     r = graph_upload(g);
     if (r) {
         spe_graph_free(g);
@@ -3776,6 +3908,8 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         f.val(has_owner);
         const int32_t aux = o.want_aux != 0;
         f.val(aux);
+        const int32_t exact_src = o.exact_sources != 0;   // shared anchor trees change the last bits
+        f.val(exact_src);
         if (has_owner) f.add(o.owner_rank, (size_t)n_attached * sizeof(int32_t));
         t->key = f.h;
     }
@@ -3919,6 +4053,15 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     t->bhp = t->cx ? &g->hpx : &g->hp;
     t->bn = t->cx ? g->hg.cx.nk : g->hg.nc;
     t->bm = t->cx ? (int32_t)g->hg.cx.col.size() : (int32_t)g->hg.icol.size();
+    // shared anchor trees: pendant sources relax as their anchor
+    t->share = !o.exact_sources && g->hg.share.eligible && t->engine == SPE_ENGINE_BATCH && !t->md.complete &&
+               !o.owner_rank && !o.want_aux && t->delta == 0.0;
+    if (t->share) {
+        bool any = false;
+        for (int32_t i = t->blk0 * WAVE; i < std::min(n_attached, t->blk1 * WAVE) && !any; ++i)
+            any = g->hg.core_id[(size_t)attached[i]] < 0;
+        t->share = any;
+    }
     t->trace = o.trace != 0;
     t->tb.A = n_attached;
     const size_t elems = (size_t)(t->blk1 - t->blk0) * n_attached * WAVE;
@@ -4047,6 +4190,15 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     t->d_srcv = t->srcv_buf[0];
     t->d_srcc = t->srcc_buf[0];
     TRY(dev_alloc(t->allocs, &t->d_min, 1));
+    const size_t owned_slots = (size_t)std::max(1, t->blk1 - t->blk0) * WAVE;
+    if (t->share) {
+        for (int i = 0; i < (t->overlap ? 2 : 1); ++i) {
+            TRY(dev_alloc(t->allocs, &t->rsrc_buf[i], owned_slots));
+            TRY(dev_alloc(t->allocs, &t->rli_buf[i], owned_slots));
+            TRY(dev_alloc(t->allocs, &t->rwa_buf[i], owned_slots));
+        }
+        TRY(dev_alloc(t->allocs, &t->d_unsafe, GW));
+    }
 #undef TRY
     // every failure from here on releases what was allocated (spe_table_free)
 #define HTRY(expr)                                                                         \
@@ -4058,6 +4210,11 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         }                                                                                  \
     } while (0)
     HTRY(hipHostMalloc((void**)&t->h_srcv, 2 * GW * sizeof(int32_t), hipHostMallocDefault));
+    if (t->share) {
+        HTRY(hipHostMalloc((void**)&t->h_rows, owned_slots * (sizeof(double2) + sizeof(int2) + sizeof(int32_t)),
+                           hipHostMallocDefault));
+        HTRY(hipHostMalloc((void**)&t->h_unsafe, GW, hipHostMallocDefault));
+    }
     HTRY(hipHostMalloc((void**)&t->h_counts, std::max<size_t>(64, (size_t)t->max_iters + 2) * sizeof(int32_t),
                        hipHostMallocDefault));
     HTRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
@@ -4334,6 +4491,15 @@ static void launch_rows_sssp(spe_table* t, int grid, int32_t blocks, int32_t sb0
     }
 #undef ROWS
 }
+static void launch_rows_shared(spe_table* t, int grid, int32_t blocks, int32_t sb0, hipStream_t s,
+                               const int32_t* rsrc, const int2* rli, const double2* rwa) {
+    if (t->lanes == 128)
+        k_rows_sssp<128, false, true><<<grid, BLOCK, 0, s>>>(t->bn, blocks, sb0, rsrc, t->d_slots, *t->bG, t->md,
+                                                              t->st, t->tb, rli, rwa);
+    else
+        k_rows_sssp<64, false, true><<<grid, BLOCK, 0, s>>>(t->bn, blocks, sb0, rsrc, t->d_slots, *t->bG, t->md,
+                                                             t->st, t->tb, rli, rwa);
+}
 }  // extern "C++"
 
 int spe_table_build(spe_table* t, void* stream) {
@@ -4388,6 +4554,214 @@ int spe_table_build_blocks_into(spe_table* t, int32_t block_begin, int32_t block
     return r;   // the table's own storage is untouched: nothing is marked built
 }
 
+// Shared anchor trees: a batch's relaxation lanes are its ROOTS --
+// each core source, and the anchor of each pruned pendant source, once -- and the
+// rows kernel gives every source its root's row (a pendant source's with its edge
+// in front).  Batches are cut at block boundaries into about equal root counts (two
+// at least with the rows / relaxation overlap, so one batch's rows hide under the
+// next one's relaxation).  Where the weights' sums are not exact, k_share_check
+// flags roots whose decisions an offset could change, and the blocks of their
+// sources are rebuilt with one lane per source.
+static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hipStream_t s, hipStream_t rs,
+                        bool ovl) {
+    const spe_graph* g = t->g;
+    const spe::HostGraph& h = g->hg;
+    const int32_t L = t->lanes;
+    const int32_t cap = t->groups * WAVE;   // root lanes one batch's state holds
+    auto root_of = [&](int32_t slot) -> int32_t {
+        const int32_t v = t->attached[(size_t)slot];
+        return h.core_id[(size_t)v] >= 0 ? h.core_id[(size_t)v] : h.anchor_core[(size_t)v];
+    };
+    std::vector<int32_t> tag((size_t)std::max(1, h.nc), -1), lane_of((size_t)std::max(1, h.nc), -1);
+    int32_t total = 0;
+    for (int32_t i = block_begin * WAVE; i < std::min(t->A, block_end * WAVE); ++i) {
+        const int32_t c = root_of(i);
+        if (c >= 0 && tag[(size_t)c] < 0) {
+            tag[(size_t)c] = 0;
+            ++total;
+        }
+    }
+    // (two batches only when each still fills 8 lane groups: smaller relaxations run near-empty rounds)
+    const int32_t nb = std::max((total + cap - 1) / cap, (ovl && total >= 16 * L) ? 2 : 1);
+    const int32_t target = (total + nb - 1) / nb;
+    std::fill(tag.begin(), tag.end(), -1);
+    std::vector<int32_t> roots, deferred;
+    std::vector<uint8_t> bad((size_t)std::max(1, h.nc), 0);
+    const spe::HostGraph::Share& sh = h.share;
+    int buf = 0;
+    for (int32_t b = block_begin, bid = 0; b < block_end; ++bid) {
+        HIP_TRY(hipStreamSynchronize(s));   // the pinned staging is reused per batch
+        roots.clear();
+        int32_t e = b;
+        while (e < block_end) {
+            const size_t before = roots.size();
+            for (int32_t l = 0; l < WAVE; ++l) {
+                const int32_t slot = e * WAVE + l;
+                if (slot >= t->A) break;
+                const int32_t c = root_of(slot);
+                if (c >= 0 && tag[(size_t)c] != bid) {
+                    tag[(size_t)c] = bid;
+                    lane_of[(size_t)c] = (int32_t)roots.size();
+                    roots.push_back(c);
+                }
+            }
+            // this block starts the next batch (the last planned batch takes the rest up to `cap`)
+            if (e > b && (int32_t)roots.size() > (bid + 1 >= nb ? cap : std::min(target, cap))) {
+                for (size_t i = before; i < roots.size(); ++i) tag[(size_t)roots[i]] = -1;
+                roots.resize(before);
+                break;
+            }
+            ++e;
+        }
+        const int32_t R = (int32_t)roots.size();
+        const int32_t nblk = e - b;
+        if (ovl) {
+            t->st = t->st_buf[buf];
+            t->d_srcv = t->srcv_buf[buf];
+            t->d_srcc = t->srcc_buf[buf];
+            if (t->rows_pending[buf]) HIP_TRY(hipStreamWaitEvent(s, t->ev_rows[buf], 0));
+        }
+        // relaxation lanes: the roots (core sources of the batch engine's state)
+        const int32_t bpg = std::max(1, L / WAVE);
+        const int32_t rb = std::max(1, (R + WAVE - 1) / WAVE);
+        const int32_t pb = (rb + bpg - 1) / bpg * bpg;
+        for (int32_t i = 0; i < pb * WAVE; ++i) {
+            const int32_t c = i < R ? roots[(size_t)i] : -1;
+            t->h_srcv[i] = c < 0 ? -1 : h.corev[(size_t)c];
+            int32_t cc = c;
+            if (t->cx && c >= 0) cc = h.cx.kid[(size_t)c] >= 0 ? h.cx.kid[(size_t)c] : -2;
+            t->h_srcv[pb * WAVE + i] = cc;
+        }
+        // rows: every source slot of blocks [b, e), its root's lane and pendant prefix
+        const size_t ns = (size_t)nblk * WAVE;
+        double2* hw = reinterpret_cast<double2*>(t->h_rows);
+        int2* hl = reinterpret_cast<int2*>(hw + ns);
+        int32_t* hr = reinterpret_cast<int32_t*>(hl + ns);
+        for (int32_t i = 0; i < nblk * WAVE; ++i) {
+            const int32_t slot = b * WAVE + i;
+            const int32_t c = slot < t->A ? root_of(slot) : -1;
+            const int32_t v = c >= 0 ? t->attached[(size_t)slot] : -1;
+            hr[i] = v;
+            hl[i] = make_int2(c >= 0 ? lane_of[(size_t)c] : -1, -1);
+            hw[i] = make_double2(0.0, 1.0);
+            if (v >= 0 && h.core_id[(size_t)v] < 0) {   // pendant: the edge s -> anchor in front
+                const int32_t kx = h.fiptr[(size_t)v];
+                const double fs = h.vfac[(size_t)v];
+                hl[i].y = h.corev[(size_t)h.anchor_core[(size_t)v]];
+                hw[i] = make_double2(h.fiw[(size_t)kx], (std::isnan(fs) ? 1.0 : 1.0 * fs) * h.fia[(size_t)kx]);
+            }
+        }
+        int32_t* d_rsrc = t->rsrc_buf[ovl ? buf : 0];
+        int2* d_rli = t->rli_buf[ovl ? buf : 0];
+        double2* d_rwa = t->rwa_buf[ovl ? buf : 0];
+        HIP_TRY(hipMemcpyAsync(t->d_srcv, t->h_srcv, sizeof(int32_t) * pb * WAVE, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(t->d_srcc, t->h_srcv + pb * WAVE, sizeof(int32_t) * pb * WAVE, hipMemcpyHostToDevice,
+                               s));
+        HIP_TRY(hipMemcpyAsync(d_rsrc, hr, sizeof(int32_t) * ns, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_rli, hl, sizeof(int2) * ns, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_rwa, hw, sizeof(double2) * ns, hipMemcpyHostToDevice, s));
+        int r = relax_to_convergence(t, rb, s);
+        if (r) return r;
+        t->stats.relaxed_lanes += R;
+        if (!sh.exact) {
+            const int32_t groups = L > WAVE ? pb / bpg : pb * (WAVE / L);
+            HIP_TRY(hipMemsetAsync(t->d_unsafe, 0, (size_t)groups * L, s));
+            {
+                LaunchTimer lt(t, s, SPE_K_HEAVY);   // (accounted with the heavy-vertex passes)
+                const int grid = grid_for((int64_t)groups * (t->bn + t->bhp->nseg) * WAVE, BLOCK, 8192);
+                const double hmax = (double)h.n + 2.0;
+                if (L == 128)
+                    k_share_check<128><<<grid, BLOCK, 0, s>>>(groups, t->bn, t->d_srcv, *t->bG, t->st, *t->bhp,
+                                                              sh.wmin, sh.omax, hmax, t->d_unsafe);
+                else
+                    k_share_check<64><<<grid, BLOCK, 0, s>>>(groups, t->bn, t->d_srcv, *t->bG, t->st, *t->bhp,
+                                                             sh.wmin, sh.omax, hmax, t->d_unsafe);
+            }
+            HIP_TRY(hipMemcpyAsync(t->h_unsafe, t->d_unsafe, (size_t)R, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            bool any = false;
+            for (int32_t i = 0; i < R; ++i)
+                if (t->h_unsafe[i]) {
+                    bad[(size_t)roots[(size_t)i]] = 1;
+                    any = true;
+                }
+            if (any)
+                for (int32_t blk = b; blk < e; ++blk)
+                    for (int32_t l = 0; l < WAVE; ++l) {
+                        const int32_t slot = blk * WAVE + l;
+                        if (slot < t->A && root_of(slot) >= 0 && bad[(size_t)root_of(slot)]) {
+                            deferred.push_back(blk);
+                            break;
+                        }
+                    }
+        }
+        if (ovl) {
+            HIP_TRY(hipEventRecord(t->ev_relaxed, s));
+            HIP_TRY(hipStreamWaitEvent(rs, t->ev_relaxed, 0));
+        }
+        const int32_t sb0 = b - t->row_base;
+#ifndef SPE_SHARED_ROWS_GRID
+#define SPE_SHARED_ROWS_GRID 8192
+#endif
+        const int row_grid = grid_for((int64_t)nblk * t->A * WAVE, BLOCK, SPE_SHARED_ROWS_GRID);
+        {
+            LaunchTimer lt(t, rs, SPE_K_ROWS);
+            launch_rows_shared(t, row_grid, nblk, sb0, rs, d_rsrc, d_rli, d_rwa);
+        }
+        if (t->md.prefer) {
+            LaunchTimer lt(t, rs, SPE_K_DIRECT);
+            k_direct_overlay<<<(nblk * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, rs>>>(nblk, sb0, d_rsrc, t->d_vertex_slot,
+                                                                                  g->dev, t->tb);
+        }
+        if (ovl) {
+            HIP_TRY(hipEventRecord(t->ev_rows[buf], rs));
+            t->rows_pending[buf] = true;
+            buf ^= 1;
+        }
+        HIP_TRY(hipGetLastError());
+        if (t->prof) {
+            HIP_TRY(hipStreamSynchronize(s));
+            r = resolve_profile(t, !ovl);
+            if (r) return r;
+        }
+        b = e;
+    }
+    if (ovl) {
+        HIP_TRY(hipStreamSynchronize(rs));
+        t->rows_pending[0] = t->rows_pending[1] = false;
+        t->st = t->st_buf[0];
+        t->d_srcv = t->srcv_buf[0];
+        t->d_srcc = t->srcc_buf[0];
+        if (t->prof) {
+            int r = resolve_profile(t);
+            if (r) return r;
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    if (!deferred.empty()) {   // one lane per source for the flagged roots' blocks
+        std::sort(deferred.begin(), deferred.end());
+        deferred.erase(std::unique(deferred.begin(), deferred.end()), deferred.end());
+        spe_build_stats keep = t->stats;
+        t->share_off = true;
+        int r = SPE_OK;
+        for (size_t i = 0; i < deferred.size() && !r;) {
+            size_t j = i + 1;
+            while (j < deferred.size() && deferred[j] == deferred[j - 1] + 1) ++j;
+            r = build_blocks_impl(t, deferred[i], deferred[j - 1] + 1, s);
+            keep.iterations += t->stats.iterations;
+            keep.active_rounds += t->stats.active_rounds;
+            keep.launches += t->stats.launches;
+            keep.relaxed_lanes += t->stats.relaxed_lanes;
+            keep.fallback_blocks += deferred[j - 1] + 1 - deferred[i];
+            i = j;
+        }
+        t->share_off = false;
+        t->stats = keep;
+        if (r) return r;
+    }
+    return SPE_OK;
+}
+
 static int build_blocks_impl(spe_table* t, int32_t block_begin, int32_t block_end, void* stream) {
     HIP_TRY(hipSetDevice(t->g->device));
     if (t->trace)   // where the relaxation state lives (run-to-run placement studies)
@@ -4400,6 +4774,13 @@ static int build_blocks_impl(spe_table* t, int32_t block_begin, int32_t block_en
     t->stats = spe_build_stats{};
     const bool ovl = t->overlap && !t->md.complete && t->engine == SPE_ENGINE_BATCH;
     hipStream_t rs = ovl ? t->rows_stream : s;
+    if (t->share && !t->share_off) {
+        const int r = build_shared(t, block_begin, block_end, s, rs, ovl);
+        if (r) return r;
+        t->stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        t->stats.n_devices = 1;
+        return SPE_OK;
+    }
     int buf = 0;
     for (int32_t b = block_begin; b < block_end; b += t->groups) {
         const int32_t groups = std::min(t->groups, block_end - b);
@@ -4485,6 +4866,7 @@ static int build_blocks_impl(spe_table* t, int32_t block_begin, int32_t block_en
         } else {
             int r = relax_to_convergence(t, groups, s);
             if (r) return r;
+            t->stats.relaxed_lanes += std::max(0, std::min(t->A, (b + groups) * WAVE) - b * WAVE);
             if (ovl) {
                 HIP_TRY(hipEventRecord(t->ev_relaxed, s));
                 HIP_TRY(hipStreamWaitEvent(rs, t->ev_relaxed, 0));
@@ -4568,6 +4950,7 @@ int spe_table_layout_get(const spe_table* t, spe_table_layout* out) {
     out->lanes_per_group = t->lanes;
     out->relax_kernel = t->relax_kernel;
     out->contracted_vertices = t->cx ? t->bn : 0;
+    out->shared_sources = t->share ? 1 : 0;
     return SPE_OK;
 }
 
@@ -4905,9 +5288,12 @@ int spe_table_source_tree(spe_table* t, int32_t s_slot, int32_t* parent) {
         // in place (aux tables): the row just rewritten lacks the DIRECT overlay; rebuild the block
         if (!rc && !scratch && t->md.prefer) rc = spe_table_build_blocks(t, b, b + 1, nullptr);
     } else {
-        // re-run the source's block; its state is left in the first buffer
+        // re-run the source's block, one lane per source (no shared anchor trees); its
+        // state is left in the first buffer
+        t->share_off = true;
         rc = scratch ? spe_table_build_blocks_into(t, b, b + 1, s_lr, s_next, s_hops, nullptr)
                      : spe_table_build_blocks(t, b, b + 1, nullptr);
+        t->share_off = false;
         if (!rc) {
             const hipError_t e = hipStreamSynchronize(t->stream);
             if (e != hipSuccess) rc = fail(SPE_EHIP, hipGetErrorString(e));
@@ -5144,6 +5530,8 @@ void spe_table_free(spe_table* t) {
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     for (void* p : t->allocs) (void)hipFree(p);
     if (t->h_srcv) (void)hipHostFree(t->h_srcv);
+    if (t->h_rows) (void)hipHostFree(t->h_rows);
+    if (t->h_unsafe) (void)hipHostFree(t->h_unsafe);
     if (t->h_counts) (void)hipHostFree(t->h_counts);
     for (hipEvent_t e : t->ev_pool) (void)hipEventDestroy(e);
     if (t->stream) (void)hipStreamDestroy(t->stream);

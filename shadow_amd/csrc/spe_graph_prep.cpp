@@ -380,4 +380,47 @@ void contract_degree3(HostGraph* hg) {
     cx.active = true;
 }
 
+// Constants of the shared anchor trees (HostGraph::Share).  The relaxation sums
+// weights in path order; when every weight is an integer multiple of 2^-q and
+// n * max weight * 2^q < 2^53, every such sum is exact, so a source offset o
+// shifts every offer, distance and tie by exactly o and the anchor's decisions are
+// the source's.  Otherwise the batch engine checks each decision's margin against
+// the rounding the offset can introduce (k_share_check, wmin / omax below).
+void share_prep(HostGraph* hg) {
+    HostGraph::Share& sh = hg->share;
+    sh = HostGraph::Share{};
+    if (!hg->pruned || hg->directed || hg->multi_rep) return;
+    for (double f : hg->vfac)
+        if (!(std::isnan(f) || f == 1.0)) return;
+    std::vector<double> ws(hg->iw.begin(), hg->iw.end());
+    if (hg->cx.active) ws.insert(ws.end(), hg->cx.w2.begin(), hg->cx.w2.end());
+    double omax = 0.0;
+    for (int32_t v = 0; v < hg->n; ++v) {
+        if (hg->core_id[(size_t)v] >= 0 || hg->anchor_core[(size_t)v] < 0) continue;
+        const double w = hg->fiw[(size_t)hg->fiptr[(size_t)v]];
+        omax = std::max(omax, w);
+        ws.push_back(w);
+    }
+    double wmin = INFINITY, wmax = 0.0;
+    for (double w : hg->iw) wmin = std::min(wmin, w);
+    for (double w : ws) {
+        if (!(w >= 0.0) || !std::isfinite(w)) return;   // (weights are validated >= 0 at creation)
+        wmax = std::max(wmax, w);
+    }
+    sh.eligible = true;
+    sh.wmin = std::isfinite(wmin) ? wmin : 0.0;
+    sh.omax = omax;
+    for (int q = 0; q <= 20 && !sh.exact; ++q) {
+        const double sc = std::ldexp(1.0, q);
+        if (!((double)hg->n * (wmax * sc + 1.0) < 0x1p53)) break;
+        bool ok = true;
+        for (double w : ws)
+            if (std::floor(w * sc) != w * sc) {
+                ok = false;
+                break;
+            }
+        sh.exact = ok;
+    }
+}
+
 }  // namespace spe

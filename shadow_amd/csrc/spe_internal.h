@@ -71,6 +71,17 @@ struct HostGraph {
         std::vector<int32_t> key;          // core id of the entry's parent (x for a shortcut, a for a plain edge)
         std::vector<int32_t> via;          // original id of x, -1 for a plain edge
     } cx;
+
+    // Shared anchor trees for the batch engine (share_prep): a pruned
+    // pendant source s reaches every vertex through its anchor c, so its row is c's
+    // row with the prefix s -> c folded in front -- exactly when c's parent decisions
+    // hold for the offset o = w(s, c) too (integer-valued sums, or a margin check).
+    struct Share {
+        bool eligible = false;     // undirected, pruned, no vertex factor other than 1 / absent
+        bool exact = false;        // every weight k / 2^q and every path sum below 2^53: fl sums exact
+        double wmin = 0.0;         // smallest relaxation weight (bounds a path's edge count)
+        double omax = 0.0;         // largest pendant-edge weight (a source's offset)
+    } share;
 };
 
 int prepare_graph(const spe_graph_desc* d, HostGraph* hg, std::string* err);
@@ -127,5 +138,7 @@ void prune_pendants(HostGraph* hg, bool enable);
 // Build hg->cx when the graph qualifies (undirected, no multigraph latency
 // representatives, no vertex factor other than 1 / absent, some eligible vertex).
 void contract_degree3(HostGraph* hg);
+// Fill hg->share (after prune_pendants / contract_degree3).
+void share_prep(HostGraph* hg);
 
 }  // namespace spe

@@ -487,6 +487,8 @@ int multi_build(MultiDev* m, spe_build_stats* stats) {
             s.iterations += q.iterations;
             s.active_rounds += q.active_rounds;
             s.launches += q.launches;
+            s.relaxed_lanes += q.relaxed_lanes;
+            s.fallback_blocks += q.fallback_blocks;
         }
     s.seconds = std::chrono::duration<double>(t2 - t0).count();
     s.gather_seconds = std::chrono::duration<double>(t2 - t1).count();   // gather time not hidden by the builds
@@ -589,6 +591,8 @@ int multi_layout(const MultiDev* m, spe_table_layout* out) {
     out->engine = p.engine;
     out->lanes_per_group = p.lanes_per_group;
     out->relax_kernel = p.relax_kernel;
+    out->contracted_vertices = p.contracted_vertices;
+    out->shared_sources = p.shared_sources;
     out->n_devices = m->n;
     out->device = m->devs[0];
     return SPE_OK;

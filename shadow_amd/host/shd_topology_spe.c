@@ -1062,6 +1062,11 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
      * engine the graph does not fit falls back to the library's choice */
     const char* eng = getenv("SHADOW_SPE_ENGINE");
     if (eng && *eng) o.engine = (int32_t)strtol(eng, NULL, 10);
+    /* SHADOW_SPE_EXACT_SOURCES=1: every pendant host relaxes on its own lane, so its
+     * latencies are the reference's path-order sums bit for bit (default: hosts on
+     * one anchor share its relaxation, latency / reliability within a few ulps) */
+    const char* ex = getenv("SHADOW_SPE_EXACT_SOURCES");
+    if (ex && *ex && strcmp(ex, "0") != 0) o.exact_sources = 1;
     int rc = spe_table_create(top->graph, s->attached, A, &o, &s->table);
     if (rc == SPE_EUNSUPPORTED && o.engine != SPE_ENGINE_AUTO) {
         o.engine = SPE_ENGINE_AUTO;

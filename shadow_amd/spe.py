@@ -31,6 +31,7 @@ WAVE = 64
 #   SPE_ENGINE=1|2|3   engine for tables that leave it AUTO (falls back to batch when
 #                      the graph does not fit the asked engine)
 #   SPE_LANES=64|128, SPE_RELAX=1|2, SPE_INFL=<rows per trip>, SPE_OCC=<waves/SIMD>, SPE_NO_CONTRACT=1,
+#   SPE_EXACT_SOURCES=1 (every pendant source on its own lane: bit-exact path-order latencies),
 #   SPE_DELTA=<ms>, SPE_NO_OVERLAP=1, SPE_TRACE=1   batch-engine tuning (spe_table_opts)
 #   SPE_NO_PRUNE=1     graphs keep their pendant vertices (spe_graph_desc.keep_pendants)
 
@@ -69,7 +70,7 @@ class TableOpts(C.Structure):
                 ("gather", C.c_int32), ("relax_kernel", C.c_int32), ("rows_in_flight", C.c_int32),
                 ("waves_per_simd", C.c_int32), ("no_overlap", C.c_int32), ("delta_ms", C.c_double),
                 ("trace", C.c_int32), ("shared_fraction", C.c_double), ("gather_gbps", C.c_double),
-                ("build_seconds_hint", C.c_double), ("no_contract", C.c_int32)]
+                ("build_seconds_hint", C.c_double), ("no_contract", C.c_int32), ("exact_sources", C.c_int32)]
 
 
 class TableLayout(C.Structure):
@@ -77,7 +78,8 @@ class TableLayout(C.Structure):
                 ("elems", C.c_int64), ("latrel", C.c_void_p),
                 ("next_hop", C.c_void_p), ("hops", C.c_void_p), ("groups_per_launch", C.c_int32),
                 ("engine", C.c_int32), ("n_devices", C.c_int32), ("device", C.c_int32),
-                ("lanes_per_group", C.c_int32), ("relax_kernel", C.c_int32), ("contracted_vertices", C.c_int32)]
+                ("lanes_per_group", C.c_int32), ("relax_kernel", C.c_int32), ("contracted_vertices", C.c_int32),
+                ("shared_sources", C.c_int32)]
 
 
 class Entry(C.Structure):
@@ -103,7 +105,7 @@ class BuildStats(C.Structure):
     _fields_ = [("iterations", C.c_int64), ("active_rounds", C.c_int64), ("launches", C.c_int64),
                 ("seconds", C.c_double), ("gather_seconds", C.c_double), ("n_devices", C.c_int32),
                 ("gather", C.c_int32), ("shared_blocks", C.c_int32), ("local_blocks", C.c_int32),
-                ("build_wait_seconds", C.c_double)]
+                ("build_wait_seconds", C.c_double), ("relaxed_lanes", C.c_int64), ("fallback_blocks", C.c_int32)]
 
 
 # every symbol include/spe.h declares (tests/test_abi.py checks the export table)
@@ -291,7 +293,7 @@ class PathTable:
                  gather: int = SPE_GATHER_AUTO, relax_kernel: int = 0, rows_in_flight: int = 0,
                  waves_per_simd: int = 0, no_overlap: Optional[bool] = None, delta_ms: Optional[float] = None,
                  shared_fraction: float = 0.0, gather_gbps: float = 0.0, build_seconds_hint: float = 0.0,
-                 no_contract: Optional[bool] = None):
+                 no_contract: Optional[bool] = None, exact_sources: Optional[bool] = None):
         self.graph = graph
         self.attached = np.ascontiguousarray(attached, np.int32)
         self.A = int(self.attached.shape[0])
@@ -309,6 +311,7 @@ class PathTable:
         o.delta_ms = float(delta_ms if delta_ms is not None else (os.environ.get("SPE_DELTA") or 0.0))
         o.trace = _env_int("SPE_TRACE")
         o.no_contract = int(bool(no_contract if no_contract is not None else _env_int("SPE_NO_CONTRACT")))
+        o.exact_sources = int(bool(exact_sources if exact_sources is not None else _env_int("SPE_EXACT_SOURCES")))
         env_engine = engine == SPE_ENGINE_AUTO and not want_aux and _env_int("SPE_ENGINE") != 0
         if env_engine:
             o.engine = _env_int("SPE_ENGINE")

@@ -30,10 +30,13 @@ def spe():
     return m
 
 
-def compare_rows(got, ref, label):
+def compare_rows(got, ref, label, rtol=0.0):
     ok = ref["kind"] != 0
     np.testing.assert_array_equal(got["ok"], ok, err_msg=f"{label}: routability")
     for k in ("lat", "rel"):
+        if rtol > 0:   # shared anchor trees: the pendant edge added to the anchor's sum
+            np.testing.assert_allclose(got[k][ok], ref[k][ok], rtol=rtol, atol=0, err_msg=f"{label}: {k}")
+            continue
         bad = np.flatnonzero(got[k][ok] != ref[k][ok])
         assert bad.size == 0, f"{label}: {k} differs at {bad.size} entries"
     np.testing.assert_array_equal(got["hops"][ok], ref["hops"][ok], err_msg=f"{label}: hops")
@@ -64,12 +67,12 @@ def bench_table(spe, top, att):
     return g, t, order
 
 
-def check_sampled_rows(t, top, order, slots, label):
+def check_sampled_rows(t, top, order, slots, label, rtol=0.0):
     ora = Oracle(top).rows(order[slots], order, nthreads=ORACLE_THREADS)
     for i, s in enumerate(slots):
         got = t.download(int(s), int(s) + 1)
         ref = {k: ora[k][i:i + 1] for k in ("lat", "rel", "next", "hops", "kind")}
-        compare_rows(got, ref, f"{label} slot {s}")
+        compare_rows(got, ref, f"{label} slot {s}", rtol=rtol)
         # properties of every routable entry: hops >= 1 and the next hop is an
         # out-neighbour of the source (or the target itself for a direct path)
         assert (got["hops"][got["ok"]] >= 1).all()
@@ -118,18 +121,24 @@ def test_c2_bench_build_lds_engine(spe):
     check_sampled_rows(t, top, order, slots, "C2")
 
 
+@pytest.mark.shared_trees
 def test_c4_one_gpu_full_table_every_launch(spe):
     """C4 (200k tiered, A = 100k stubs): the whole 10^10-pair table (220 GB) built on
-    ONE GPU with the bench settings; two rows of every launch vs the oracle."""
+    ONE GPU with the bench settings -- the library default, so the stubs on one
+    anchor share its relaxation: routes exact, latency / reliability
+    within 1e-12 relative; 16 rows of every 64-block span vs the oracle."""
     top = graphs.gen_tiered()
     att = graphs.tiered_attached(top)
     g, t, order = bench_table(spe, top, att)
     lay = t.layout()
     assert lay["block_begin"] == 0 and lay["block_end"] == t.nblocks
+    assert lay["shared_sources"] == 1
+    st = t.stats()
+    assert st["relaxed_lanes"] < t.A // 4, st   # ~20k anchors for 100k stubs
     slots = launch_sample_slots(t.A, lay["groups_per_launch"], extra_per_launch=14, seed=4)
     nlaunch = -(-t.nblocks // lay["groups_per_launch"])
     assert len(slots) >= 8 * nlaunch
-    check_sampled_rows(t, top, order, slots, "C4")
+    check_sampled_rows(t, top, order, slots, "C4", rtol=1e-12)
     # next hops of stub sources are their (unattached) anchors: no hop rule here
     check_whole_table(t, t.A, "C4", hop_rule=False)
 
