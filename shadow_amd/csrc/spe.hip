@@ -1697,8 +1697,11 @@ __device__ double aux_fold(const DevGraph& G, const State& st, int32_t g, int32_
 // core source} and rwa[.] = {pendant edge latency w, f_s * (1 - p)}: a pruned pendant
 // source's row is its anchor's with the edge folded in front (latency w + d,
 // reliability (f_s a) r, one more hop, first hop the anchor).
-#ifndef SPE_ROWS_CACHE
-#define SPE_ROWS_CACHE 1
+#ifndef SPE_SHARED_ROWS_TILE
+#define SPE_SHARED_ROWS_TILE 8
+#endif
+#ifndef SPE_SHARED_ROWS_PREFETCH
+#define SPE_SHARED_ROWS_PREFETCH 0   // measured slower (89 VGPRs, 5 waves / SIMD)
 #endif
 template <int L, bool AUX, bool SHARE = false>
 __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, int32_t sb0,
@@ -1731,46 +1734,72 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
         int2 ri;       // SHARE: (root's state lane, first hop of a pendant source or -1)
     };
     constexpr int NI = ROWS_ITEMS;
-    // SHARE: a wave's items walk the targets of one source block for long stretches,
-    // so the block's per-lane source constants are loaded once per block
-    int32_t cb = -1, cs = -1;
-    int2 cri = make_int2(0, -1);
-    for (int64_t it0 = lo + wave0; it0 < items; it0 += NI * nwaves) {
-        In in[NI];
+    // SHARE: items run over tiles of BT consecutive source blocks, the blocks fastest:
+    // the ~10 blocks whose sources share one lane group of roots then read a target's
+    // root row from L2 one after the other instead of once per block sweep (each
+    // item still writes one whole 1-KB record segment)
+    constexpr int BT = SHARE ? SPE_SHARED_ROWS_TILE : 1;
+    // SHARE: the next trip's item constants (slot, source, root lane) are requested
+    // before this trip's state gathers, so a trip waits for one memory round trip
+    constexpr bool PF = SHARE && SPE_SHARED_ROWS_PREFETCH;
+    auto load1 = [&](int64_t i0, In (&dst)[NI]) {
 #pragma unroll
         for (int q = 0; q < NI; ++q) {
-            const int64_t it = it0 + q * nwaves;
-            In& x = in[q];
+            const int64_t it = i0 + q * nwaves;
+            In& x = dst[q];
             x.b = -1;
             if (it < items) {
-                x.b = (int32_t)(it / tb.A);
-                x.jt = (int32_t)(it - (int64_t)x.b * tb.A);
-                x.si = slots[x.jt];
-                if constexpr (SHARE && SPE_ROWS_CACHE) {
-                    if (x.b != cb) {   // (wave-uniform)
-                        cb = x.b;
-                        cs = srcv[x.b * WAVE + lane];
-                        cri = rli[x.b * WAVE + lane];
-                    }
-                    x.s = cs;
-                    x.ri = cri;
+                if constexpr (BT > 1) {
+                    const int64_t tile = it / ((int64_t)BT * tb.A);
+                    const int32_t b0 = (int32_t)tile * BT;
+                    const int32_t bt = min(BT, blocks - b0);
+                    const int64_t r = it - tile * BT * (int64_t)tb.A;
+                    x.jt = (int32_t)(r / bt);
+                    x.b = b0 + (int32_t)(r - (int64_t)x.jt * bt);
                 } else {
-                    x.s = srcv[x.b * WAVE + lane];
-                    if constexpr (SHARE) x.ri = rli[x.b * WAVE + lane];
+                    x.b = (int32_t)(it / tb.A);
+                    x.jt = (int32_t)(it - (int64_t)x.b * tb.A);
                 }
+                x.si = slots[x.jt];
+                x.s = srcv[x.b * WAVE + lane];
+                if constexpr (SHARE) x.ri = rli[x.b * WAVE + lane];
             }
+        }
+    };
+    In nxt[NI];
+    if constexpr (PF) load1(lo + wave0, nxt);
+    for (int64_t it0 = lo + wave0; it0 < items; it0 += NI * nwaves) {
+        In in[NI];
+        if constexpr (PF) {
+#pragma unroll
+            for (int q = 0; q < NI; ++q) in[q] = nxt[q];
+            load1(it0 + NI * nwaves, nxt);
+        } else {
+            load1(it0, in);
         }
 #pragma unroll
         for (int q = 0; q < NI; ++q) {
             In& x = in[q];
             x.dc = INF;
             if (x.b >= 0 && x.s >= 0 && x.si.t != x.s) {
+#ifdef SPE_ROWS_EXP_COALESCED   // experiment: contiguous lanes instead of the root gather (wrong rows)
+                const int32_t sl = SHARE ? ((x.ri.x & ~63) + lane) : x.b * WAVE + lane;
+#else
                 const int32_t sl = SHARE ? x.ri.x : x.b * WAVE + lane;   // state lane
+#endif
                 const int32_t g = sl / L, j = sl % L;
                 if (x.si.c >= 0) {
                     const size_t rt = sidx<L>(g, n, x.si.c, j);
+#ifdef SPE_ROWS_WRITE_ONLY   // experiment: the store stream alone (wrong rows)
+                    x.dc = 1.0 + (double)rt * 0.0;
+                    x.rc = Route{1.0, 1, 0};
+#elif defined(SPE_ROWS_EXP_DONLY)   // experiment: no route gather (wrong rows)
+                    x.dc = st.D[rt];
+                    x.rc = Route{1.0, 1, 0};
+#else
                     x.dc = st.D[rt];
                     x.rc = st.RT[rt];
+#endif
                 } else {   // a contracted target: the best of its three neighbours (d, then d[u], then u)
                     const int32_t r = -2 - x.si.c;
                     const int32_t u0 = G.rnb[3 * r], u1 = G.rnb[3 * r + 1], u2 = G.rnb[3 * r + 2];
