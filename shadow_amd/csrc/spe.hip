@@ -1703,8 +1703,11 @@ __device__ double aux_fold(const DevGraph& G, const State& st, int32_t g, int32_
 #ifndef SPE_SHARED_ROWS_PREFETCH
 #define SPE_SHARED_ROWS_PREFETCH 0   // measured slower (89 VGPRs, 5 waves / SIMD)
 #endif
-template <int L, bool AUX, bool SHARE = false>
-__global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, int32_t sb0,
+#ifndef SPE_SHARED_ROWS_OCC
+#define SPE_SHARED_ROWS_OCC 1   // waves / SIMD the shared rows kernel is held to (1: the compiler's choice)
+#endif
+template <int L, bool AUX, bool SHARE = false, int OCC = 1>
+__global__ __launch_bounds__(BLOCK, OCC) void k_rows_sssp(int32_t n, int32_t blocks, int32_t sb0,
                                                      const int32_t* __restrict__ srcv,
                                                      const SlotInfo* __restrict__ slots, DevGraph G,
                                                      RowMode md, State st, Table tb,
@@ -1937,6 +1940,122 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
     }
 }
 
+
+// Shared anchor trees, rows through LDS (plain relaxation graph, fast targets): a
+// workgroup takes a tile of RT_B consecutive source blocks x RT_T consecutive
+// targets.  The tile's sources read the root lanes [r0, r1] (rng[tile], host-built;
+// roots are numbered in first-appearance order, so a tile's ~100 roots are
+// consecutive lanes), so the workgroup first stages those lanes' distance and route
+// for its RT_T targets in LDS -- every load of the tile in flight at once, one
+// memory round trip -- and then writes the tile's 64-lane records from LDS (each
+// wave one source block's targets in order: contiguous 1-KB record segments).
+// A tile whose lane span exceeds RT_R takes the per-lane gathers of k_rows_sssp.
+#ifndef SPE_RT_B
+#define SPE_RT_B 8
+#endif
+#ifndef SPE_RT_T
+#define SPE_RT_T 8
+#endif
+constexpr int RT_B = SPE_RT_B, RT_T = SPE_RT_T, RT_R = 24 * SPE_RT_B;
+
+template <int L>
+__global__ __launch_bounds__(BLOCK) void k_rows_shared_lds(int32_t n, int32_t blocks, int32_t sb0,
+                                                           const int32_t* __restrict__ srcv,
+                                                           const SlotInfo* __restrict__ slots, DevGraph G,
+                                                           RowMode md, State st, Table tb,
+                                                           const int2* __restrict__ rli,
+                                                           const double2* __restrict__ rwa,
+                                                           const int2* __restrict__ rng) {
+    __shared__ double sD[RT_T][RT_R];
+    __shared__ Route sR[RT_T][RT_R];
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int32_t wib = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));
+    const int32_t ntiles = (blocks + RT_B - 1) / RT_B;
+    const int32_t ntc = (tb.A + RT_T - 1) / RT_T;
+    const int64_t work = (int64_t)ntiles * ntc;
+    for (int64_t w = blockIdx.x; w < work; w += gridDim.x) {   // workgroup-uniform
+        const int32_t tile = (int32_t)(w / ntc);
+        const int32_t jt0 = (int32_t)(w - (int64_t)tile * ntc) * RT_T;
+        const int32_t b0 = tile * RT_B, nb = min(RT_B, blocks - b0);
+        const int32_t nt = min(RT_T, tb.A - jt0);
+        const int2 rr = rng[tile];
+        const int32_t nr = rr.y - rr.x + 1;
+        const bool staged = nr > 0 && nr <= RT_R;
+        if (staged) {
+            for (int32_t i = threadIdx.x; i < nt * nr; i += BLOCK) {
+                const int32_t tl = i / nr, q = i - tl * nr;
+                const int32_t c = slots[jt0 + tl].c;
+                const int32_t R = rr.x + q;
+                double d = INF;
+                Route rt{1.0, 0, -1};
+                if (c >= 0) {
+                    const size_t x = sidx<L>(R / L, n, c, R % L);
+                    d = st.D[x];
+                    rt = st.RT[x];
+                }
+                sD[tl][q] = d;
+                sR[tl][q] = rt;
+            }
+        }
+        __syncthreads();
+        for (int32_t bl = wib; bl < nb; bl += BLOCK / WAVE) {
+            const int32_t b = b0 + bl;
+            const int32_t s = srcv[b * WAVE + lane];
+            const int2 ri = rli[b * WAVE + lane];
+            const double2 wa = rwa[b * WAVE + lane];
+            for (int32_t tl = 0; tl < nt; ++tl) {
+                const int32_t jt = jt0 + tl;
+                const SlotInfo si = slots[jt];
+                double Lt = -1.0, R = -1.0;
+                int32_t N = -1, H = 0;
+                if (s >= 0) {
+                    if (si.t == s) {
+                        self_entry(G, md, s, Lt, R, N, H);
+                    } else {
+                        double dc = INF;
+                        Route rc{1.0, 0, -1};
+                        if (staged) {
+                            dc = sD[tl][ri.x - rr.x];
+                            rc = sR[tl][ri.x - rr.x];
+                        } else if (si.c >= 0) {
+                            const size_t x = sidx<L>(ri.x / L, n, si.c, ri.x % L);
+                            dc = st.D[x];
+                            rc = st.RT[x];
+                        }
+                        if (dc < INF) {
+                            if (ri.y >= 0) {   // a pruned pendant source: s -> anchor, then the root's path
+                                dc = wa.x + dc;
+                                rc.r = wa.y * rc.r;
+                                rc.h = rc.h + 1;
+                                rc.f = ri.y;
+                            }
+                            double d = dc;
+                            Route rt2 = rc;
+                            if (si.kt >= 0) {   // a pruned pendant target: one edge past its anchor
+                                d = dc + si.pw;
+                                rt2.r = rc.r * si.pa;
+                                rt2.h = rc.h + 1;
+                                rt2.f = (rc.h == 0) ? si.t : rc.f;
+                            }
+                            Lt = d == 0 ? 1.0 : d;   // shd-topology.c:1833-1837
+                            R = rt2.r;
+                            N = rt2.f;
+                            H = rt2.h;
+                        }
+                    }
+                }
+                const size_t o = tidx(sb0 + b, tb.A, jt, lane);
+                dvec2 e;
+                e.x = Lt;
+                e.y = R;
+                __builtin_nontemporal_store(e, reinterpret_cast<dvec2*>(tb.lr + o));
+                __builtin_nontemporal_store(N, tb.next + o);
+                __builtin_nontemporal_store((uint16_t)(H > 65535 ? 65535 : H), tb.hops + o);
+            }
+        }
+        __syncthreads();   // the next tile's staging overwrites sD / sR
+    }
+}
 
 // Shared anchor trees: after a batch's relaxation over its roots, flag every root
 // some of whose parent decisions a source offset could change.  A source s with
@@ -3348,6 +3467,7 @@ struct spe_table {
     int32_t* rsrc_buf[2] = {nullptr, nullptr};    // per source slot of the batch: original id (-1 pad)
     int2* rli_buf[2] = {nullptr, nullptr};        // per source slot: {root's state lane, first hop / -1}
     double2* rwa_buf[2] = {nullptr, nullptr};     // per source slot: {pendant latency, f_s (1 - p)}
+    int2* rng_buf[2] = {nullptr, nullptr};        // per tile of RT_B source blocks: root lane span
     unsigned char* h_rows = nullptr;   // pinned staging for the three (owned blocks x 64 x 28 B)
     uint8_t* d_unsafe = nullptr;   // per root lane: k_share_check's flag
     uint8_t* h_unsafe = nullptr;
@@ -4225,6 +4345,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
             TRY(dev_alloc(t->allocs, &t->rsrc_buf[i], owned_slots));
             TRY(dev_alloc(t->allocs, &t->rli_buf[i], owned_slots));
             TRY(dev_alloc(t->allocs, &t->rwa_buf[i], owned_slots));
+            TRY(dev_alloc(t->allocs, &t->rng_buf[i], owned_slots / WAVE / RT_B + 2));
         }
         TRY(dev_alloc(t->allocs, &t->d_unsafe, GW));
     }
@@ -4240,7 +4361,9 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     } while (0)
     HTRY(hipHostMalloc((void**)&t->h_srcv, 2 * GW * sizeof(int32_t), hipHostMallocDefault));
     if (t->share) {
-        HTRY(hipHostMalloc((void**)&t->h_rows, owned_slots * (sizeof(double2) + sizeof(int2) + sizeof(int32_t)),
+        HTRY(hipHostMalloc((void**)&t->h_rows,
+                           owned_slots * (sizeof(double2) + sizeof(int2) + sizeof(int32_t)) +
+                               (owned_slots / WAVE / RT_B + 2) * sizeof(int2),
                            hipHostMallocDefault));
         HTRY(hipHostMalloc((void**)&t->h_unsafe, GW, hipHostMallocDefault));
     }
@@ -4520,13 +4643,27 @@ static void launch_rows_sssp(spe_table* t, int grid, int32_t blocks, int32_t sb0
     }
 #undef ROWS
 }
+#ifndef SPE_SHARED_ROWS_LDS
+#define SPE_SHARED_ROWS_LDS 1
+#endif
 static void launch_rows_shared(spe_table* t, int grid, int32_t blocks, int32_t sb0, hipStream_t s,
-                               const int32_t* rsrc, const int2* rli, const double2* rwa) {
+                               const int32_t* rsrc, const int2* rli, const double2* rwa, const int2* rng) {
+    if (SPE_SHARED_ROWS_LDS && !t->cx) {   // (contracted targets read three rows: the gather kernel)
+        const int64_t work = (int64_t)((blocks + RT_B - 1) / RT_B) * ((t->A + RT_T - 1) / RT_T);
+        const int g = (int)std::max<int64_t>(1, std::min<int64_t>(work, 2048));
+        if (t->lanes == 128)
+            k_rows_shared_lds<128><<<g, BLOCK, 0, s>>>(t->bn, blocks, sb0, rsrc, t->d_slots, *t->bG, t->md, t->st,
+                                                       t->tb, rli, rwa, rng);
+        else
+            k_rows_shared_lds<64><<<g, BLOCK, 0, s>>>(t->bn, blocks, sb0, rsrc, t->d_slots, *t->bG, t->md, t->st,
+                                                      t->tb, rli, rwa, rng);
+        return;
+    }
     if (t->lanes == 128)
-        k_rows_sssp<128, false, true><<<grid, BLOCK, 0, s>>>(t->bn, blocks, sb0, rsrc, t->d_slots, *t->bG, t->md,
+        k_rows_sssp<128, false, true, SPE_SHARED_ROWS_OCC><<<grid, BLOCK, 0, s>>>(t->bn, blocks, sb0, rsrc, t->d_slots, *t->bG, t->md,
                                                               t->st, t->tb, rli, rwa);
     else
-        k_rows_sssp<64, false, true><<<grid, BLOCK, 0, s>>>(t->bn, blocks, sb0, rsrc, t->d_slots, *t->bG, t->md,
+        k_rows_sssp<64, false, true, SPE_SHARED_ROWS_OCC><<<grid, BLOCK, 0, s>>>(t->bn, blocks, sb0, rsrc, t->d_slots, *t->bG, t->md,
                                                              t->st, t->tb, rli, rwa);
 }
 }  // extern "C++"
@@ -4680,15 +4817,29 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
                 hw[i] = make_double2(h.fiw[(size_t)kx], (std::isnan(fs) ? 1.0 : 1.0 * fs) * h.fia[(size_t)kx]);
             }
         }
+        // per tile of RT_B blocks: the span of root lanes its sources read
+        const int32_t ntile = (nblk + RT_B - 1) / RT_B;
+        int2* hg = reinterpret_cast<int2*>(hr + ns);
+        for (int32_t k = 0; k < ntile; ++k) {
+            int32_t lo = INT32_MAX, hi = -1;
+            for (int32_t i = k * RT_B * WAVE; i < std::min(nblk, (k + 1) * RT_B) * WAVE; ++i)
+                if (hl[i].x >= 0) {
+                    lo = std::min(lo, hl[i].x);
+                    hi = std::max(hi, hl[i].x);
+                }
+            hg[k] = hi >= 0 ? make_int2(lo, hi) : make_int2(0, -1);
+        }
         int32_t* d_rsrc = t->rsrc_buf[ovl ? buf : 0];
         int2* d_rli = t->rli_buf[ovl ? buf : 0];
         double2* d_rwa = t->rwa_buf[ovl ? buf : 0];
+        int2* d_rng = t->rng_buf[ovl ? buf : 0];
         HIP_TRY(hipMemcpyAsync(t->d_srcv, t->h_srcv, sizeof(int32_t) * pb * WAVE, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(t->d_srcc, t->h_srcv + pb * WAVE, sizeof(int32_t) * pb * WAVE, hipMemcpyHostToDevice,
                                s));
         HIP_TRY(hipMemcpyAsync(d_rsrc, hr, sizeof(int32_t) * ns, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_rli, hl, sizeof(int2) * ns, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_rwa, hw, sizeof(double2) * ns, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_rng, hg, sizeof(int2) * ntile, hipMemcpyHostToDevice, s));
         int r = relax_to_convergence(t, rb, s);
         if (r) return r;
         t->stats.relaxed_lanes += R;
@@ -4735,7 +4886,7 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
         const int row_grid = grid_for((int64_t)nblk * t->A * WAVE, BLOCK, SPE_SHARED_ROWS_GRID);
         {
             LaunchTimer lt(t, rs, SPE_K_ROWS);
-            launch_rows_shared(t, row_grid, nblk, sb0, rs, d_rsrc, d_rli, d_rwa);
+            launch_rows_shared(t, row_grid, nblk, sb0, rs, d_rsrc, d_rli, d_rwa, d_rng);
         }
         if (t->md.prefer) {
             LaunchTimer lt(t, rs, SPE_K_DIRECT);

@@ -3,7 +3,7 @@ set -e
 O=gpurun_out/share_rows_ab; mkdir -p $O
 run() {  # name, env...
   N=$1; shift
-  env SPE_NO_OVERLAP=1 "$@" timeout -k 10 300 python -u bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-side > $O/b_${N}_$rep.log 2>&1 || { tail -20 $O/b_${N}_$rep.log; exit 1; }
+  env "$@" timeout -k 10 300 python -u bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-side > $O/b_${N}_$rep.log 2>&1 || { tail -20 $O/b_${N}_$rep.log; exit 1; }
   python - $O/b_${N}_$rep.log "c4 $N rep=$rep" <<'PY'
 import json,sys
 l=json.loads([x for x in open(sys.argv[1]) if x.startswith("{")][-1])
@@ -11,8 +11,9 @@ print(sys.argv[2], "table_s", l["full_table_time_s"], "src/s", l["value"], "kern
 PY
 }
 for rep in 1 2; do
-  run base X=1
-  run coal SPE_LIB=build_ab/coal/libspe.so
-  run donly SPE_LIB=build_ab/donly/libspe.so
-  run wonly SPE_LIB=build_ab/wonly/libspe.so
+  run b8t8 X=1
+  run b8t4 SPE_LIB=build_ab/t4/libspe.so
+  run b8t16 SPE_LIB=build_ab/t16/libspe.so
+  run b16t4 SPE_LIB=build_ab/b16/libspe.so
+  run b4t16 SPE_LIB=build_ab/b4/libspe.so
 done
