@@ -1942,7 +1942,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_rows_sssp(int32_t n, int32_t blo
 
 
 // Shared anchor trees, rows through LDS (plain relaxation graph, fast targets): a
-// workgroup takes a tile of RT_B consecutive source blocks x RT_T consecutive
+// workgroup takes a tile of RT_B (16) consecutive source blocks x RT_T (4) consecutive
 // targets.  The tile's sources read the root lanes [r0, r1] (rng[tile], host-built;
 // roots are numbered in first-appearance order, so a tile's ~100 roots are
 // consecutive lanes), so the workgroup first stages those lanes' distance and route
@@ -1951,10 +1951,10 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_rows_sssp(int32_t n, int32_t blo
 // wave one source block's targets in order: contiguous 1-KB record segments).
 // A tile whose lane span exceeds RT_R takes the per-lane gathers of k_rows_sssp.
 #ifndef SPE_RT_B
-#define SPE_RT_B 8
+#define SPE_RT_B 16
 #endif
 #ifndef SPE_RT_T
-#define SPE_RT_T 8
+#define SPE_RT_T 4
 #endif
 constexpr int RT_B = SPE_RT_B, RT_T = SPE_RT_T, RT_R = 24 * SPE_RT_B;
 

@@ -11,9 +11,5 @@ print(sys.argv[2], "table_s", l["full_table_time_s"], "src/s", l["value"], "kern
 PY
 }
 for rep in 1 2; do
-  run b8t8 X=1
-  run b8t4 SPE_LIB=build_ab/t4/libspe.so
-  run b8t16 SPE_LIB=build_ab/t16/libspe.so
-  run b16t4 SPE_LIB=build_ab/b16/libspe.so
-  run b4t16 SPE_LIB=build_ab/b4/libspe.so
+  for V in b16t4 b32t2 b16t8 b32t4 b16t2; do run $V SPE_LIB=build_ab/$V/libspe.so; done
 done
