@@ -1697,17 +1697,9 @@ __device__ double aux_fold(const DevGraph& G, const State& st, int32_t g, int32_
 // core source} and rwa[.] = {pendant edge latency w, f_s * (1 - p)}: a pruned pendant
 // source's row is its anchor's with the edge folded in front (latency w + d,
 // reliability (f_s a) r, one more hop, first hop the anchor).
-#ifndef SPE_SHARED_ROWS_TILE
-#define SPE_SHARED_ROWS_TILE 8
-#endif
-#ifndef SPE_SHARED_ROWS_PREFETCH
-#define SPE_SHARED_ROWS_PREFETCH 0   // measured slower (89 VGPRs, 5 waves / SIMD)
-#endif
-#ifndef SPE_SHARED_ROWS_OCC
-#define SPE_SHARED_ROWS_OCC 1   // waves / SIMD the shared rows kernel is held to (1: the compiler's choice)
-#endif
-template <int L, bool AUX, bool SHARE = false, int OCC = 1>
-__global__ __launch_bounds__(BLOCK, OCC) void k_rows_sssp(int32_t n, int32_t blocks, int32_t sb0,
+// (Here only for contracted shared tables; plain ones take k_rows_shared_lds.)
+template <int L, bool AUX, bool SHARE = false>
+__global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, int32_t sb0,
                                                      const int32_t* __restrict__ srcv,
                                                      const SlotInfo* __restrict__ slots, DevGraph G,
                                                      RowMode md, State st, Table tb,
@@ -1741,10 +1733,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_rows_sssp(int32_t n, int32_t blo
     // the ~10 blocks whose sources share one lane group of roots then read a target's
     // root row from L2 one after the other instead of once per block sweep (each
     // item still writes one whole 1-KB record segment)
-    constexpr int BT = SHARE ? SPE_SHARED_ROWS_TILE : 1;
-    // SHARE: the next trip's item constants (slot, source, root lane) are requested
-    // before this trip's state gathers, so a trip waits for one memory round trip
-    constexpr bool PF = SHARE && SPE_SHARED_ROWS_PREFETCH;
+    constexpr int BT = SHARE ? 8 : 1;
     auto load1 = [&](int64_t i0, In (&dst)[NI]) {
 #pragma unroll
         for (int q = 0; q < NI; ++q) {
@@ -1769,40 +1758,20 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_rows_sssp(int32_t n, int32_t blo
             }
         }
     };
-    In nxt[NI];
-    if constexpr (PF) load1(lo + wave0, nxt);
     for (int64_t it0 = lo + wave0; it0 < items; it0 += NI * nwaves) {
         In in[NI];
-        if constexpr (PF) {
-#pragma unroll
-            for (int q = 0; q < NI; ++q) in[q] = nxt[q];
-            load1(it0 + NI * nwaves, nxt);
-        } else {
-            load1(it0, in);
-        }
+        load1(it0, in);
 #pragma unroll
         for (int q = 0; q < NI; ++q) {
             In& x = in[q];
             x.dc = INF;
             if (x.b >= 0 && x.s >= 0 && x.si.t != x.s) {
-#ifdef SPE_ROWS_EXP_COALESCED   // experiment: contiguous lanes instead of the root gather (wrong rows)
-                const int32_t sl = SHARE ? ((x.ri.x & ~63) + lane) : x.b * WAVE + lane;
-#else
                 const int32_t sl = SHARE ? x.ri.x : x.b * WAVE + lane;   // state lane
-#endif
                 const int32_t g = sl / L, j = sl % L;
                 if (x.si.c >= 0) {
                     const size_t rt = sidx<L>(g, n, x.si.c, j);
-#ifdef SPE_ROWS_WRITE_ONLY   // experiment: the store stream alone (wrong rows)
-                    x.dc = 1.0 + (double)rt * 0.0;
-                    x.rc = Route{1.0, 1, 0};
-#elif defined(SPE_ROWS_EXP_DONLY)   // experiment: no route gather (wrong rows)
-                    x.dc = st.D[rt];
-                    x.rc = Route{1.0, 1, 0};
-#else
                     x.dc = st.D[rt];
                     x.rc = st.RT[rt];
-#endif
                 } else {   // a contracted target: the best of its three neighbours (d, then d[u], then u)
                     const int32_t r = -2 - x.si.c;
                     const int32_t u0 = G.rnb[3 * r], u1 = G.rnb[3 * r + 1], u2 = G.rnb[3 * r + 2];
@@ -4660,10 +4629,10 @@ static void launch_rows_shared(spe_table* t, int grid, int32_t blocks, int32_t s
         return;
     }
     if (t->lanes == 128)
-        k_rows_sssp<128, false, true, SPE_SHARED_ROWS_OCC><<<grid, BLOCK, 0, s>>>(t->bn, blocks, sb0, rsrc, t->d_slots, *t->bG, t->md,
+        k_rows_sssp<128, false, true><<<grid, BLOCK, 0, s>>>(t->bn, blocks, sb0, rsrc, t->d_slots, *t->bG, t->md,
                                                               t->st, t->tb, rli, rwa);
     else
-        k_rows_sssp<64, false, true, SPE_SHARED_ROWS_OCC><<<grid, BLOCK, 0, s>>>(t->bn, blocks, sb0, rsrc, t->d_slots, *t->bG, t->md,
+        k_rows_sssp<64, false, true><<<grid, BLOCK, 0, s>>>(t->bn, blocks, sb0, rsrc, t->d_slots, *t->bG, t->md,
                                                              t->st, t->tb, rli, rwa);
 }
 }  // extern "C++"
@@ -4880,10 +4849,7 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
             HIP_TRY(hipStreamWaitEvent(rs, t->ev_relaxed, 0));
         }
         const int32_t sb0 = b - t->row_base;
-#ifndef SPE_SHARED_ROWS_GRID
-#define SPE_SHARED_ROWS_GRID 8192
-#endif
-        const int row_grid = grid_for((int64_t)nblk * t->A * WAVE, BLOCK, SPE_SHARED_ROWS_GRID);
+        const int row_grid = grid_for((int64_t)nblk * t->A * WAVE, BLOCK, 8192);
         {
             LaunchTimer lt(t, rs, SPE_K_ROWS);
             launch_rows_shared(t, row_grid, nblk, sb0, rs, d_rsrc, d_rli, d_rwa, d_rng);
