@@ -102,7 +102,8 @@ typedef struct spe_graph_info {
 typedef struct spe_table_opts {
     int32_t self_mode;              /* SPE_SELF_ROW | SPE_SELF_RULE */
     int32_t force_sssp;             /* 1: ignore complete/preferdirectpaths (diagnostic) */
-    int32_t groups_per_launch;      /* 64-source groups relaxed together; 0 = auto */
+    int32_t groups_per_launch;      /* 64-source groups relaxed together; 0 = auto (with shared
+                                     * anchor trees: 64-lane blocks of roots the state holds) */
     int32_t block_begin;            /* first 64-row source block owned by this table */
     int32_t block_end;              /* one past the last; 0,0 = all blocks */
     /* optional caller-owned device storage for the owned blocks (all three or none),
@@ -210,7 +211,8 @@ typedef struct spe_table_layout {
     void* latrel;                   /* device pointers: double[2] {latency, reliability} */
     void* next_hop;
     void* hops;
-    int32_t groups_per_launch;      /* 64-source blocks one build launch covers */
+    int32_t groups_per_launch;      /* 64-source blocks one build launch covers (shared anchor
+                                     * trees: 64-lane blocks of roots one relaxation holds) */
     int32_t engine;                 /* the engine the table runs on (SPE_ENGINE_BATCH / _LDS) */
     int32_t n_devices;              /* > 1: a multi-device table; latrel is the home device's
                                      * replica of ALL blocks (padded to n_devices equal shares),
