@@ -1426,6 +1426,9 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_relax_s(int32_t total, int32_t n
     if (__ballot(wrote) && lane == 0) *fl.any_changed = 1;
 }
 
+#ifndef SPE_HEAVY_CX_INFL
+#define SPE_HEAVY_CX_INFL 5   // flagged rows per round trip of the contracted heavy partial
+#endif
 template <int M, int INFL, bool CX = false>
 __global__ __launch_bounds__(BLOCK) void k_heavy_partial_m(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
                                                            DevGraph G, State st, HeavyPlan hp, Partial pp, Flags fl) {
@@ -4549,7 +4552,7 @@ static int relax_to_convergence_l(spe_table* t, int32_t blocks, hipStream_t s) {
                 const int64_t cw = ((int64_t)groups * HP.nheavy + subs_per_wave - 1) / subs_per_wave;
                 if constexpr (M > 1) {
                     if (t->cx) {
-                        k_heavy_partial_m<M, INFL, true><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
+                        k_heavy_partial_m<M, SPE_HEAVY_CX_INFL, true><<<grid_for(pw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
                             groups, n, t->d_srcc, G, t->st, HP, t->pp, fl);
                         k_heavy_combine_m<M, true><<<grid_for(cw * WAVE, BLOCK, 4096), BLOCK, 0, s>>>(
                             groups, n, t->d_srcc, G, t->st, HP, t->pp, fl);
