@@ -1427,7 +1427,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_relax_s(int32_t total, int32_t n
 }
 
 #ifndef SPE_HEAVY_CX_INFL
-#define SPE_HEAVY_CX_INFL 5   // flagged rows per round trip of the contracted heavy partial
+#define SPE_HEAVY_CX_INFL 2   // flagged rows per round trip of the contracted heavy partial (A/B: 2 / 3 / 4 / 5 -> 61 / 68 / 72 / 72 ms of heavy passes per two C3 tables)
 #endif
 template <int M, int INFL, bool CX = false>
 __global__ __launch_bounds__(BLOCK) void k_heavy_partial_m(int32_t groups, int32_t n, const int32_t* __restrict__ srcv,
