@@ -437,7 +437,9 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
     from shadow_amd import spe
     config = config or args.config
     top, att, desc = workload(config)
-    g = spe.Graph(top, device=local)
+    t_prep = time.perf_counter()
+    g = spe.Graph(top, device=local)   # validation, pendant pruning, degree-3 contraction, heavy plan, upload
+    t_prep = time.perf_counter() - t_prep
     t_ord = time.perf_counter()
     att = g.order_sources(att)   # slot numbering is the caller's: clustered sources (host side)
     t_ord = time.perf_counter() - t_ord
@@ -596,15 +598,6 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
         extra["kernel_ms"] = {k: round(v["ms"], 3) for k, v in kp.items()}
         extra["kernel_launches"] = {k: v["launches"] for k, v in kp.items()}
         extra["engine"] = "lds" if lds else ("direct" if direct else "batch")
-        # the whole build against the full-graph SURVEY bytes (what BASELINE's B_s prices)
-        m_full = int(np.count_nonzero(top.esrc != top.edst)) * (1 if top.directed else 2)
-        b_full = 12.0 * m_full + 28.0 * top.n + 22.0 * A + 8.0
-        extra["roofline_full_graph_pricing"] = {
-            "achieved": round(b_full * built / (tb_sum / steps) / 1e9, 1), "unit": "GB/s",
-            "frac": round(b_full * built / (tb_sum / steps) / 1e9 / HBM_PEAK_GBS, 4),
-            "algorithmic_bytes_per_source": b_full,
-            "note": "SURVEY 8d B_s = 12 m_dir + 28 n + 22 A + 8 over the FULL graph, per GPU build time; the "
-                    "engine relaxes the pruned graph, so this overstates the kernel's achieved bandwidth"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not emulated:
         cpu = cpu_baseline(top, att, args.cpu_seconds, args.cpu_sources)
@@ -625,6 +618,11 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
                                        f"round (overlapped), blocks [{l0}, {l1}) built by every GPU itself"
                                        if gather else f"{world} GPU(s), no collective")},
             "full_table_time_s": round(el / steps, 4) if not emulated else None,
+            # the precompute outside the timed step (once per topology, shd-topology.c:356-384 /
+            # :1172-1195): spe_graph_create (validation, pruning, contraction, heavy plan, upload)
+            # and the clustered slot order
+            "graph_prep_s": round(t_prep, 4), "slot_order_s": round(t_ord, 4),
+            "precompute_end_to_end_s": round(t_prep + t_ord + el / steps, 4) if not emulated else None,
             "build_s_per_step": round(tb_sum / steps, 4),
             "gather_wait_s_per_step": round(tg_sum / steps, 4) if gather else None,
             "gather_bytes_per_gpu_per_step": gathered,
@@ -661,6 +659,125 @@ SIDE_CONFIGS = (
 )
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def launch_ranks(n: int, argv, timeout_s: float = 0.0):
+    """`python bench.py --gpus N` without torchrun: start N rank processes of this
+    script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on
+    127.0.0.1), as torchrun would.  The parent never touches the GPU and never
+    execs: it waits for the children, echoes their progress, and returns rank 0's
+    JSON line (None when any rank failed: the others are then terminated, since
+    they would block in a collective)."""
+    import threading
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "GROUP_RANK", "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)
+    env.update({"WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(_free_port())})
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=e, cwd=ROOT,
+                                      stdout=subprocess.PIPE, text=True, start_new_session=True))
+    found = [None]
+
+    def pump(p, rank):   # rank 0's JSON line is the result; everything else is progress
+        for line in p.stdout:
+            if rank == 0 and line.startswith("{"):
+                found[0] = line.strip()
+            else:
+                sys.stderr.write(f"[rank {rank}] {line}")
+                sys.stderr.flush()
+
+    th = [threading.Thread(target=pump, args=(p, r), daemon=True) for r, p in enumerate(procs)]
+    for x in th:
+        x.start()
+    t0 = time.perf_counter()
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = bad
+            break
+        if all(c == 0 for c in codes):
+            break
+        if timeout_s > 0 and time.perf_counter() - t0 > timeout_s:
+            failed = [("timeout", timeout_s)]
+            break
+        time.sleep(0.2)
+    if failed:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, 15)
+                except OSError:
+                    pass
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, 9)
+                except OSError:
+                    pass
+                p.wait()
+        print(f"[bench] rank(s) failed: {failed}", file=sys.stderr, flush=True)
+    for x in th:
+        x.join(timeout=10)
+    return None if failed else found[0]
+
+
+def bench_inproc(args, n: int, config: str):
+    """Shadow's own multi-GPU model (one process, shd-master.c:390-394): ONE path
+    table over devices 0..N-1 (spe_table_opts.devices), each device building its
+    share on its own host thread and stream, the records broadcast / gathered into
+    a replica on every device (the compute-versus-gather split of DESIGN §6).  A
+    step is one whole table build (spe_table_build), replicas included."""
+    from shadow_amd import spe
+    top, att, desc = workload(config)
+    t0 = time.perf_counter()
+    g = spe.Graph(top, device=0)
+    prep_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    att = g.order_sources(att)
+    order_s = time.perf_counter() - t0
+    rehearse = os.environ.get("SPE_BENCH_REHEARSE_ONE_GPU") == "1"
+    devs = [0] * n if rehearse else list(range(n))
+    t = spe.PathTable(g, att, devices=devs)
+    for _ in range(max(0, args.warmup)):
+        t.build()
+    steps = args.steps if args.steps > 0 else 2
+    runs, stats = [], []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        st = t.build()
+        runs.append(time.perf_counter() - t0)
+        stats.append(st)
+    el = sum(runs)
+    A = int(att.shape[0])
+    st = stats[-1]
+    line = {"metric": f"{config.upper()} whole path table, one process over {n} devices (spe_table_opts.devices)",
+            "value": round(A * steps / el, 1), "unit": "sources/s", "n_gpus": n, "steps": steps,
+            "higher_is_better": True, "scaling": "strong", "dtype": "f64", "data": "synthetic",
+            "devices": devs, "rehearsal_one_gpu": rehearse,
+            "config": {"workload": desc, "attached": A},
+            "full_table_time_s": round(el / steps, 4), "all_runs_s": [round(x, 4) for x in runs],
+            "graph_prep_s": round(prep_s, 4), "slot_order_s": round(order_s, 4),
+            "build_wait_s": round(st.get("build_wait_seconds", 0.0), 4),
+            "gather_s": round(st.get("gather_seconds", 0.0), 4),
+            "gather_mode": {1: "rccl", 2: "peer"}.get(st.get("gather", 0), st.get("gather", 0)),
+            "shared_blocks": st.get("shared_blocks"), "local_blocks": st.get("local_blocks"),
+            "nblk": (A + 63) // 64}
+    t.close()
+    print(json.dumps(line), flush=True)
+
+
 def side_configs(timeout_s: float = 240.0):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
@@ -684,9 +801,46 @@ def side_configs(timeout_s: float = 240.0):
     return out
 
 
+def run_multi(args, n: int):
+    """`python bench.py --gpus N` (N > 1) without torchrun -- the driver's plain
+    command line: N rank processes of this script (launch_ranks), then, unless
+    --no-inproc, the in-process multi-device table (bench_inproc) for C3 and C4 in
+    child processes once the ranks have exited; rank 0's line is printed with
+    those under side_configs.  Exits non-zero when a rank fails."""
+    argv = [a for a in sys.argv[1:]]
+    line = launch_ranks(n, argv)
+    if line is None:
+        raise SystemExit(1)
+    out = json.loads(line)
+    dry = os.environ.get("SPE_BENCH_LAUNCH_DRYRUN") == "1"
+    if not dry and not args.no_inproc and args.config == "c3":
+        env = dict(os.environ)
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+            env.pop(k, None)
+        rehearse = env.get("SPE_BENCH_REHEARSE_ONE_GPU") == "1"
+        side = out.setdefault("side_configs", {})
+        # (rehearsal on one GPU: C4's replicated records, 160 GB per replica, do not fit twice)
+        for cfg in (("c3",) if rehearse else ("c3", "c4")):
+            t0 = time.perf_counter()
+            try:
+                r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--inproc", str(n), "--config", cfg,
+                                    "--steps", "3", "--warmup", "1"], env=env, cwd=ROOT, capture_output=True,
+                                   text=True, timeout=300)
+                lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+                side[f"inproc_{cfg}"] = (json.loads(lines[-1]) if r.returncode == 0 and lines else
+                                         {"error": f"exit status {r.returncode}", "tail": (r.stdout + r.stderr)[-600:]})
+            except subprocess.TimeoutExpired:
+                side[f"inproc_{cfg}"] = {"error": "timed out after 300 s"}
+            side[f"inproc_{cfg}"]["wall_s"] = round(time.perf_counter() - t0, 1)
+            print(f"[bench] in-process {cfg} over {n} devices: {side[f'inproc_{cfg}'].get('value', side[f'inproc_{cfg}'].get('error'))}",
+                  file=sys.stderr, flush=True)
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node (default 1).  Without torchrun, N > 1 starts N rank processes itself")
     ap.add_argument("--steps", type=int, default=0, help="whole tables timed (0 = 3)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3")
@@ -713,15 +867,37 @@ def main():
     ap.add_argument("--share-index", type=int, default=0, help="--shares: the rank whose chunks this run builds")
     ap.add_argument("--no-side", action="store_true",
                     help="default C3 run at N = 1: skip the C1/C2/C4/C5 lines measured in child processes")
+    ap.add_argument("--inproc", type=int, default=0,
+                    help="N > 1: one process over devices 0..N-1 (spe_table_opts.devices) instead of N ranks")
+    ap.add_argument("--no-inproc", action="store_true",
+                    help="N > 1 without torchrun: skip the in-process multi-device lines after the ranks")
     args = ap.parse_args()
     if args.config == "complete":
         return bench_complete(args)
     if args.config == "c2fw":
         return bench_fw(args)
+    if args.inproc > 0:
+        return bench_inproc(args, args.inproc, args.config)
 
+    gpus = args.gpus if args.gpus is not None else 1
+    if "WORLD_SIZE" not in os.environ and gpus > 1:
+        return run_multi(args, gpus)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (torchrun's --nproc-per-node)")
+    if os.environ.get("SPE_BENCH_LAUNCH_DRYRUN") == "1":   # the launcher's CPU test: gloo ranks, no GPU
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        x = torch.tensor([float(rank + 1)])
+        dist.all_reduce(x)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "n_gpus": world, "rank_sum": float(x.item()), "dryrun": True}),
+                  flush=True)
+        dist.destroy_process_group()
+        return
     # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, gloo
     # instead of RCCL (RCCL refuses two ranks on one device); never for numbers
     rehearse = os.environ.get("SPE_BENCH_REHEARSE_ONE_GPU") == "1"
