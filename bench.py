@@ -456,15 +456,19 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
     gather = world > 1 and not args.no_gather
     # one chunk = one build launch: the LDS engine covers every block in one launch,
     # the batch engine `groups` blocks (auto rule above)
-    gpl = nblk if lds_engine else (args.groups if args.groups > 0 else auto_groups(info, nblk, A, world, dev))
+    # (one GPU: the library's own rule, spe_table_create -- shared tables size the batch by their roots)
+    gpl = (nblk if lds_engine else args.groups if args.groups > 0 else
+           0 if world == 1 and not emulated else auto_groups(info, nblk, A, world, dev))
     blk_elems = A * 64
-    pad_blocks = shares * sum(sd.chunk_schedule(nblk, shares, gpl))   # the pure-sharding span (>= nblk)
+    pad_blocks = shares * sum(sd.chunk_schedule(nblk, shares, gpl)) if gpl > 0 else nblk   # pure-sharding span
     lr = torch.empty((pad_blocks * blk_elems, 2), dtype=torch.float64, device=dev)
     # the table owns no storage of its own that is ever written: every build goes
     # into the caller's buffers (spe_table_build_blocks_into); lr doubles as its
     # nominal external storage
     t = spe.PathTable(g, att, blocks=(0, nblk), ext=[lr.data_ptr(), lr.data_ptr(), lr.data_ptr()], groups=gpl,
                       engine=args.engine)
+    if gpl == 0:
+        gpl = t.layout()["groups_per_launch"]
     calib = None
     frac = 1.0 if not gather else args.shared_frac
     if gather and frac < 0:   # auto: measure T1 and B on this job, then plan
@@ -489,6 +493,7 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
                                    hp_base + s0 * blk_elems * 2)
 
     lanes_run = [0]   # relaxation lanes (sources, or shared anchor roots) of this rank's builds
+    derived_run = [0, 0]   # derived sources (no lane) and fallback blocks of this rank's builds
 
     def one_table():
         works, tb, tg, its = [], 0.0, 0.0, 0
@@ -498,6 +503,8 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
                 st = into(b0, b1)
                 its += st["iterations"]
                 lanes_run[0] += st["relaxed_lanes"]
+                derived_run[0] += st["derived_sources"]
+                derived_run[1] += st["fallback_blocks"]
             tb += time.perf_counter() - t0
             if gather:   # overlaps the next round's build and the local part (RCCL runs on its own stream)
                 w = sd.allgather_span(lr, off, gk, world, rank, blk_elems, dist, async_op=True)
@@ -508,6 +515,8 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
             st = into(l0, l1)
             its += st["iterations"]
             lanes_run[0] += st["relaxed_lanes"]
+            derived_run[0] += st["derived_sources"]
+            derived_run[1] += st["fallback_blocks"]
             tb += time.perf_counter() - t0
         t1 = time.perf_counter()
         for w in works:
@@ -532,6 +541,7 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
     torch.cuda.synchronize(dev)
     barrier()
     lanes_run[0] = 0
+    derived_run[0] = derived_run[1] = 0
     t0 = time.perf_counter()
     tb_sum = tg_sum = 0.0
     it_total = 0
@@ -586,6 +596,8 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
                 "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
                 "algorithmic_bytes_per_source": b_relax,
                 "relaxed_lanes_per_step": round(relaxed / steps),
+                "derived_sources_per_step": round(derived_run[0] / steps),
+                "fallback_blocks_per_step": round(derived_run[1] / steps, 2),
                 "shared_anchor_trees": bool(lay.get("shared_sources", 0)),
                 "lanes_per_group": lay["lanes_per_group"],
                 "bytes_basis": "relaxation graph: 12 m_relax + 28 n_relax + 8 (SURVEY 8d B_s minus the row stage)"}

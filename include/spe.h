@@ -34,6 +34,14 @@
 #ifndef SPE_H_
 #define SPE_H_
 
+/* ABI guard: every struct the library reads or fills starts with struct_size,
+ * which the caller sets to sizeof() of the struct as IT was compiled
+ * (SPE_STRUCT_INIT).  The library refuses (SPE_EINVAL) a struct of another size,
+ * so a caller built against an older spe.h -- whose structs lack trailing fields
+ * this one has -- is rejected instead of having its stack read as options or
+ * overwritten with statistics. */
+#define SPE_STRUCT_INIT(T) {(uint32_t)sizeof(T)}
+
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -70,6 +78,7 @@ typedef struct spe_table spe_table;
  * pointer is NULL: all absent).  Validation mirrors _topology_checkGraph:
  * latency > 0, 0 <= packetloss <= 1, endpoints in range. */
 typedef struct spe_graph_desc {
+    uint32_t struct_size;           /* sizeof(spe_graph_desc) as the caller compiled it */
     int32_t n_vertices;
     int64_t n_edges;
     const int32_t* edge_source;
@@ -84,6 +93,7 @@ typedef struct spe_graph_desc {
 } spe_graph_desc;
 
 typedef struct spe_graph_info {
+    uint32_t struct_size;           /* sizeof(spe_graph_info) as the caller compiled it */
     int32_t n_vertices;
     int64_t n_edges;
     int64_t n_relax_entries;        /* directed adjacency entries after merging parallel edges
@@ -100,6 +110,7 @@ typedef struct spe_graph_info {
 } spe_graph_info;
 
 typedef struct spe_table_opts {
+    uint32_t struct_size;           /* sizeof(spe_table_opts) as the caller compiled it */
     int32_t self_mode;              /* SPE_SELF_ROW | SPE_SELF_RULE */
     int32_t force_sssp;             /* 1: ignore complete/preferdirectpaths (diagnostic) */
     int32_t groups_per_launch;      /* 64-source groups relaxed together; 0 = auto (with shared
@@ -204,6 +215,7 @@ int spe_device_split(int32_t n_attached, int32_t n_devices, double shared_fracti
  * reliability share one 16-byte record (the per-packet lookup reads both:
  * one HBM line per query instead of two). */
 typedef struct spe_table_layout {
+    uint32_t struct_size;           /* sizeof(spe_table_layout) as the caller compiled it */
     int32_t n_attached;
     int32_t block_begin;
     int32_t block_end;
@@ -234,6 +246,7 @@ typedef struct spe_entry {
 } spe_entry;
 
 typedef struct spe_build_stats {
+    uint32_t struct_size;           /* sizeof(spe_build_stats) as the caller compiled it */
     int64_t iterations;             /* relaxation rounds summed over launches */
     int64_t active_rounds;          /* relaxation rounds in which some distance/route changed */
     int64_t launches;
@@ -247,6 +260,8 @@ typedef struct spe_build_stats {
     int64_t relaxed_lanes;          /* batch engine: relaxation lanes (sources, or shared anchor
                                      * roots) the last build ran, padding excluded */
     int32_t fallback_blocks;        /* shared anchor trees: source blocks rebuilt lane per source */
+    int64_t derived_sources;        /* contracted shared tables: sources whose rows came from their
+                                     * three neighbours' roots, without a relaxation lane */
 } spe_build_stats;
 
 const char* spe_last_error(void);

@@ -63,6 +63,9 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+#define ABI_MSG(T) (std::string(T) + ".struct_size is not sizeof(" T ") of this libspe: the caller was built " \
+                    "against another include/spe.h (set it with SPE_STRUCT_INIT)")
+
 // FNV-1a 64 over raw bytes (table cache keys)
 struct Fnv {
     uint64_t h = 1469598103934665603ull;
@@ -2029,6 +2032,219 @@ __global__ __launch_bounds__(BLOCK) void k_rows_shared_lds(int32_t n, int32_t bl
     }
 }
 
+// Contracted shared tables: derived rows.  The relaxation lanes are
+// the batch's roots (kept core sources, pendant anchors); a contracted source x (a
+// removed degree-3 vertex whose three neighbours are all roots of the batch) takes
+// no lane: every path from x leaves through one of its neighbours u_i, so
+//   d_x(t) = min_i fl(w(x, u_i) + d_{u_i}(t)),  next hop u*, hops 1 + h_{u*}(t),
+//   reliability a(x, u*) r_{u*}(t)
+// (shd-topology.c:1741 runs one Dijkstra per source instead).  x's route is u*'s
+// route behind the edge x -> u* exactly when u* wins by more than the rounding
+// both sums carry and u*'s own decisions hold for the offset w(x, u*)
+// (k_share_check); a source where the first test fails is flagged in `sunsafe`
+// and its block is rebuilt one lane per source.  A removed TARGET y reads its three
+// neighbours in the root's row (best by (d, d[u], u), as k_rows_sssp); for a
+// source with an offset (pendant or derived) that choice is margin-checked too.
+// Items are (tile of TT targets, source block) with the target tile slowest and
+// XCD-contiguous: an XCD's resident waves work on the same few targets, so the
+// state columns the derived sources gather (every root lane at those vertices)
+// stay in that XCD's L2, and each wave writes TT consecutive 1-KB segments.
+struct alignas(16) DerivedSrc {
+    int32_t lane[3];   // root lanes of the three neighbours, in G.rnb order
+    int32_t rid;       // removed index of the source (G.rnb / rw / ra at 3 rid + i)
+};
+
+// A root lane's value at a target: the relaxation vertex c's distance, or for a
+// removed target (c = -2 - r) the best of its three neighbours; `tight` when an
+// offset could change that choice (runner-up within the margin of k_share_check).
+struct RootVal {
+    double d;
+    size_t ri;      // state index whose route record the row continues
+    int32_t q;      // removed target: the neighbour taken, -1 otherwise
+    bool tight;
+};
+
+__device__ __forceinline__ bool near_tie(double best, double alt, double wmin, double omax, double hmax) {
+    const double h = wmin > 0.0 ? fmin(hmax, alt / wmin + 3.0) : hmax;
+    return alt - best <= 4.5 * h * 0x1p-53 * (omax + alt);
+}
+
+template <int L>
+__device__ __forceinline__ RootVal root_val(const DevGraph& G, const State& st, int32_t n, int32_t sl, int32_t c,
+                                            bool check, double wmin, double omax, double hmax) {
+    RootVal o;
+    const int32_t g = sl / L, j = sl - (sl / L) * L;
+    o.q = -1;
+    o.tight = false;
+    if (c >= 0) {
+        o.ri = sidx<L>(g, n, c, j);
+        o.d = st.D[o.ri];
+        return o;
+    }
+    const int32_t r = -2 - c;
+    const size_t i0 = sidx<L>(g, n, G.rnb[3 * r], j), i1 = sidx<L>(g, n, G.rnb[3 * r + 1], j),
+                 i2 = sidx<L>(g, n, G.rnb[3 * r + 2], j);
+    const double d0 = st.D[i0], d1 = st.D[i1], d2 = st.D[i2];
+    const double a0 = d0 + G.rw[3 * r], a1 = d1 + G.rw[3 * r + 1], a2 = d2 + G.rw[3 * r + 2];
+    int32_t q = d0 < INF ? 0 : -1;
+    double bd = d0 < INF ? a0 : INF, bu = d0;
+    if (d1 < INF && (a1 < bd || (a1 == bd && d1 < bu))) {
+        q = 1;
+        bd = a1;
+        bu = d1;
+    }
+    if (d2 < INF && (a2 < bd || (a2 == bd && d2 < bu))) {
+        q = 2;
+        bd = a2;
+    }
+    o.d = bd;
+    o.q = q;
+    o.ri = q == 0 ? i0 : (q == 1 ? i1 : i2);
+    if (check && q >= 0) {
+        bool t = false;
+        if (q != 0 && d0 < INF) t |= near_tie(bd, a0, wmin, omax, hmax);
+        if (q != 1 && d1 < INF) t |= near_tie(bd, a1, wmin, omax, hmax);
+        if (q != 2 && d2 < INF) t |= near_tie(bd, a2, wmin, omax, hmax);
+        o.tight = t;
+    }
+    return o;
+}
+
+#ifndef SPE_DERIVED_TT
+#define SPE_DERIVED_TT 2
+#endif
+template <int L, int TT>
+__global__ __launch_bounds__(BLOCK) void k_rows_derived(int32_t n, int32_t blocks, int32_t sb0,
+                                                        const int32_t* __restrict__ srcv,
+                                                        const SlotInfo* __restrict__ slots, DevGraph G,
+                                                        RowMode md, State st, Table tb,
+                                                        const int2* __restrict__ rli,
+                                                        const double2* __restrict__ rwa,
+                                                        const DerivedSrc* __restrict__ der,
+                                                        const int32_t* __restrict__ lane_v, double wmin,
+                                                        double omax, double hmax, int32_t exact,
+                                                        uint8_t* __restrict__ sunsafe) {
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int32_t ntt = (tb.A + TT - 1) / TT;
+    const int64_t items_all = (int64_t)ntt * blocks;
+    const bool xs = (gridDim.x & 7) == 0;
+    const int32_t xcd = xs ? (int32_t)(blockIdx.x & 7) : 0;
+    const int64_t nwaves = xs ? (((int64_t)(gridDim.x >> 3) * BLOCK) >> 6) : (((int64_t)gridDim.x * BLOCK) >> 6);
+    const int64_t lo = xs ? items_all * xcd / 8 : 0;
+    const int64_t items = xs ? items_all * (xcd + 1) / 8 : items_all;
+    const int64_t wave0 = xs ? ((((int64_t)(blockIdx.x >> 3) * BLOCK + threadIdx.x) >> 6))
+                             : ((((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6));
+    for (int64_t it = lo + wave0; it < items; it += nwaves) {   // wave-uniform
+        const int32_t tt = (int32_t)(it / blocks);
+        const int32_t b = (int32_t)(it - (int64_t)tt * blocks);
+        const int32_t s = srcv[b * WAVE + lane];
+        const int2 ri = rli[b * WAVE + lane];
+        const bool pend = ri.y >= 0, derv = ri.y <= -2;
+        double2 wa = make_double2(0.0, 1.0);
+        if (pend) wa = rwa[b * WAVE + lane];
+        DerivedSrc dx{{0, 0, 0}, 0};
+        double w0 = 0.0, w1 = 0.0, w2 = 0.0;
+        if (derv) {
+            dx = der[-2 - ri.y];
+            w0 = G.rw[3 * dx.rid];
+            w1 = G.rw[3 * dx.rid + 1];
+            w2 = G.rw[3 * dx.rid + 2];
+        }
+        const bool chk = (pend || derv) && !exact;
+        bool bad = false;
+        for (int32_t tl = 0; tl < TT; ++tl) {
+            const int32_t jt = tt * TT + tl;
+            if (jt >= tb.A) break;
+            const SlotInfo si = slots[jt];
+            double Lt = -1.0, R = -1.0;
+            int32_t N = -1, H = 0;
+            if (s >= 0) {
+                if (si.t == s) {
+                    self_entry(G, md, s, Lt, R, N, H);
+                } else {
+                    double d = INF;
+                    Route rt{1.0, 0, -1};
+                    RootVal v;
+                    int32_t hop = -1;
+                    double apre = 1.0;
+                    if (!derv) {
+                        v = root_val<L>(G, st, n, ri.x, si.c, chk, wmin, omax, hmax);
+                        d = v.d;
+                        if (pend && d < INF) {
+                            d = wa.x + d;
+                            apre = wa.y;
+                            hop = ri.y;
+                        }
+                    } else {
+                        const RootVal v0 = root_val<L>(G, st, n, dx.lane[0], si.c, chk, wmin, omax, hmax);
+                        const RootVal v1 = root_val<L>(G, st, n, dx.lane[1], si.c, chk, wmin, omax, hmax);
+                        const RootVal v2 = root_val<L>(G, st, n, dx.lane[2], si.c, chk, wmin, omax, hmax);
+                        const double o0 = w0 + v0.d, o1 = w1 + v1.d, o2 = w2 + v2.d;
+                        int32_t bi = 0;
+                        double bo = o0;
+                        if (o1 < bo) {
+                            bi = 1;
+                            bo = o1;
+                        }
+                        if (o2 < bo) {
+                            bi = 2;
+                            bo = o2;
+                        }
+                        if (bo < INF) {
+                            // u* must beat the other first hops by more than rounding (exact
+                            // sums: strictly; a tie needs x's own tree)
+                            if (exact) {
+                                bad |= (bi != 0 && o0 <= bo) || (bi != 1 && o1 <= bo) || (bi != 2 && o2 <= bo);
+                            } else {
+                                if (bi != 0 && o0 < INF) bad |= near_tie(bo, o0, wmin, omax, hmax);
+                                if (bi != 1 && o1 < INF) bad |= near_tie(bo, o1, wmin, omax, hmax);
+                                if (bi != 2 && o2 < INF) bad |= near_tie(bo, o2, wmin, omax, hmax);
+                            }
+                            v = bi == 0 ? v0 : (bi == 1 ? v1 : v2);
+                            d = bo;
+                            apre = G.ra[3 * dx.rid + bi];
+                            hop = lane_v[dx.lane[bi]];
+                        }
+                    }
+                    if (d < INF) {
+                        bad |= v.tight;
+                        const Route rc = st.RT[v.ri];
+                        rt = rc;
+                        if (v.q >= 0) {   // removed target: one edge past the neighbour taken
+                            rt.r = rc.r * G.ra[3 * (-2 - si.c) + v.q];
+                            rt.h = rc.h + 1;
+                            rt.f = (rc.h == 0) ? si.t : rc.f;
+                        }
+                        if (hop >= 0) {   // an offset source: its first edge in front
+                            rt.r = apre * rt.r;
+                            rt.h = rt.h + 1;
+                            rt.f = hop;
+                        }
+                        if (si.kt >= 0) {   // a pruned pendant target: one edge past its anchor
+                            d = d + si.pw;
+                            rt.r = rt.r * si.pa;
+                            rt.f = (rt.h == 0) ? si.t : rt.f;
+                            rt.h = rt.h + 1;
+                        }
+                        Lt = d == 0 ? 1.0 : d;   // shd-topology.c:1833-1837
+                        R = rt.r;
+                        N = rt.f;
+                        H = rt.h;
+                    }
+                }
+            }
+            const size_t o = tidx(sb0 + b, tb.A, jt, lane);
+            dvec2 e;
+            e.x = Lt;
+            e.y = R;
+            __builtin_nontemporal_store(e, reinterpret_cast<dvec2*>(tb.lr + o));
+            __builtin_nontemporal_store(N, tb.next + o);
+            __builtin_nontemporal_store((uint16_t)(H > 65535 ? 65535 : H), tb.hops + o);
+        }
+        if (bad) sunsafe[b * WAVE + lane] = 1;
+    }
+}
+
 // Shared anchor trees: after a batch's relaxation over its roots, flag every root
 // some of whose parent decisions a source offset could change.  A source s with
 // offset o (its pendant edge, o <= omax) sums every path in the same order as its
@@ -3443,6 +3659,12 @@ struct spe_table {
     unsigned char* h_rows = nullptr;   // pinned staging for the three (owned blocks x 64 x 28 B)
     uint8_t* d_unsafe = nullptr;   // per root lane: k_share_check's flag
     uint8_t* h_unsafe = nullptr;
+    // contracted shared tables: derived sources (k_rows_derived)
+    DerivedSrc* d_der = nullptr;   // per derived source of the batch
+    DerivedSrc* h_der = nullptr;   // pinned staging
+    uint8_t* d_sunsafe = nullptr;  // per source slot of the batch: a derived row's margin failed
+    uint8_t* h_sunsafe = nullptr;
+    bool derive = false;           // contracted sources take their neighbours' roots (no lane)
 };
 
 namespace {
@@ -3518,6 +3740,7 @@ int spe_device_count(int32_t* out) {
 
 int spe_graph_create(const spe_graph_desc* desc, int32_t device, spe_graph** out) {
     if (!out) return fail(SPE_EINVAL, "out is NULL");
+    if (desc && desc->struct_size != sizeof(spe_graph_desc)) return fail(SPE_EINVAL, ABI_MSG("spe_graph_desc"));
     *out = nullptr;
     auto* g = new spe_graph();
     std::string err;
@@ -3827,6 +4050,7 @@ int spe_graph_set_edge_aux(spe_graph* g, const double* edge_aux) {
 
 int spe_graph_info_get(const spe_graph* g, spe_graph_info* out) {
     if (!g || !out) return fail(SPE_EINVAL, "NULL argument");
+    if (out->struct_size != sizeof(spe_graph_info)) return fail(SPE_EINVAL, ABI_MSG("spe_graph_info"));
     out->n_vertices = g->hg.n;
     out->n_edges = g->hg.m;
     out->n_relax_entries = (int64_t)g->hg.icol.size();
@@ -3989,7 +4213,11 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         vslot[v] = i;
     }
     spe_table_opts o{};
-    if (opts) o = *opts;
+    o.struct_size = sizeof(spe_table_opts);
+    if (opts) {
+        if (opts->struct_size != sizeof(spe_table_opts)) return fail(SPE_EINVAL, ABI_MSG("spe_table_opts"));
+        o = *opts;
+    }
     const int32_t nblk_all = (n_attached + WAVE - 1) / WAVE;
     // every argument check before the first allocation (nothing to unwind)
     if (o.block_begin != 0 || o.block_end != 0) {
@@ -4177,11 +4405,58 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     // shared anchor trees: pendant sources relax as their anchor
     t->share = !o.exact_sources && g->hg.share.eligible && t->engine == SPE_ENGINE_BATCH && !t->md.complete &&
                !o.owner_rank && !o.want_aux && t->delta == 0.0;
-    if (t->share) {
+    if (t->share) {   // some offset source: a pruned pendant, or (contracted tables) a removed vertex
         bool any = false;
-        for (int32_t i = t->blk0 * WAVE; i < std::min(n_attached, t->blk1 * WAVE) && !any; ++i)
-            any = g->hg.core_id[(size_t)attached[i]] < 0;
+        for (int32_t i = t->blk0 * WAVE; i < std::min(n_attached, t->blk1 * WAVE) && !any; ++i) {
+            const int32_t c = g->hg.core_id[(size_t)attached[i]];
+            any = c < 0 || (t->cx && g->hg.cx.rid[(size_t)c] >= 0);
+        }
         t->share = any;
+    }
+    t->derive = t->share && t->cx;
+    if (t->share && o.groups_per_launch <= 0) {
+        // lane groups per batch for shared tables: every root of the owned range in one
+        // relaxation when the state fits (the rows of a contracted source read its
+        // neighbours' lanes, so they must be in its batch).  Roots: each core source and
+        // pendant anchor once, a contracted source none when its three neighbours are
+        // roots (derived), else its own lane.  State held once (no rows overlap).
+        const spe::HostGraph& h = g->hg;
+        std::vector<uint8_t> isroot((size_t)std::max(1, h.nc), 0);
+        int64_t roots = 0;
+        const int32_t s0 = t->blk0 * WAVE, s1 = std::min(n_attached, t->blk1 * WAVE);
+        for (int32_t i = s0; i < s1; ++i) {
+            const int32_t v = attached[i];
+            int32_t c = h.core_id[(size_t)v];
+            if (c < 0) c = h.anchor_core[(size_t)v];
+            else if (t->cx && h.cx.rid[(size_t)c] >= 0) continue;
+            if (c >= 0 && !isroot[(size_t)c]) {
+                isroot[(size_t)c] = 1;
+                ++roots;
+            }
+        }
+        if (t->cx)
+            for (int32_t i = s0; i < s1; ++i) {
+                const int32_t c = h.core_id[(size_t)attached[i]];
+                if (c < 0 || h.cx.rid[(size_t)c] < 0) continue;
+                const int32_t r = h.cx.rid[(size_t)c];
+                bool all = true;
+                for (int q = 0; q < 3; ++q) all &= isroot[(size_t)h.cx.kcore[(size_t)h.cx.rnb[3 * (size_t)r + q]]] != 0;
+                if (!all) ++roots;
+            }
+        const int32_t need = (int32_t)std::max<int64_t>(1, (roots + WAVE - 1) / WAVE);
+        const double per_group = (double)t->bn * WAVE * 28.0 + 4.0 * t->bn + 2.0 * std::max(1, t->bm);
+        double cap = (double)need;
+        size_t free_b = 0, total_b = 0;
+        if (hipSetDevice(g->device) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
+            const bool ext = o.ext_latrel || o.ext_next_hop || o.ext_hops;
+            const double table_b = ext ? 0.0 : (double)owned * n_attached * WAVE * 22.0;
+            cap = std::max(1.0, ((double)free_b - table_b - 4.0e9) / per_group);
+        }
+        const int32_t w = (int32_t)std::min<double>(need, cap);
+        const int32_t batches = (need + w - 1) / w;
+        int32_t gg = (need + batches - 1) / batches;
+        if (t->lanes == 128 && gg > 1 && gg % 2) ++gg;   // no padding lanes at L = 128
+        t->groups = std::max(1, std::min(gg, owned));
     }
     t->trace = o.trace != 0;
     t->tb.A = n_attached;
@@ -4263,7 +4538,8 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
     const size_t GW = GL * (size_t)t->lanes;   // source entries per batch (>= G * 64: padding lanes)
     if (!t->md.complete && t->engine == SPE_ENGINE_BATCH) {
         const size_t se = GW * (size_t)t->bn;
-        t->overlap = o.no_overlap == 0;
+        // (shared tables relax and write rows on one stream: one state buffer)
+        t->overlap = o.no_overlap == 0 && !t->share;
         for (int i = 0; i < (t->overlap ? 2 : 1); ++i) {
             TRY(dev_alloc(t->allocs, &t->st_buf[i].D, se));
             TRY(dev_alloc(t->allocs, &t->st_buf[i].P, se));
@@ -4320,6 +4596,10 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
             TRY(dev_alloc(t->allocs, &t->rng_buf[i], owned_slots / WAVE / RT_B + 2));
         }
         TRY(dev_alloc(t->allocs, &t->d_unsafe, GW));
+        if (t->derive) {
+            TRY(dev_alloc(t->allocs, &t->d_der, owned_slots));
+            TRY(dev_alloc(t->allocs, &t->d_sunsafe, owned_slots));
+        }
     }
 #undef TRY
     // every failure from here on releases what was allocated (spe_table_free)
@@ -4338,6 +4618,10 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
                                (owned_slots / WAVE / RT_B + 2) * sizeof(int2),
                            hipHostMallocDefault));
         HTRY(hipHostMalloc((void**)&t->h_unsafe, GW, hipHostMallocDefault));
+        if (t->derive) {
+            HTRY(hipHostMalloc((void**)&t->h_der, owned_slots * sizeof(DerivedSrc), hipHostMallocDefault));
+            HTRY(hipHostMalloc((void**)&t->h_sunsafe, owned_slots, hipHostMallocDefault));
+        }
     }
     HTRY(hipHostMalloc((void**)&t->h_counts, std::max<size_t>(64, (size_t)t->max_iters + 2) * sizeof(int32_t),
                        hipHostMallocDefault));
@@ -4692,55 +4976,84 @@ int spe_table_build_blocks_into(spe_table* t, int32_t block_begin, int32_t block
     return r;   // the table's own storage is untouched: nothing is marked built
 }
 
-// Shared anchor trees: a batch's relaxation lanes are its ROOTS --
-// each core source, and the anchor of each pruned pendant source, once -- and the
-// rows kernel gives every source its root's row (a pendant source's with its edge
-// in front).  Batches are cut at block boundaries into about equal root counts (two
-// at least with the rows / relaxation overlap, so one batch's rows hide under the
-// next one's relaxation).  Where the weights' sums are not exact, k_share_check
-// flags roots whose decisions an offset could change, and the blocks of their
-// sources are rebuilt with one lane per source.
-static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hipStream_t s, hipStream_t rs,
-                        bool ovl) {
+// Shared anchor trees and derived rows: a batch's relaxation lanes
+// are its ROOTS -- each core source, and the anchor of each pruned pendant source,
+// once -- and the rows kernel gives every source its root's row (a pendant
+// source's with its edge in front).  On a contracted graph a removed source whose
+// three neighbours are all roots of the call's range takes no lane (derived, see
+// k_rows_derived); any other removed source relaxes on its own lane.  Batches are
+// cut at block boundaries into about equal root counts.  Where the weights' sums
+// are not exact, k_share_check flags roots whose decisions an offset could change;
+// the blocks holding an offset source (pendant or derived) of a flagged root, or a
+// source whose derived row failed its own margin (sunsafe), are rebuilt with one
+// lane per source.
+static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hipStream_t s) {
     const spe_graph* g = t->g;
     const spe::HostGraph& h = g->hg;
     const int32_t L = t->lanes;
     const int32_t cap = t->groups * WAVE;   // root lanes one batch's state holds
-    auto root_of = [&](int32_t slot) -> int32_t {
-        const int32_t v = t->attached[(size_t)slot];
-        return h.core_id[(size_t)v] >= 0 ? h.core_id[(size_t)v] : h.anchor_core[(size_t)v];
+    const int32_t s_end = std::min(t->A, block_end * WAVE);
+    // per slot: root core id (core source, pendant anchor, or a removed source itself),
+    // or -3 for a derived source, -1 padding
+    auto removed = [&](int32_t c) { return t->derive && c >= 0 && h.cx.rid[(size_t)c] >= 0; };
+    auto nbr = [&](int32_t c, int q) {   // core id of removed vertex c's neighbour q (G.rnb order)
+        return h.cx.kcore[(size_t)h.cx.rnb[3 * (size_t)h.cx.rid[(size_t)c] + q]];
     };
     std::vector<int32_t> tag((size_t)std::max(1, h.nc), -1), lane_of((size_t)std::max(1, h.nc), -1);
+    // the call's non-derived roots: a removed source is derivable iff its three neighbours are among them
     int32_t total = 0;
-    for (int32_t i = block_begin * WAVE; i < std::min(t->A, block_end * WAVE); ++i) {
-        const int32_t c = root_of(i);
-        if (c >= 0 && tag[(size_t)c] < 0) {
+    for (int32_t i = block_begin * WAVE; i < s_end; ++i) {
+        const int32_t v = t->attached[(size_t)i];
+        const int32_t c0 = h.core_id[(size_t)v];
+        const int32_t c = c0 >= 0 ? c0 : h.anchor_core[(size_t)v];
+        if (c >= 0 && !removed(c) && tag[(size_t)c] < 0) {
             tag[(size_t)c] = 0;
             ++total;
         }
     }
-    // (two batches only when each still fills 8 lane groups: smaller relaxations run near-empty rounds)
-    const int32_t nb = std::max((total + cap - 1) / cap, (ovl && total >= 16 * L) ? 2 : 1);
+    std::vector<uint8_t> derivable((size_t)std::max(0, s_end - block_begin * WAVE), 0);
+    for (int32_t i = block_begin * WAVE; i < s_end; ++i) {
+        const int32_t c = h.core_id[(size_t)t->attached[(size_t)i]];
+        if (!removed(c)) continue;
+        bool all = true;
+        for (int q = 0; q < 3; ++q) all &= tag[(size_t)nbr(c, q)] == 0;
+        derivable[(size_t)(i - block_begin * WAVE)] = all;
+        if (!all) ++total;
+    }
+    auto root_of = [&](int32_t slot) -> int32_t {
+        const int32_t v = t->attached[(size_t)slot];
+        const int32_t c0 = h.core_id[(size_t)v];
+        if (c0 >= 0 && removed(c0) && derivable[(size_t)(slot - block_begin * WAVE)]) return -3;
+        return c0 >= 0 ? c0 : h.anchor_core[(size_t)v];
+    };
+    const int32_t nb = std::max(1, (total + cap - 1) / cap);
     const int32_t target = (total + nb - 1) / nb;
     std::fill(tag.begin(), tag.end(), -1);
     std::vector<int32_t> roots, deferred;
     std::vector<uint8_t> bad((size_t)std::max(1, h.nc), 0);
     const spe::HostGraph::Share& sh = h.share;
-    int buf = 0;
     for (int32_t b = block_begin, bid = 0; b < block_end; ++bid) {
         HIP_TRY(hipStreamSynchronize(s));   // the pinned staging is reused per batch
         roots.clear();
         int32_t e = b;
+        auto add = [&](int32_t c) {
+            if (c >= 0 && tag[(size_t)c] != bid) {
+                tag[(size_t)c] = bid;
+                lane_of[(size_t)c] = (int32_t)roots.size();
+                roots.push_back(c);
+            }
+        };
         while (e < block_end) {
             const size_t before = roots.size();
             for (int32_t l = 0; l < WAVE; ++l) {
                 const int32_t slot = e * WAVE + l;
                 if (slot >= t->A) break;
                 const int32_t c = root_of(slot);
-                if (c >= 0 && tag[(size_t)c] != bid) {
-                    tag[(size_t)c] = bid;
-                    lane_of[(size_t)c] = (int32_t)roots.size();
-                    roots.push_back(c);
+                if (c == -3) {   // a derived source: its neighbours must be roots of this batch
+                    const int32_t x = h.core_id[(size_t)t->attached[(size_t)slot]];
+                    for (int q = 0; q < 3; ++q) add(nbr(x, q));
+                } else {
+                    add(c);
                 }
             }
             // this block starts the next batch (the last planned batch takes the rest up to `cap`)
@@ -4752,13 +5065,8 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
             ++e;
         }
         const int32_t R = (int32_t)roots.size();
+        if (R > cap) return fail(SPE_ESTATE, "shared batch exceeds the state (one block's roots > groups * 64)");
         const int32_t nblk = e - b;
-        if (ovl) {
-            t->st = t->st_buf[buf];
-            t->d_srcv = t->srcv_buf[buf];
-            t->d_srcc = t->srcc_buf[buf];
-            if (t->rows_pending[buf]) HIP_TRY(hipStreamWaitEvent(s, t->ev_rows[buf], 0));
-        }
         // relaxation lanes: the roots (core sources of the batch engine's state)
         const int32_t bpg = std::max(1, L / WAVE);
         const int32_t rb = std::max(1, (R + WAVE - 1) / WAVE);
@@ -4770,18 +5078,30 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
             if (t->cx && c >= 0) cc = h.cx.kid[(size_t)c] >= 0 ? h.cx.kid[(size_t)c] : -2;
             t->h_srcv[pb * WAVE + i] = cc;
         }
-        // rows: every source slot of blocks [b, e), its root's lane and pendant prefix
+        // rows: every source slot of blocks [b, e), its root's lane and pendant prefix,
+        // or (derived) its record of neighbour lanes
         const size_t ns = (size_t)nblk * WAVE;
         double2* hw = reinterpret_cast<double2*>(t->h_rows);
         int2* hl = reinterpret_cast<int2*>(hw + ns);
         int32_t* hr = reinterpret_cast<int32_t*>(hl + ns);
+        int32_t nder = 0;
         for (int32_t i = 0; i < nblk * WAVE; ++i) {
             const int32_t slot = b * WAVE + i;
             const int32_t c = slot < t->A ? root_of(slot) : -1;
-            const int32_t v = c >= 0 ? t->attached[(size_t)slot] : -1;
+            const int32_t v = (slot < t->A && c != -1) ? t->attached[(size_t)slot] : -1;
             hr[i] = v;
-            hl[i] = make_int2(c >= 0 ? lane_of[(size_t)c] : -1, -1);
             hw[i] = make_double2(0.0, 1.0);
+            if (c == -3) {
+                const int32_t x = h.core_id[(size_t)v];
+                DerivedSrc d;
+                for (int q = 0; q < 3; ++q) d.lane[q] = lane_of[(size_t)nbr(x, q)];
+                d.rid = h.cx.rid[(size_t)x];
+                t->h_der[nder] = d;
+                hl[i] = make_int2(d.lane[0], -2 - nder);
+                ++nder;
+                continue;
+            }
+            hl[i] = make_int2(c >= 0 ? lane_of[(size_t)c] : -1, -1);
             if (v >= 0 && h.core_id[(size_t)v] < 0) {   // pendant: the edge s -> anchor in front
                 const int32_t kx = h.fiptr[(size_t)v];
                 const double fs = h.vfac[(size_t)v];
@@ -4789,7 +5109,7 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
                 hw[i] = make_double2(h.fiw[(size_t)kx], (std::isnan(fs) ? 1.0 : 1.0 * fs) * h.fia[(size_t)kx]);
             }
         }
-        // per tile of RT_B blocks: the span of root lanes its sources read
+        // per tile of RT_B blocks: the span of root lanes its sources read (k_rows_shared_lds)
         const int32_t ntile = (nblk + RT_B - 1) / RT_B;
         int2* hg = reinterpret_cast<int2*>(hr + ns);
         for (int32_t k = 0; k < ntile; ++k) {
@@ -4801,10 +5121,10 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
                 }
             hg[k] = hi >= 0 ? make_int2(lo, hi) : make_int2(0, -1);
         }
-        int32_t* d_rsrc = t->rsrc_buf[ovl ? buf : 0];
-        int2* d_rli = t->rli_buf[ovl ? buf : 0];
-        double2* d_rwa = t->rwa_buf[ovl ? buf : 0];
-        int2* d_rng = t->rng_buf[ovl ? buf : 0];
+        int32_t* d_rsrc = t->rsrc_buf[0];
+        int2* d_rli = t->rli_buf[0];
+        double2* d_rwa = t->rwa_buf[0];
+        int2* d_rng = t->rng_buf[0];
         HIP_TRY(hipMemcpyAsync(t->d_srcv, t->h_srcv, sizeof(int32_t) * pb * WAVE, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(t->d_srcc, t->h_srcv + pb * WAVE, sizeof(int32_t) * pb * WAVE, hipMemcpyHostToDevice,
                                s));
@@ -4812,9 +5132,12 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
         HIP_TRY(hipMemcpyAsync(d_rli, hl, sizeof(int2) * ns, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_rwa, hw, sizeof(double2) * ns, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_rng, hg, sizeof(int2) * ntile, hipMemcpyHostToDevice, s));
+        if (nder > 0) HIP_TRY(hipMemcpyAsync(t->d_der, t->h_der, sizeof(DerivedSrc) * nder, hipMemcpyHostToDevice, s));
         int r = relax_to_convergence(t, rb, s);
         if (r) return r;
         t->stats.relaxed_lanes += R;
+        t->stats.derived_sources += nder;
+        bool any_bad = false;
         if (!sh.exact) {
             const int32_t groups = L > WAVE ? pb / bpg : pb * (WAVE / L);
             HIP_TRY(hipMemsetAsync(t->d_unsafe, 0, (size_t)groups * L, s));
@@ -4831,63 +5154,72 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
             }
             HIP_TRY(hipMemcpyAsync(t->h_unsafe, t->d_unsafe, (size_t)R, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
-            bool any = false;
             for (int32_t i = 0; i < R; ++i)
                 if (t->h_unsafe[i]) {
                     bad[(size_t)roots[(size_t)i]] = 1;
-                    any = true;
+                    any_bad = true;
                 }
-            if (any)
-                for (int32_t blk = b; blk < e; ++blk)
-                    for (int32_t l = 0; l < WAVE; ++l) {
-                        const int32_t slot = blk * WAVE + l;
-                        if (slot < t->A && root_of(slot) >= 0 && bad[(size_t)root_of(slot)]) {
-                            deferred.push_back(blk);
-                            break;
-                        }
-                    }
-        }
-        if (ovl) {
-            HIP_TRY(hipEventRecord(t->ev_relaxed, s));
-            HIP_TRY(hipStreamWaitEvent(rs, t->ev_relaxed, 0));
         }
         const int32_t sb0 = b - t->row_base;
-        const int row_grid = grid_for((int64_t)nblk * t->A * WAVE, BLOCK, 8192);
         {
-            LaunchTimer lt(t, rs, SPE_K_ROWS);
-            launch_rows_shared(t, row_grid, nblk, sb0, rs, d_rsrc, d_rli, d_rwa, d_rng);
+            LaunchTimer lt(t, s, SPE_K_ROWS);
+            if (t->derive) {
+                HIP_TRY(hipMemsetAsync(t->d_sunsafe, 0, ns, s));
+                const int64_t items = (int64_t)((t->A + SPE_DERIVED_TT - 1) / SPE_DERIVED_TT) * nblk;
+                const int grid = (grid_for(items * WAVE, BLOCK, 8192) + 7) & ~7;
+                const double hmax = (double)h.n + 2.0;
+                k_rows_derived<128, SPE_DERIVED_TT><<<grid, BLOCK, 0, s>>>(
+                    t->bn, nblk, sb0, d_rsrc, t->d_slots, *t->bG, t->md, t->st, t->tb, d_rli, d_rwa, t->d_der,
+                    t->d_srcv, sh.wmin, sh.omax, hmax, sh.exact ? 1 : 0, t->d_sunsafe);
+            } else {
+                launch_rows_shared(t, grid_for((int64_t)nblk * t->A * WAVE, BLOCK, 8192), nblk, sb0, s, d_rsrc,
+                                   d_rli, d_rwa, d_rng);
+            }
         }
         if (t->md.prefer) {
-            LaunchTimer lt(t, rs, SPE_K_DIRECT);
-            k_direct_overlay<<<(nblk * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, rs>>>(nblk, sb0, d_rsrc, t->d_vertex_slot,
-                                                                                  g->dev, t->tb);
-        }
-        if (ovl) {
-            HIP_TRY(hipEventRecord(t->ev_rows[buf], rs));
-            t->rows_pending[buf] = true;
-            buf ^= 1;
+            LaunchTimer lt(t, s, SPE_K_DIRECT);
+            k_direct_overlay<<<(nblk * WAVE + BLOCK - 1) / BLOCK, BLOCK, 0, s>>>(nblk, sb0, d_rsrc, t->d_vertex_slot,
+                                                                                 g->dev, t->tb);
         }
         HIP_TRY(hipGetLastError());
+        bool any_sunsafe = false;
+        if (t->derive) {
+            HIP_TRY(hipMemcpyAsync(t->h_sunsafe, t->d_sunsafe, ns, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            for (size_t i = 0; i < ns && !any_sunsafe; ++i) any_sunsafe = t->h_sunsafe[i] != 0;
+        }
+        if (any_bad || any_sunsafe)
+            for (int32_t blk = b; blk < e; ++blk)
+                for (int32_t l = 0; l < WAVE; ++l) {
+                    const int32_t slot = blk * WAVE + l;
+                    if (slot >= t->A) break;
+                    const size_t i = (size_t)(slot - b * WAVE);
+                    bool d = any_sunsafe && t->h_sunsafe[i];
+                    const int32_t v = t->attached[(size_t)slot];
+                    const int32_t c = root_of(slot);
+                    if (!d && any_bad) {
+                        // an offset source of a flagged root (a core source is its own root: exact)
+                        if (c == -3) {
+                            const int32_t x = h.core_id[(size_t)v];
+                            for (int q = 0; q < 3; ++q) d |= bad[(size_t)nbr(x, q)] != 0;
+                        } else if (c >= 0 && h.core_id[(size_t)v] != c) {
+                            d = bad[(size_t)c] != 0;
+                        }
+                    }
+                    if (d) {
+                        deferred.push_back(blk);
+                        break;
+                    }
+                }
         if (t->prof) {
             HIP_TRY(hipStreamSynchronize(s));
-            r = resolve_profile(t, !ovl);
+            r = resolve_profile(t, true);
             if (r) return r;
         }
         b = e;
     }
-    if (ovl) {
-        HIP_TRY(hipStreamSynchronize(rs));
-        t->rows_pending[0] = t->rows_pending[1] = false;
-        t->st = t->st_buf[0];
-        t->d_srcv = t->srcv_buf[0];
-        t->d_srcc = t->srcc_buf[0];
-        if (t->prof) {
-            int r = resolve_profile(t);
-            if (r) return r;
-        }
-    }
     HIP_TRY(hipStreamSynchronize(s));
-    if (!deferred.empty()) {   // one lane per source for the flagged roots' blocks
+    if (!deferred.empty()) {   // one lane per source for the flagged blocks
         std::sort(deferred.begin(), deferred.end());
         deferred.erase(std::unique(deferred.begin(), deferred.end()), deferred.end());
         spe_build_stats keep = t->stats;
@@ -4928,7 +5260,7 @@ static int build_blocks_impl(spe_table* t, int32_t block_begin, int32_t block_en
         // concurrent relaxation of the next batch only queues behind it (the launches
         // between them wait for slots); one batch of every root, then its rows, was
         // as fast or faster (C4 0.1275 vs 0.130 s, same box, two passes)
-        const int r = build_shared(t, block_begin, block_end, s, s, false);
+        const int r = build_shared(t, block_begin, block_end, s);
         if (r) return r;
         t->stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         t->stats.n_devices = 1;
@@ -5082,12 +5414,15 @@ int spe_table_profile_get(const spe_table* t, spe_kernel_profile* out) {
 
 int spe_table_build_stats(const spe_table* t, spe_build_stats* out) {
     if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
+    if (out->struct_size != sizeof(spe_build_stats)) return fail(SPE_EINVAL, ABI_MSG("spe_build_stats"));
     *out = t->stats;
+    out->struct_size = sizeof(spe_build_stats);
     return SPE_OK;
 }
 
 int spe_table_layout_get(const spe_table* t, spe_table_layout* out) {
     if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
+    if (out->struct_size != sizeof(spe_table_layout)) return fail(SPE_EINVAL, ABI_MSG("spe_table_layout"));
     if (t->multi) return spe::multi_layout(t->multi, out);
     out->n_devices = 1;
     out->device = t->g->device;
@@ -5685,6 +6020,8 @@ void spe_table_free(spe_table* t) {
     if (t->h_srcv) (void)hipHostFree(t->h_srcv);
     if (t->h_rows) (void)hipHostFree(t->h_rows);
     if (t->h_unsafe) (void)hipHostFree(t->h_unsafe);
+    if (t->h_der) (void)hipHostFree(t->h_der);
+    if (t->h_sunsafe) (void)hipHostFree(t->h_sunsafe);
     if (t->h_counts) (void)hipHostFree(t->h_counts);
     for (hipEvent_t e : t->ev_pool) (void)hipEventDestroy(e);
     if (t->stream) (void)hipStreamDestroy(t->stream);

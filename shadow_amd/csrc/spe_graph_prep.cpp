@@ -389,7 +389,9 @@ void contract_degree3(HostGraph* hg) {
 void share_prep(HostGraph* hg) {
     HostGraph::Share& sh = hg->share;
     sh = HostGraph::Share{};
-    if (!hg->pruned || hg->directed || hg->multi_rep) return;
+    // pendant sources (pruning) and contracted sources (derived from their three
+    // neighbours' rows) are the two kinds of offset sources
+    if (!(hg->pruned || hg->cx.active) || hg->directed || hg->multi_rep) return;
     for (double f : hg->vfac)
         if (!(std::isnan(f) || f == 1.0)) return;
     std::vector<double> ws(hg->iw.begin(), hg->iw.end());
@@ -401,6 +403,8 @@ void share_prep(HostGraph* hg) {
         omax = std::max(omax, w);
         ws.push_back(w);
     }
+    if (hg->cx.active)   // a derived source's offset is the edge to one of its three neighbours
+        for (double w : hg->cx.rw) omax = std::max(omax, w);
     double wmin = INFINITY, wmax = 0.0;
     for (double w : hg->iw) wmin = std::min(wmin, w);
     for (double w : ws) {

@@ -120,7 +120,7 @@ int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_tab
                                            "(no block range, external storage, owner replay or want_aux)");
     if (o.gather < SPE_GATHER_AUTO || o.gather > SPE_GATHER_PEER) return set_error(SPE_EINVAL, "unknown gather mode");
     if (o.shared_fraction < 0.0 || o.shared_fraction > 1.0) return set_error(SPE_EINVAL, "shared_fraction must be in [0, 1]");
-    spe_graph_info gi;
+    spe_graph_info gi = SPE_STRUCT_INIT(spe_graph_info);
     spe_graph_info_get(g, &gi);
     auto* m = new MultiDev();
     m->home = g;
@@ -202,7 +202,7 @@ int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_tab
             po.ext_hops = m->hops[d];
             r = spe_table_create(m->graphs[d], attached, A, &po, &m->parts[d]);
             if (!r) {
-                spe_table_layout pl{};
+                spe_table_layout pl = SPE_STRUCT_INIT(spe_table_layout);
                 spe_table_layout_get(m->parts[d], &pl);
                 FwPart fp;
                 m->fw = pl.engine == SPE_ENGINE_FW && fw_part(m->parts[d], &fp) == SPE_OK;   // not for DIRECT tables
@@ -482,13 +482,14 @@ int multi_build(MultiDev* m, spe_build_stats* stats) {
     for (int d = 0; d < m->n; ++d)
         for (spe_table* p : {m->parts[d], m->lparts[d]}) {
             if (!p) continue;
-            spe_build_stats q{};
+            spe_build_stats q = SPE_STRUCT_INIT(spe_build_stats);
             spe_table_build_stats(p, &q);
             s.iterations += q.iterations;
             s.active_rounds += q.active_rounds;
             s.launches += q.launches;
             s.relaxed_lanes += q.relaxed_lanes;
             s.fallback_blocks += q.fallback_blocks;
+            s.derived_sources += q.derived_sources;
         }
     s.seconds = std::chrono::duration<double>(t2 - t0).count();
     s.gather_seconds = std::chrono::duration<double>(t2 - t1).count();   // gather time not hidden by the builds
@@ -574,7 +575,7 @@ int multi_min_latency(const MultiDev* m, double* out) {
 }
 
 int multi_layout(const MultiDev* m, spe_table_layout* out) {
-    spe_table_layout p{};
+    spe_table_layout p = SPE_STRUCT_INIT(spe_table_layout);
     for (spe_table* x : {m->parts[0], m->lparts[0]})
         if (x) {
             spe_table_layout_get(x, &p);

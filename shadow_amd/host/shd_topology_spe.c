@@ -704,7 +704,7 @@ Topology* topology_new_on_device(const char* graphPath, int32_t device) {
         nanv = malloc(((size_t)top->n + 1) * sizeof(double));
         for (int32_t v = 0; v < top->n; ++v) nanv[v] = NAN;
     }
-    spe_graph_desc d = {top->n, top->m, top->esrc, top->edst, top->elat, top->eloss, vloss ? vloss : nanv,
+    spe_graph_desc d = {sizeof(spe_graph_desc), top->n, top->m, top->esrc, top->edst, top->elat, top->eloss, vloss ? vloss : nanv,
                         top->directed, top->prefer_direct};
     const int rc = spe_graph_create(&d, device, &top->graph);
     free(nanv);
@@ -713,7 +713,7 @@ Topology* topology_new_on_device(const char* graphPath, int32_t device) {
         topo_release(top);
         return NULL;
     }
-    spe_graph_info info;
+    spe_graph_info info = SPE_STRUCT_INIT(spe_graph_info);
     spe_graph_info_get(top->graph, &info);
     top->complete = info.complete;
     if (!info.weight_floor_ok)   /* outside the bit-exactness argument */
@@ -1041,6 +1041,7 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
     for (int32_t i = 0; i < A; ++i) s->slot_of_vertex[s->attached[i]] = i;
     spe_table_opts o;
     memset(&o, 0, sizeof o);
+    o.struct_size = sizeof o;
     o.self_mode = SPE_SELF_ROW;
     /* SHADOW_SPE_DEVICES=0,1,...: build on several GPUs of this node (one share of
      * the sources each, then an all-gather of the records, spe_table_opts.devices) */

@@ -45,23 +45,30 @@ class SpeError(RuntimeError):
     pass
 
 
-class GraphDesc(C.Structure):
-    _fields_ = [("n_vertices", C.c_int32), ("n_edges", C.c_int64),
+class _Sized(C.Structure):
+    """A spe.h struct that starts with struct_size (the ABI guard): set on creation."""
+
+    def __init__(self, *args, **kw):
+        super().__init__(C.sizeof(type(self)), *args, **kw)
+
+
+class GraphDesc(_Sized):
+    _fields_ = [("struct_size", C.c_uint32), ("n_vertices", C.c_int32), ("n_edges", C.c_int64),
                 ("edge_source", C.c_void_p), ("edge_target", C.c_void_p),
                 ("edge_latency", C.c_void_p), ("edge_packetloss", C.c_void_p),
                 ("vertex_packetloss", C.c_void_p), ("directed", C.c_int32), ("prefer_direct", C.c_int32),
                 ("keep_pendants", C.c_int32)]
 
 
-class GraphInfo(C.Structure):
-    _fields_ = [("n_vertices", C.c_int32), ("n_edges", C.c_int64), ("n_relax_entries", C.c_int64),
+class GraphInfo(_Sized):
+    _fields_ = [("struct_size", C.c_uint32), ("n_vertices", C.c_int32), ("n_edges", C.c_int64), ("n_relax_entries", C.c_int64),
                 ("directed", C.c_int32), ("prefer_direct", C.c_int32), ("complete", C.c_int32),
                 ("parallel_latency_differs", C.c_int32), ("weight_floor_ok", C.c_int32), ("device", C.c_int32),
                 ("n_relax_vertices", C.c_int32)]
 
 
-class TableOpts(C.Structure):
-    _fields_ = [("self_mode", C.c_int32), ("force_sssp", C.c_int32), ("groups_per_launch", C.c_int32),
+class TableOpts(_Sized):
+    _fields_ = [("struct_size", C.c_uint32), ("self_mode", C.c_int32), ("force_sssp", C.c_int32), ("groups_per_launch", C.c_int32),
                 ("block_begin", C.c_int32), ("block_end", C.c_int32),
                 ("ext_latrel", C.c_void_p),
                 ("ext_next_hop", C.c_void_p), ("ext_hops", C.c_void_p), ("ext_filled", C.c_int32),
@@ -73,8 +80,8 @@ class TableOpts(C.Structure):
                 ("build_seconds_hint", C.c_double), ("no_contract", C.c_int32), ("exact_sources", C.c_int32)]
 
 
-class TableLayout(C.Structure):
-    _fields_ = [("n_attached", C.c_int32), ("block_begin", C.c_int32), ("block_end", C.c_int32),
+class TableLayout(_Sized):
+    _fields_ = [("struct_size", C.c_uint32), ("n_attached", C.c_int32), ("block_begin", C.c_int32), ("block_end", C.c_int32),
                 ("elems", C.c_int64), ("latrel", C.c_void_p),
                 ("next_hop", C.c_void_p), ("hops", C.c_void_p), ("groups_per_launch", C.c_int32),
                 ("engine", C.c_int32), ("n_devices", C.c_int32), ("device", C.c_int32),
@@ -101,11 +108,12 @@ class KernelProfile(C.Structure):
     _fields_ = [("ms", C.c_double * 8), ("launches", C.c_int64 * 8)]
 
 
-class BuildStats(C.Structure):
-    _fields_ = [("iterations", C.c_int64), ("active_rounds", C.c_int64), ("launches", C.c_int64),
+class BuildStats(_Sized):
+    _fields_ = [("struct_size", C.c_uint32), ("iterations", C.c_int64), ("active_rounds", C.c_int64), ("launches", C.c_int64),
                 ("seconds", C.c_double), ("gather_seconds", C.c_double), ("n_devices", C.c_int32),
                 ("gather", C.c_int32), ("shared_blocks", C.c_int32), ("local_blocks", C.c_int32),
-                ("build_wait_seconds", C.c_double), ("relaxed_lanes", C.c_int64), ("fallback_blocks", C.c_int32)]
+                ("build_wait_seconds", C.c_double), ("relaxed_lanes", C.c_int64), ("fallback_blocks", C.c_int32),
+                ("derived_sources", C.c_int64)]
 
 
 # every symbol include/spe.h declares (tests/test_abi.py checks the export table)

@@ -42,3 +42,40 @@ def test_no_cpu_fallback_when_library_missing(monkeypatch, tmp_path):
     monkeypatch.setattr(spe, "_lib", None)
     with pytest.raises(spe.SpeError):
         spe.lib()
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """Every spe.h struct the ctypes mirror declares has the C size and field
+    offsets (the mirror is what the tests and bench.py call through)."""
+    from shadow_amd import spe
+    structs = {"spe_graph_desc": spe.GraphDesc, "spe_graph_info": spe.GraphInfo, "spe_table_opts": spe.TableOpts,
+               "spe_table_layout": spe.TableLayout, "spe_build_stats": spe.BuildStats, "spe_entry": spe.Entry,
+               "spe_check_report": spe.CheckReport, "spe_kernel_profile": spe.KernelProfile}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "spe.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "sz.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                        check=True).stdout.splitlines())
+    for cname, py in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(py, f).offset, f"{cname}.{f}"
+
+
+def test_stale_struct_size_is_refused_without_gpu():
+    """The ABI guard: a caller built against another spe.h (struct_size differs)
+    gets SPE_EINVAL before anything is read (spe_graph_create checks it first)."""
+    from shadow_amd import spe
+    d = spe.GraphDesc()
+    d.struct_size = ctypes.sizeof(spe.GraphDesc) - 4
+    h = ctypes.c_void_p()
+    rc = spe.lib().spe_graph_create(ctypes.byref(d), 0, ctypes.byref(h))
+    assert rc == -1   # SPE_EINVAL
+    assert b"struct_size" in spe.lib().spe_last_error()

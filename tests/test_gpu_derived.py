@@ -1,0 +1,178 @@
+"""GPU parity of the derived rows, the batch engine's default for
+contracted sources on shared tables: a removed degree-3 vertex x whose three
+neighbours are relaxation roots of its batch takes no lane; its row is
+min_i fl(w(x, u_i) + d_{u_i}(t)) with first hop u*, one more hop, reliability
+a(x, u*) r_{u*}(t).
+
+The reference runs one Dijkstra per source (shd-topology.c:1741-1742) and folds
+each path in path order (:1413-1493).  Routability, next hops and hop counts must
+equal the oracle's exactly; latency and reliability agree within 1e-12 relative
+(the north star allows 1e-9), and bit for bit where every latency is an integer.
+A source whose first hop is within rounding of a tie, or whose neighbour roots'
+decisions are (k_share_check), is rebuilt one lane per source
+(spe_build_stats.fallback_blocks).  The rest of the GPU suite pins
+spe_table_opts.exact_sources (tests/conftest.py); this file runs the default.
+"""
+import numpy as np
+import pytest
+
+from shadow_amd import graphs
+from oracle import Oracle
+
+pytestmark = [pytest.mark.gpu, pytest.mark.engine_fixed, pytest.mark.shared_trees]
+
+RTOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def spe():
+    from shadow_amd import spe as m
+    assert m.device_count() > 0, "no GPU visible"
+    return m
+
+
+def near(got, ref, label, exact_lat=False):
+    ok = ref["kind"] != 0
+    np.testing.assert_array_equal(got["ok"], ok, err_msg=f"{label}: routability")
+    np.testing.assert_array_equal(got["next"][ok], ref["next"][ok], err_msg=f"{label}: next hop")
+    np.testing.assert_array_equal(got["hops"][ok], ref["hops"][ok], err_msg=f"{label}: hops")
+    if exact_lat:
+        np.testing.assert_array_equal(got["lat"][ok], ref["lat"][ok], err_msg=f"{label}: latency")
+    else:
+        np.testing.assert_allclose(got["lat"][ok], ref["lat"][ok], rtol=RTOL, atol=0, err_msg=f"{label}: latency")
+    np.testing.assert_allclose(got["rel"][ok], ref["rel"][ok], rtol=RTOL, atol=0, err_msg=f"{label}: reliability")
+    assert (got["lat"][~ok] == -1).all() and (got["hops"][~ok] == 0).all(), f"{label}: unroutable entries"
+
+
+def with_pendants(top, k, seed):
+    rng = np.random.default_rng(seed)
+    anc = rng.integers(0, top.n, k)
+    n2 = top.n + k
+    return graphs.Topology(n=n2, esrc=np.concatenate([top.esrc, np.arange(top.n, n2)]).astype(np.int32),
+                           edst=np.concatenate([top.edst, anc]).astype(np.int32),
+                           elat=np.concatenate([top.elat, rng.uniform(0.5, 10.0, k)]),
+                           eloss=np.concatenate([top.eloss, rng.uniform(0, 0.01, k)]),
+                           vloss=np.zeros(n2), directed=False, prefer_direct=False)
+
+
+def integer_ba(n, seed):
+    top = graphs.gen_ba(n, 3, seed)
+    rng = np.random.default_rng(seed + 100)
+    top.elat = rng.integers(1, 30, top.elat.shape[0]).astype(np.float64)
+    return top
+
+
+def decimal_ba(n, seed):
+    top = graphs.gen_ba(n, 3, seed)
+    rng = np.random.default_rng(seed + 200)
+    top.elat = rng.integers(1, 60, top.elat.shape[0]) * 0.1
+    return top
+
+
+def partial(top, frac, seed):
+    rng = np.random.default_rng(seed)
+    return top, np.sort(rng.choice(top.n, int(frac * top.n), replace=False)).astype(np.int32)
+
+
+def all_of(top):
+    return top, np.arange(top.n, dtype=np.int32)
+
+
+# (graph + attached, oracle tie mode, latencies bit-exact, every contracted source derivable)
+CASES = {
+    "ba": (lambda: all_of(graphs.gen_ba(4000, 3, 21)), 0, False, True),
+    "ba_partial": (lambda: partial(graphs.gen_ba(4000, 3, 22), 0.7, 5), 0, False, False),
+    "ba_pendants": (lambda: all_of(with_pendants(graphs.gen_ba(3000, 3, 23), 400, 6)), 0, False, True),
+    "integer": (lambda: all_of(integer_ba(3000, 24)), 1, True, True),
+    "decimal": (lambda: all_of(decimal_ba(3000, 25)), 1, False, True),
+}
+
+
+def exact_build(spe, g, A, **kw):
+    te = spe.PathTable(g, A, engine=spe.SPE_ENGINE_BATCH, exact_sources=True, **kw)
+    se = te.build()
+    assert te.layout()["shared_sources"] == 0 and se["derived_sources"] == 0
+    return te.download()
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("groups", [0, 6])
+def test_derived_rows_match_oracle_and_exact_build(spe, name, groups):
+    mk, tie_mode, exact_lat, all_derivable = CASES[name]
+    top, A = mk()
+    g = spe.Graph(top)
+    A = g.order_sources(A)
+    t = spe.PathTable(g, A, engine=spe.SPE_ENGINE_BATCH, groups=groups)
+    st = t.build()
+    lay = t.layout()
+    assert lay["shared_sources"] == 1 and lay["contracted_vertices"] > 0, (name, lay)
+    assert st["derived_sources"] > 0, (name, st)
+    assert st["relaxed_lanes"] < len(A), (name, st)
+    if all_derivable and groups == 0:   # one batch: every contracted source derived, no lane of its own
+        n_removed = g.info()["n_relax_vertices"] - lay["contracted_vertices"]
+        assert st["derived_sources"] + 64 * st["fallback_blocks"] >= min(n_removed, len(A)) - 64, (name, st)
+    got = t.download()
+    ref = Oracle(top).rows(A, A, tie_mode=tie_mode)
+    near(got, ref, f"{name} groups={groups}", exact_lat=exact_lat)
+    ex = exact_build(spe, g, A, groups=groups)
+    for k in ("ok", "next", "hops"):
+        np.testing.assert_array_equal(got[k], ex[k], err_msg=f"{name}: {k} vs exact build")
+    if name == "integer":
+        assert st["fallback_blocks"] > 0, "integer latencies: first-hop ties must fall back"
+    if name == "decimal":
+        assert st["fallback_blocks"] > 0, "decimal latencies: near ties must fall back"
+
+
+def test_derived_rows_block_ranges_and_source_trees(spe):
+    """A block range of a derived table equals the same rows of the whole exact
+    table (derivability is decided over the call's own range); source trees
+    recompute one lane per source."""
+    top, A = all_of(graphs.gen_ba(4000, 3, 26))
+    g = spe.Graph(top)
+    A = g.order_sources(A)
+    full = exact_build(spe, g, A)
+    t = spe.PathTable(g, A, engine=spe.SPE_ENGINE_BATCH, blocks=(3, 11))
+    st = t.build()
+    assert t.layout()["shared_sources"] == 1 and st["derived_sources"] > 0, st
+    part = t.download(3 * 64, 11 * 64)
+    for k in ("ok", "next", "hops"):
+        np.testing.assert_array_equal(part[k], full[k][3 * 64:11 * 64], err_msg=k)
+    ok = full["ok"][3 * 64:11 * 64]
+    for k in ("lat", "rel"):
+        np.testing.assert_allclose(part[k][ok], full[k][3 * 64:11 * 64][ok], rtol=RTOL, atol=0, err_msg=k)
+    te = spe.PathTable(g, A, engine=spe.SPE_ENGINE_BATCH, exact_sources=True)
+    te.build()
+    for s in (3 * 64, 3 * 64 + 17, 11 * 64 - 1):
+        np.testing.assert_array_equal(t.source_tree(s), te.source_tree(s), err_msg=f"source tree {s}")
+
+
+def test_derived_rows_kept_sources_bit_exact(spe):
+    """A kept (core) source is its own root: its row is the exact build's bit for
+    bit; only derived rows may differ in the last bits of latency / reliability."""
+    top, A = all_of(graphs.gen_ba(3000, 3, 27))
+    g = spe.Graph(top)
+    A = g.order_sources(A)
+    t = spe.PathTable(g, A, engine=spe.SPE_ENGINE_BATCH)
+    t.build()
+    got = t.download()
+    ex = exact_build(spe, g, A)
+    nl = top.esrc != top.edst
+    deg = np.bincount(np.concatenate([top.esrc[nl], top.edst[nl]]), minlength=top.n)
+    lat_diff = (got["lat"] != ex["lat"]).any(axis=1)
+    # every differing row is a degree-3 (contractible) source
+    assert (deg[A[lat_diff]] == 3).all()
+    np.testing.assert_allclose(got["lat"], ex["lat"], rtol=RTOL, atol=0)
+
+
+def test_derived_rows_full_table_self_check(spe):
+    """spe_table_check over a whole derived table: next hops adjacent, hop
+    recursion, symmetric latencies within 1e-12."""
+    top, A = all_of(graphs.gen_ba(6000, 3, 28))
+    g = spe.Graph(top)
+    A = g.order_sources(A)
+    t = spe.PathTable(g, A, engine=spe.SPE_ENGINE_BATCH)
+    st = t.build()
+    assert st["derived_sources"] > 0
+    rep = t.check()
+    assert rep["bad_values"] == 0 and rep["next_not_adjacent"] == 0, rep
+    assert rep["hop_mismatch"] == 0 and rep["sym_mismatch"] == 0, rep
