@@ -288,6 +288,80 @@ def bench_complete(args):
     print(json.dumps(line), flush=True)
 
 
+def bench_shim(args, config: str):
+    """The drop-in end to end (include/shd_topology_spe.h, libshdtopo): the config's
+    topology written once as GraphML (every vertex an "ip"), then what Shadow does
+    at start-up -- topology_new (libxml2 ingest + the reference's validation +
+    spe_graph_create), topology_attach of every host by exact IP hint, topology_seal
+    (slot order + the whole path table + the host mirror) -- each phase timed
+    (shd-topology.c:2469-2490 / 2354-2413 / the first query's row runs).  Then C5
+    through the drop-in: rounds of uniform (src, dst) host-address pairs answered by
+    topology_getPathInfoBatch (per query the reference's path-cache bookkeeping on
+    the host, the table read in one device launch), against the reference's
+    per-packet lookup restated on one core."""
+    import shutil
+    import tempfile
+    from shadow_amd import graphs
+    from shadow_amd import topology as T
+    top_g, att, desc = workload(config)
+    ips = [f"10.{(v >> 16) & 255}.{(v >> 8) & 255}.{v & 255}" for v in range(top_g.n)]
+    tmp = tempfile.mkdtemp(prefix="spe-shim-")
+    try:
+        path = os.path.join(tmp, "topology.graphml")
+        t0 = time.perf_counter()
+        graphs.write_graphml(top_g, path, ips=ips)
+        write_s = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        top = T.Topology(path)
+        new_s = time.perf_counter() - t0
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    A = int(att.shape[0])
+    hosts = np.array([T.ip(f"11.{(i >> 16) & 255}.{(i >> 8) & 255}.{i & 255}") for i in range(A)], np.uint32)
+    t0 = time.perf_counter()
+    for i in range(A):
+        top.attach(int(hosts[i]), ip_hint=ips[int(att[i])])
+    attach_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    rc = top.seal()
+    seal_s = time.perf_counter() - t0
+    assert rc == 0, f"topology_seal failed ({rc})"
+    q = min(args.queries, 20_000_000)
+    rng = np.random.default_rng(5)
+    pi = rng.integers(0, A, (q, 2))
+    src, dst = hosts[pi[:, 0]], hosts[pi[:, 1]]
+    ok, lat, rel = top.path_info_batch(src[:1 << 16], dst[:1 << 16])   # warm-up (code objects, staging)
+    steps = args.steps if args.steps > 0 else 3
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ok, lat, rel = top.path_info_batch(src, dst)
+    el = time.perf_counter() - t0
+    assert ok.all(), "every pair of the synthetic topologies is routable"
+    # the same pairs one call at a time (topology_getPathInfo), a bounded sample
+    ns = 200_000
+    t1 = time.perf_counter()
+    for i in range(ns):
+        top.path_info(int(src[i]), int(dst[i]))
+    single_s = time.perf_counter() - t1
+    top.close()
+    value = q * steps / el
+    cpu = None if args.no_cpu_baseline else cpu_lookup_baseline(A, args.cpu_seconds)
+    line = {"metric": "per-packet lookups through the drop-in (topology_getPathInfoBatch), queries/s",
+            "value": round(value, 1), "unit": "queries/s", "n_gpus": 1, "steps": steps,
+            "ms_per_step": round(1e3 * el / steps, 3), "higher_is_better": True, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"{q} uniform (src, dst) host-address pairs per step over the {desc} table, "
+                                   f"{A} hosts attached by exact IP hint"},
+            "startup_s": {"graphml_write_untimed": round(write_s, 3), "topology_new": round(new_s, 3),
+                          "attach_all_hosts": round(attach_s, 3), "seal_table_and_mirror": round(seal_s, 3),
+                          "end_to_end": round(new_s + attach_s + seal_s, 3)},
+            "single_call_queries_per_s": round(ns / single_s, 1),
+            "single_call_note": f"{ns} topology_getPathInfo calls through ctypes (Python call overhead included)",
+            "cpu_baseline": cpu}
+    if cpu:
+        line["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)
+    print(json.dumps(line), flush=True)
+
+
 def bench_fw(args):
     """C2 on the FW engine (SPE_ENGINE_FW): the north star's dense algorithm -- a
     blocked min-plus Floyd-Warshall closure carrying (latency, reliability, first
@@ -668,6 +742,9 @@ SIDE_CONFIGS = (
     ("c1", ["--config", "c1", "--cpu-seconds", "4", "--cpu-sources", "0"]),
     ("c2fw", ["--config", "c2fw", "--steps", "1"]),   # the FW engine's whole C2 table
     ("c5_on_c4", ["--config", "c5", "--c5-table", "c4", "--steps", "10", "--warmup", "2", "--cpu-seconds", "6"]),
+    # the drop-in end to end: GraphML -> topology_new -> attach -> seal, then batched lookups
+    ("c3_shim", ["--config", "c3shim", "--steps", "3", "--cpu-seconds", "4", "--queries", "20000000"]),
+    ("c4_shim", ["--config", "c4shim", "--steps", "2", "--cpu-seconds", "4", "--queries", "20000000"]),
 )
 
 
@@ -888,6 +965,8 @@ def main():
         return bench_complete(args)
     if args.config == "c2fw":
         return bench_fw(args)
+    if args.config in ("c3shim", "c4shim"):
+        return bench_shim(args, args.config[:2])
     if args.inproc > 0:
         return bench_inproc(args, args.inproc, args.config)
 

@@ -78,6 +78,22 @@ void SHD_TOPO(topology_incrementPathPacketCounter)(Topology* top, spe_in_addr_t 
 int32_t SHD_TOPO(topology_getPathInfo)(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress, double* latency,
                              double* reliability);
 
+/* A whole round of packets at once (no reference counterpart: Shadow's workers
+ * ask per packet, shd-worker.c:235-247).  For i < n: routable[i], latency[i] and
+ * reliability[i] exactly as topology_getPathInfo(src[i], dst[i]) would answer,
+ * with the same path-cache bookkeeping per query, in order; the table reads of a
+ * batch of n >= 256 (n >= 4096 when the whole table is mirrored on the host) go to
+ * ONE device lookup launch (spe_lookup_batch_host), smaller ones to the host
+ * mirror / single reads.  Returns the number of
+ * routable pairs, -1 on bad arguments. */
+int64_t SHD_TOPO(topology_getPathInfoBatch)(Topology* top, int64_t n, const spe_in_addr_t* srcAddress,
+                                  const spe_in_addr_t* dstAddress, double* latency, double* reliability,
+                                  uint8_t* routable);
+/* topology_incrementPathPacketCounter for n (src, dst) pairs (e.g. the delivered
+ * packets of a round), each counted on the Path its query hits. */
+void SHD_TOPO(topology_incrementPathPacketCounterBatch)(Topology* top, int64_t n, const spe_in_addr_t* srcAddress,
+                                              const spe_in_addr_t* dstAddress);
+
 /* engine hooks (callbacks run on the calling thread, some inside the topology's
  * locks: they must not call back into the topology) */
 void SHD_TOPO(topology_set_log_callback)(Topology* top, topology_log_fn fn, void* ctx);

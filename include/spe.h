@@ -17,6 +17,7 @@
  *                        for every source row                              shd-topology.c:1530-1912
  *   spe_table_get        _topology_getPathEntry + path_getLatency/Reliability shd-topology.c:1952-2070
  *   spe_lookup_batch     3 x _topology_getPathEntry per packet (shd-worker.c:235,243,247), batched
+ *   spe_lookup_batch_host  the same from host arrays (the shim's topology_getPathInfoBatch)
  *   spe_table_min_latency top->minimumPathLatency -> worker_updateMinTimeJump shd-topology.c:1359-1370
  *   spe_last_error       the critical()/warning() log lines of the reference
  *
@@ -107,6 +108,9 @@ typedef struct spe_graph_info {
     int32_t n_relax_vertices;       /* vertices the relaxation runs on: undirected pendant
                                      * vertices (one neighbour) are one edge off their anchor
                                      * and need no relaxation state */
+    int32_t sums_exact;             /* every latency is k / 2^q with every path sum below 2^53:
+                                     * every f64 path sum is exact, so shared / derived rows
+                                     * (spe_table_opts.exact_sources = 0) are bit-exact too */
 } spe_graph_info;
 
 typedef struct spe_table_opts {
@@ -384,6 +388,13 @@ int spe_lookup_batch(const spe_table* t, const int32_t* d_pairs, int64_t q, doub
 int spe_lookup_batch_replica(const spe_table* t, int32_t replica, const int32_t* d_pairs, int64_t q,
                              double* d_latency, double* d_reliability, uint8_t* d_ok, void* stream);
 int spe_table_replica_device(const spe_table* t, int32_t replica, int32_t* device);
+/* spe_lookup_batch with HOST arrays (pairs: q (s_slot, t_slot) int32 pairs): the
+ * batch is staged through pinned buffers to the home replica and answered there,
+ * in chunks of 4M queries, synchronously.  For a host caller (the topology shim's
+ * topology_getPathInfoBatch) that resolves a round of packets at once instead of
+ * one device read per query.  Thread-safe (callers are serialised per table). */
+int spe_lookup_batch_host(const spe_table* t, const int32_t* pairs, int64_t q, double* latency,
+                          double* reliability, uint8_t* ok);
 
 /* Whole-table self-check on the device (every (s, t) entry, s != t, of a built
  * single-device table owning every row): the consequences of the reference's

@@ -3665,6 +3665,24 @@ struct spe_table {
     uint8_t* d_sunsafe = nullptr;  // per source slot of the batch: a derived row's margin failed
     uint8_t* h_sunsafe = nullptr;
     bool derive = false;           // contracted sources take their neighbours' roots (no lane)
+    // spe_lookup_batch_host / spe_table_get: device + pinned staging, grown on demand,
+    // one caller at a time (the topology shim queries from several worker threads)
+    struct HostLookup {
+        std::mutex mu;
+        int32_t device = -1;
+        hipStream_t stream = nullptr;
+        int64_t cap = 0;
+        int2* d_pairs = nullptr;
+        double* d_lat = nullptr;
+        double* d_rel = nullptr;
+        uint8_t* d_ok = nullptr;
+        int2* h_pairs = nullptr;
+        double* h_lat = nullptr;
+        double* h_rel = nullptr;
+        uint8_t* h_ok = nullptr;
+        unsigned char* h_entry = nullptr;   // spe_table_get: 16 + 4 + 2 B read back with one sync
+    };
+    HostLookup* hlk = new HostLookup();
 };
 
 namespace {
@@ -4061,6 +4079,7 @@ int spe_graph_info_get(const spe_graph* g, spe_graph_info* out) {
     out->parallel_latency_differs = g->hg.multi_rep;
     out->weight_floor_ok = g->hg.weight_floor_ok;
     out->device = g->device;
+    out->sums_exact = g->hg.share.eligible && g->hg.share.exact;
     return SPE_OK;
 }
 
@@ -5442,6 +5461,44 @@ int spe_table_layout_get(const spe_table* t, spe_table_layout* out) {
     return SPE_OK;
 }
 
+}  // extern "C"
+
+// Staging of the host-side lookups (caller holds h->mu): a stream on `device` and
+// room for `q` queries (0: only the single-entry buffer).
+static int host_lookup_reserve(spe_table::HostLookup* h, int32_t device, int64_t q) {
+    if (h->device < 0) {
+        HIP_TRY(hipSetDevice(device));
+        HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        HIP_TRY(hipHostMalloc((void**)&h->h_entry, 64, hipHostMallocDefault));
+        h->device = device;
+    }
+    HIP_TRY(hipSetDevice(h->device));
+    if (q <= h->cap) return SPE_OK;
+    for (void* p : {(void*)h->d_pairs, (void*)h->d_lat, (void*)h->d_rel, (void*)h->d_ok})
+        if (p) HIP_TRY(hipFree(p));
+    for (void* p : {(void*)h->h_pairs, (void*)h->h_lat, (void*)h->h_rel, (void*)h->h_ok})
+        if (p) HIP_TRY(hipHostFree(p));
+    h->d_pairs = nullptr;
+    h->d_lat = h->d_rel = nullptr;
+    h->d_ok = nullptr;
+    h->h_pairs = nullptr;
+    h->h_lat = h->h_rel = nullptr;
+    h->h_ok = nullptr;
+    h->cap = 0;
+    HIP_TRY(hipMalloc(&h->d_pairs, (size_t)q * sizeof(int2)));
+    HIP_TRY(hipMalloc(&h->d_lat, (size_t)q * sizeof(double)));
+    HIP_TRY(hipMalloc(&h->d_rel, (size_t)q * sizeof(double)));
+    HIP_TRY(hipMalloc(&h->d_ok, (size_t)q));
+    HIP_TRY(hipHostMalloc((void**)&h->h_pairs, (size_t)q * sizeof(int2), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&h->h_lat, (size_t)q * sizeof(double), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&h->h_rel, (size_t)q * sizeof(double), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&h->h_ok, (size_t)q, hipHostMallocDefault));
+    h->cap = q;
+    return SPE_OK;
+}
+
+extern "C" {
+
 int spe_table_get(const spe_table* t, int32_t s_slot, int32_t t_slot, spe_entry* out) {
     if (!t || !out) return fail(SPE_EINVAL, "NULL argument");
     if (t->multi) {
@@ -5454,13 +5511,22 @@ int spe_table_get(const spe_table* t, int32_t s_slot, int32_t t_slot, spe_entry*
     if (!t->blk_built[(size_t)(sb - t->blk0)]) return fail(SPE_ESTATE, "source row not built");
     HIP_TRY(hipSetDevice(t->g->device));
     const size_t o = ((size_t)(sb - t->blk0) * t->A + t_slot) * WAVE + (s_slot % WAVE);
-    uint16_t h = 0;
+    // the three fields read back into pinned memory on one stream, one synchronisation
+    spe_table::HostLookup* hl = t->hlk;
+    std::lock_guard<std::mutex> lock(hl->mu);
+    if (int r = host_lookup_reserve(hl, t->g->device, 0)) return r;
+    unsigned char* b = hl->h_entry;
+    HIP_TRY(hipMemcpyAsync(b, t->tb.lr + o, sizeof(double2), hipMemcpyDeviceToHost, hl->stream));
+    HIP_TRY(hipMemcpyAsync(b + 16, t->tb.next + o, sizeof(int32_t), hipMemcpyDeviceToHost, hl->stream));
+    HIP_TRY(hipMemcpyAsync(b + 20, t->tb.hops + o, sizeof(uint16_t), hipMemcpyDeviceToHost, hl->stream));
+    HIP_TRY(hipStreamSynchronize(hl->stream));
     double2 e;
-    HIP_TRY(hipMemcpy(&e, t->tb.lr + o, sizeof(double2), hipMemcpyDeviceToHost));
+    uint16_t h = 0;
+    std::memcpy(&e, b, sizeof e);
+    std::memcpy(&out->next_hop, b + 16, sizeof(int32_t));
+    std::memcpy(&h, b + 20, sizeof h);
     out->latency = e.x;
     out->reliability = e.y;
-    HIP_TRY(hipMemcpy(&out->next_hop, t->tb.next + o, sizeof(int32_t), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(&h, t->tb.hops + o, sizeof(uint16_t), hipMemcpyDeviceToHost));
     out->hops = h;
     return SPE_OK;
 }
@@ -5593,6 +5659,37 @@ int spe_lookup_batch_replica(const spe_table* t, int32_t replica, const int32_t*
                                                            d_latency, d_reliability, d_ok);
     HIP_TRY(hipGetLastError());
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
+    return SPE_OK;
+}
+
+int spe_lookup_batch_host(const spe_table* t, const int32_t* pairs, int64_t q, double* latency, double* reliability,
+                          uint8_t* ok) {
+    if (!t || q < 0 || (q > 0 && (!pairs || !latency || !reliability || !ok))) return fail(SPE_EINVAL, "bad arguments");
+    if (!t->built) return fail(SPE_ESTATE, "table not built");
+    if (q == 0) return SPE_OK;
+    int32_t dev = 0;
+    if (int r = spe_table_replica_device(t, 0, &dev)) return r;
+    spe_table::HostLookup* h = t->hlk;
+    std::lock_guard<std::mutex> lock(h->mu);
+    // chunks of up to 4M queries through pinned staging: H2D pairs, k_lookup on the
+    // home replica, D2H answers, one synchronisation per chunk
+    const int64_t chunk = std::min<int64_t>(q, (int64_t)1 << 22);
+    if (int r = host_lookup_reserve(h, dev, chunk)) return r;
+    for (int64_t i0 = 0; i0 < q; i0 += chunk) {
+        const int64_t n = std::min(chunk, q - i0);
+        std::memcpy(h->h_pairs, pairs + 2 * i0, (size_t)n * sizeof(int2));
+        HIP_TRY(hipMemcpyAsync(h->d_pairs, h->h_pairs, (size_t)n * sizeof(int2), hipMemcpyHostToDevice, h->stream));
+        if (int r = spe_lookup_batch_replica(t, 0, (const int32_t*)h->d_pairs, n, h->d_lat, h->d_rel, h->d_ok,
+                                             h->stream))
+            return r;
+        HIP_TRY(hipMemcpyAsync(h->h_lat, h->d_lat, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->h_rel, h->d_rel, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->h_ok, h->d_ok, (size_t)n, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        std::memcpy(latency + i0, h->h_lat, (size_t)n * sizeof(double));
+        std::memcpy(reliability + i0, h->h_rel, (size_t)n * sizeof(double));
+        std::memcpy(ok + i0, h->h_ok, (size_t)n);
+    }
     return SPE_OK;
 }
 
@@ -6007,8 +6104,24 @@ int spe_table_load(spe_table* t, const char* path) {
     return rc;
 }
 
+static void host_lookup_free(spe_table::HostLookup* h) {
+    if (!h) return;
+    if (h->device >= 0) {
+        (void)hipSetDevice(h->device);
+        if (h->stream) (void)hipStreamSynchronize(h->stream);
+        for (void* p : {(void*)h->d_pairs, (void*)h->d_lat, (void*)h->d_rel, (void*)h->d_ok})
+            if (p) (void)hipFree(p);
+        for (void* p : {(void*)h->h_pairs, (void*)h->h_lat, (void*)h->h_rel, (void*)h->h_ok, (void*)h->h_entry})
+            if (p) (void)hipHostFree(p);
+        if (h->stream) (void)hipStreamDestroy(h->stream);
+    }
+    delete h;
+}
+
 void spe_table_free(spe_table* t) {
     if (!t) return;
+    host_lookup_free(t->hlk);
+    t->hlk = nullptr;
     if (t->multi) {
         spe::multi_free(t->multi);
         delete t;

@@ -47,6 +47,8 @@
 #define topology_free spe_topology_free
 #define topology_getLatency spe_topology_getLatency
 #define topology_getPathInfo spe_topology_getPathInfo
+#define topology_getPathInfoBatch spe_topology_getPathInfoBatch
+#define topology_incrementPathPacketCounterBatch spe_topology_incrementPathPacketCounterBatch
 #define topology_getReliability spe_topology_getReliability
 #define topology_incrementPathPacketCounter spe_topology_incrementPathPacketCounter
 #define topology_isRoutable spe_topology_isRoutable
@@ -112,10 +114,14 @@ struct _Topology {
     int32_t directed;
     int32_t prefer_direct;
     int32_t complete;
+    int32_t sums_exact;            /* spe_graph_info.sums_exact: shared rows are bit-exact too */
     /* graph, edge list form (GraphML order) */
     int32_t *esrc, *edst;
     double *elat, *eloss;
     char** vstr[VS_COUNT];     /* NULL array = attribute absent from the graph */
+    uint32_t* vip;             /* [n] address_stringToIP of each vertex's "ip" (INADDR_NONE when absent) */
+    uint64_t* vip_index;       /* (ip << 32 | v) of every vertex with a usable ip, sorted: exact hints in O(log n) */
+    int64_t n_vip;
     double* vnum[VN_COUNT];
     spe_graph* graph;
 
@@ -634,6 +640,17 @@ static int strongly_connected(const Topology* top) {
 
 /* --------------------------------------------------------- lifecycle */
 
+static uint32_t string_to_ip(const char* s) {   /* address_stringToIP, shd-address.c:137-144 */
+    struct in_addr a;
+    if (s && inet_pton(AF_INET, s, &a) == 1) return a.s_addr;
+    return INADDR_NONE;
+}
+
+static int cmp_u64(const void* a, const void* b) {
+    const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : x > y;
+}
+
 static void snap_free(Snap* s) {
     if (!s) return;
     if (s->table) spe_table_free(s->table);
@@ -660,6 +677,7 @@ static void topo_release(Topology* top) {
         }
     for (int a = 0; a < VN_COUNT; ++a) free(top->vnum[a]);
     free(top->esrc); free(top->edst); free(top->elat); free(top->eloss);
+    free(top->vip); free(top->vip_index);
     free(top->ip_keys); free(top->ip_vals); free(top->ip_used);
     free(top->is_attached); free(top->attached);
     free((void*)top->run_seq);
@@ -716,6 +734,7 @@ Topology* topology_new_on_device(const char* graphPath, int32_t device) {
     spe_graph_info info = SPE_STRUCT_INIT(spe_graph_info);
     spe_graph_info_get(top->graph, &info);
     top->complete = info.complete;
+    top->sums_exact = info.sums_exact;
     if (!info.weight_floor_ok)   /* outside the bit-exactness argument */
         tlog(top, LOG_WARNING, "some edge latency is below ulp(path latency)/2: a relaxation could leave a "
                                "distance unchanged (fl(d + w) == d); routes are exact only when every "
@@ -723,6 +742,16 @@ Topology* topology_new_on_device(const char* graphPath, int32_t device) {
     tlog(top, LOG_MESSAGE, "topology graph is %s, %s, and strongly connected with 1 cluster. It does%s prefer "
                            "direct paths.", info.complete ? "complete" : "incomplete",
          top->directed ? "directed" : "undirected", top->prefer_direct ? "" : " not");
+    /* every vertex's ip parsed once; the usable ones indexed by (ip, vertex) */
+    top->vip = malloc(((size_t)top->n + 1) * sizeof(uint32_t));
+    top->vip_index = malloc(((size_t)top->n + 1) * sizeof(uint64_t));
+    for (int32_t v = 0; v < top->n; ++v) {
+        const uint32_t ip = string_to_ip(top->vstr[VS_IP] ? top->vstr[VS_IP][v] : NULL);
+        top->vip[v] = ip;
+        if (ip != INADDR_NONE && ip != INADDR_ANY && ip != INADDR_LOOPBACK)
+            top->vip_index[top->n_vip++] = ((uint64_t)ip << 32) | (uint32_t)v;
+    }
+    qsort(top->vip_index, (size_t)top->n_vip, sizeof(uint64_t), cmp_u64);
     top->ip_cap = 1024;
     top->ip_keys = calloc(top->ip_cap, sizeof(uint32_t));
     top->ip_vals = calloc(top->ip_cap, sizeof(int32_t));
@@ -836,12 +865,6 @@ static void ip_del(Topology* top, uint32_t ip) {
 
 /* ---------------------------------------------------------- attachment */
 
-static uint32_t string_to_ip(const char* s) {   /* address_stringToIP, shd-address.c:137-144 */
-    struct in_addr a;
-    if (s && inet_pton(AF_INET, s, &a) == 1) return a.s_addr;
-    return INADDR_NONE;
-}
-
 typedef struct {
     int32_t* q;
     size_t n;
@@ -875,23 +898,39 @@ static int32_t find_attachment_vertex(Topology* top, topology_random_fn rnd, voi
             requestedIP = ip;
         }
     }
+    if (requestedUsable && top->vip_index) {
+        /* Vertices whose ip equals the hint: the scan below would clear every queue at
+         * the first of them and keep exactly these, in vertex order, then pick one at
+         * random (no longest-prefix match once an exact one was found).  The sorted
+         * index finds them without the O(n) scan (a 100k-host attach on a 200k-vertex
+         * graph would otherwise be 2e10 string compares). */
+        int64_t lo = 0, hi = top->n_vip;
+        const uint64_t key = (uint64_t)requestedIP << 32;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) / 2;
+            if (top->vip_index[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        int64_t e = lo;
+        while (e < top->n_vip && (uint32_t)(top->vip_index[e] >> 32) == requestedIP) ++e;
+        if (e > lo) {
+            const double r = rnd ? rnd(rctx) : 0.0;
+            const int indexRange = (int)(e - lo) - 1;
+            int idx = (int)round((double)(indexRange * r));   /* :2310-2316 */
+            if (idx < 0) idx = 0;
+            if (idx > indexRange) idx = indexRange;
+            return (int32_t)(uint32_t)top->vip_index[lo + idx];
+        }
+    }
     for (int32_t v = 0; v < top->n; ++v) {
-        const char* ipS = top->vstr[VS_IP] ? top->vstr[VS_IP][v] : NULL;
         const char* city = top->vstr[VS_CITYCODE] ? top->vstr[VS_CITYCODE][v] : NULL;
         const char* country = top->vstr[VS_COUNTRYCODE] ? top->vstr[VS_COUNTRYCODE][v] : NULL;
         const char* geo = top->vstr[VS_GEOCODE] ? top->vstr[VS_GEOCODE][v] : NULL;
         const char* type = top->vstr[VS_TYPE] ? top->vstr[VS_TYPE][v] : NULL;
         const int cityM = str_match(city, cityHint), countryM = str_match(country, countryHint);
         const int geoM = str_match(geo, geoHint), typeM = str_match(type, typeHint);
-        int usable = 0;
-        uint32_t vip = INADDR_NONE;
-        if (ipS && ipS[0] != '\0') {
-            const uint32_t ip = string_to_ip(ipS);
-            if (ip != INADDR_NONE && ip != INADDR_ANY && ip != INADDR_LOOPBACK) {
-                usable = 1;
-                vip = ip;
-            }
-        }
+        const uint32_t vip = top->vip[v];
+        const int usable = vip != INADDR_NONE && vip != INADDR_ANY && vip != INADDR_LOOPBACK;
         if (requestedUsable && usable && vip == requestedIP) {
             if (!foundExact)   /* g_queue_clear on every queue; the numIPs counters are kept */
                 for (int i = 0; i < C_N; ++i) c[i].n = 0;
@@ -925,7 +964,7 @@ static int32_t find_attachment_vertex(Topology* top, topology_random_fn rnd, voi
             uint32_t best = 0;
             for (size_t i = 0; i < pick->n; ++i) {
                 const int32_t v = pick->q[i];
-                const uint32_t vip = string_to_ip(top->vstr[VS_IP] ? top->vstr[VS_IP][v] : NULL);
+                const uint32_t vip = top->vip[v];
                 const uint32_t match = vip & requestedIP;
                 if (match > best) {
                     best = match;
@@ -997,10 +1036,12 @@ static int64_t env_bytes(const char* name, int64_t dflt) {
     return (s && *s) ? (int64_t)strtoll(s, NULL, 10) : dflt;
 }
 
-/* Build a table over `att` (A vertices) and its host-side view. */
-/* Host-mirror budget: SHADOW_SPE_MIRROR_BYTES, else min(8 GiB, a quarter of the
- * host's available memory) -- a re-seal holds the old snapshot's mirror while the
- * new one is filled, so the caller subtracts what the published snapshot holds. */
+/* Host-mirror budget: SHADOW_SPE_MIRROR_BYTES, else min(48 GiB, half of the host's
+ * available memory) -- the whole record span of a 50k-host table (40 GB) where the
+ * host has the room.  A re-seal fills the new mirror while the published one is
+ * still held: MemAvailable already excludes what it holds, a fixed cap does not,
+ * so `held` is subtracted from a fixed cap only (*fixed = 1) and handed back to
+ * the new snapshot once the old one is freed (topology_seal). */
 static int64_t mem_available_bytes(void) {
     FILE* f = fopen("/proc/meminfo", "r");
     if (!f) return -1;
@@ -1012,11 +1053,13 @@ static int64_t mem_available_bytes(void) {
     return kb < 0 ? -1 : kb * 1024;
 }
 
-static int64_t mirror_budget_default(void) {
-    int64_t b = (int64_t)8 << 30;
+static int64_t mirror_budget(int64_t held, int* fixed) {
+    const char* e = getenv("SHADOW_SPE_MIRROR_BYTES");
     const int64_t avail = mem_available_bytes();
-    if (avail > 0 && avail / 4 < b) b = avail / 4;
-    return env_bytes("SHADOW_SPE_MIRROR_BYTES", b);
+    *fixed = (e && *e) || avail <= 0;
+    if (*fixed) return env_bytes("SHADOW_SPE_MIRROR_BYTES", (int64_t)8 << 30) - held;
+    const int64_t cap = (int64_t)48 << 30;
+    return avail / 2 < cap ? avail / 2 : cap;
 }
 
 /* bytes of host mirror a snapshot holds */
@@ -1063,11 +1106,18 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
      * engine the graph does not fit falls back to the library's choice */
     const char* eng = getenv("SHADOW_SPE_ENGINE");
     if (eng && *eng) o.engine = (int32_t)strtol(eng, NULL, 10);
-    /* SHADOW_SPE_EXACT_SOURCES=1: every pendant host relaxes on its own lane, so its
-     * latencies are the reference's path-order sums bit for bit (default: hosts on
-     * one anchor share its relaxation, latency / reliability within a few ulps) */
+    /* Every host on its own relaxation lane unless every path sum is exact in f64.
+     * Shadow turns a latency into simulated time as ceil(latency * 1e6) ns
+     * (shd-worker.c:244), and real topologies carry decimal latencies (the shipped
+     * one: 5.0 .. 2293.85 ms), whose products sit on or next to an integer: the few
+     * ulps by which a shared / derived row differs from the path-order sum
+     *  would move a delivery by 1 ns.  So the drop-in's default is
+     * bit-exact: shared anchor trees and derived rows only where sums are exact
+     * (spe_graph_info.sums_exact; e.g. integer latencies), where they are bit-exact
+     * as well.  SHADOW_SPE_EXACT_SOURCES=0 / 1 overrides it either way. */
     const char* ex = getenv("SHADOW_SPE_EXACT_SOURCES");
-    if (ex && *ex && strcmp(ex, "0") != 0) o.exact_sources = 1;
+    o.exact_sources = top->sums_exact ? 0 : 1;
+    if (ex && *ex) o.exact_sources = strcmp(ex, "0") != 0;
     int rc = spe_table_create(top->graph, s->attached, A, &o, &s->table);
     if (rc == SPE_EUNSUPPORTED && o.engine != SPE_ENGINE_AUTO) {
         o.engine = SPE_ENGINE_AUTO;
@@ -1090,9 +1140,10 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
         if (rc == SPE_OK && cpath[0] && spe_table_save(s->table, cpath) != SPE_OK)
             tlog(top, LOG_WARNING, "could not save the path table cache: %s", spe_last_error());
     }
-    /* host view: the whole table when it fits the mirror budget (mirror_budget_default:
-     * 8 GiB holds A <= 23k), else 64-source blocks mirrored on first use within that
-     * budget, then single-entry device reads (spe_table_get) */
+    /* host view: the whole table when it fits the mirror budget (mirror_budget: up to
+     * 48 GiB, A <= 56k), else 64-source blocks mirrored on first use within that
+     * budget, then single-entry device reads (spe_table_get); batches of queries
+     * read the device table in one launch (topology_getPathInfoBatch) */
     if (budget < 0) budget = 0;
     s->mirror_budget = budget;
     const int64_t full = (int64_t)A * A * 16;
@@ -1126,6 +1177,8 @@ int32_t topology_seal(Topology* top) {
     if (att) memcpy(att, top->attached, (size_t)A * sizeof(int32_t));
     pthread_rwlock_unlock(&top->state_lock);
     int rc = SPE_OK;
+    int64_t held = 0;
+    int fixed = 0;
     if (!fresh) {
         Snap* s = NULL;
         if (A == 0) {
@@ -1134,9 +1187,9 @@ int32_t topology_seal(Topology* top) {
             const double t0 = now_s();
             /* the published snapshot's mirror stays allocated until the swap below */
             pthread_rwlock_rdlock(&top->state_lock);
-            const int64_t held = snap_mirror_bytes(top->snap);
+            held = snap_mirror_bytes(top->snap);
             pthread_rwlock_unlock(&top->state_lock);
-            rc = snap_build(top, att, A, mirror_budget_default() - held, &s);   /* no lock held: queries on the old table go on */
+            rc = snap_build(top, att, A, mirror_budget(held, &fixed), &s);   /* no lock held: queries on the old table go on */
             if (rc == SPE_OK) {
                 top->build_seconds += now_s() - t0;
                 top->build_rows += A;
@@ -1148,6 +1201,10 @@ int32_t topology_seal(Topology* top) {
             top->snap = s;
             pthread_rwlock_unlock(&top->state_lock);
             snap_free(old);
+            if (fixed && held > 0 && s->blocks) {   /* the old mirror's bytes are free again */
+                atomic_fetch_add(&s->row_budget, held);
+                s->mirror_budget += held;
+            }
             /* worker_updateMinTimeJump(minimumPathLatency), shd-topology.c:1359-1370: on the
              * querying (worker) thread, as the reference requires */
             if (top->cache_mode == TOPOLOGY_ANSWER_ROWS && top->minlat_fn && s->min_latency > 0)
@@ -1571,6 +1628,144 @@ int32_t topology_isRoutable(Topology* top, spe_in_addr_t srcAddress, spe_in_addr
 void topology_incrementPathPacketCounter(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {
     double l, r;
     query(top, srcAddress, dstAddress, 1, &l, &r, NULL);   /* path->packetCount++, shd-path.c:53-56 */
+}
+
+/* Batches (worker_sendPacket's lookups for a whole round of packets).  Under
+ * state_lock shared: every address resolved, and a published table that holds
+ * them all (else the lock is dropped, a covering table sealed, and the batch
+ * retried).  Returns the snapshot, or NULL with the lock released when a seal
+ * failed. */
+static Snap* batch_snapshot(Topology* top, int64_t n, const spe_in_addr_t* src, const spe_in_addr_t* dst) {
+    for (int attempt = 0; attempt < 64; ++attempt) {
+        pthread_rwlock_rdlock(&top->state_lock);
+        Snap* sn = top->snap;
+        int covered = sn != NULL;
+        for (int64_t i = 0; i < n && covered; ++i) {
+            const int32_t sv = ip_get(top, src[i]), dv = ip_get(top, dst[i]);
+            if (sv >= 0 && dv >= 0) covered = sn->slot_of_vertex[sv] >= 0 && sn->slot_of_vertex[dv] >= 0;
+        }
+        if (covered) return sn;
+        pthread_rwlock_unlock(&top->state_lock);
+        if (topology_seal(top) != SPE_OK) return NULL;
+    }
+    return NULL;
+}
+
+static void batch_bad_address(Topology* top, int32_t sv, uint32_t src, uint32_t dst) {
+    struct in_addr a = {sv < 0 ? src : dst};
+    tlog(top, LOG_CRITICAL, "invalid vertex, %s address %s is not connected to topology",
+         sv < 0 ? "source" : "destination", inet_ntoa(a));
+}
+
+static void batch_min_callback(Topology* top, int min_updated) {
+    if (min_updated && top->minlat_fn) {   /* worker_updateMinTimeJump, :1369 */
+        double m;
+        const uint64_t b = atomic_load(&top->stored_min_bits);
+        memcpy(&m, &b, sizeof m);
+        top->minlat_fn(m, top->minlat_ctx);
+    }
+}
+
+int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t* srcAddress,
+                                  const spe_in_addr_t* dstAddress, double* latency, double* reliability,
+                                  uint8_t* routable) {
+    if (!top || n < 0 || (n > 0 && (!srcAddress || !dstAddress || !latency || !reliability || !routable))) return -1;
+    if (n == 0) return 0;
+    for (int64_t i = 0; i < n; ++i) {
+        latency[i] = reliability[i] = -1.0;
+        routable[i] = 0;
+    }
+    Snap* sn = batch_snapshot(top, n, srcAddress, dstAddress);
+    if (!sn) return -1;
+    /* the cache model per query (which Path answers it, the stores a miss makes,
+     * the log lines), then every table read of the batch at once: from the host
+     * mirror, or one device lookup launch for the lot (spe_lookup_batch_host) */
+    /* (random reads of a whole-table host mirror cost ~100 ns each; one device launch
+     * for a large batch costs ~25 B of PCIe traffic per query) */
+    const int dev = n >= (sn->mlat ? 4096 : 256);
+    int32_t* pairs = dev ? malloc((size_t)n * 2 * sizeof(int32_t)) : NULL;
+    int64_t* at = dev ? malloc((size_t)n * sizeof(int64_t)) : NULL;
+    int64_t nd = 0;
+    int min_updated = 0;
+    const int ref = top->cache_mode == TOPOLOGY_ANSWER_REFERENCE;
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t sv = ip_get(top, srcAddress[i]), dv = ip_get(top, dstAddress[i]);
+        if (sv < 0 || dv < 0) {
+            batch_bad_address(top, sv, srcAddress[i], dstAddress[i]);
+            continue;
+        }
+        int32_t x, y, kind = K_NONE;
+        const int found = cache_lookup(top, sn, sv, dv, &x, &y, &kind, &min_updated);
+        int32_t s = sn->slot_of_vertex[sv], t = sn->slot_of_vertex[dv];
+        if (ref) {
+            if (!found) {   /* :2023-2029 */
+                tlog(top, LOG_ERROR, "unable to find path between vertex %d (%s) and vertex %d (%s)", sv,
+                     top->vstr[VS_ID][sv], dv, top->vstr[VS_ID][dv]);
+                continue;
+            }
+            if (kind == K_SELF) {
+                spe_entry e;
+                spe_graph_self_path(top->graph, x, &e);
+                latency[i] = e.latency;
+                reliability[i] = e.reliability;
+                continue;
+            }
+            s = sn->slot_of_vertex[x];
+            t = sn->slot_of_vertex[y];
+        }
+        if (dev) {
+            pairs[2 * nd] = s;
+            pairs[2 * nd + 1] = t;
+            at[nd++] = i;
+        } else {
+            snap_value(top, sn, s, t, &latency[i], &reliability[i]);
+        }
+    }
+    if (nd > 0) {
+        double* lr = malloc((size_t)nd * 2 * sizeof(double));
+        uint8_t* okd = malloc((size_t)nd);
+        if (lr && okd && spe_lookup_batch_host(sn->table, pairs, nd, lr, lr + nd, okd) == SPE_OK) {
+            for (int64_t k = 0; k < nd; ++k) {
+                latency[at[k]] = lr[k];
+                reliability[at[k]] = lr[nd + k];
+            }
+        } else {   /* per query */
+            tlog(top, LOG_WARNING, "batched path table read failed (%s): reading per query", spe_last_error());
+            for (int64_t k = 0; k < nd; ++k)
+                snap_value(top, sn, pairs[2 * k], pairs[2 * k + 1], &latency[at[k]], &reliability[at[k]]);
+        }
+        free(lr);
+        free(okd);
+    }
+    pthread_rwlock_unlock(&top->state_lock);
+    free(pairs);
+    free(at);
+    batch_min_callback(top, min_updated);
+    int64_t nok = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        routable[i] = latency[i] > -1.0;
+        nok += routable[i];
+    }
+    return nok;
+}
+
+void topology_incrementPathPacketCounterBatch(Topology* top, int64_t n, const spe_in_addr_t* srcAddress,
+                                              const spe_in_addr_t* dstAddress) {
+    if (!top || n <= 0 || !srcAddress || !dstAddress) return;
+    Snap* sn = batch_snapshot(top, n, srcAddress, dstAddress);
+    if (!sn) return;
+    int min_updated = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t sv = ip_get(top, srcAddress[i]), dv = ip_get(top, dstAddress[i]);
+        if (sv < 0 || dv < 0) {
+            batch_bad_address(top, sv, srcAddress[i], dstAddress[i]);
+            continue;
+        }
+        int32_t x, y, kind = K_NONE;
+        if (cache_lookup(top, sn, sv, dv, &x, &y, &kind, &min_updated)) pair_count(top, x, y, 1);
+    }
+    pthread_rwlock_unlock(&top->state_lock);
+    batch_min_callback(top, min_updated);
 }
 
 uint64_t topology_path_packet_count(Topology* top, spe_in_addr_t srcAddress, spe_in_addr_t dstAddress) {

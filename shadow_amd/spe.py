@@ -64,7 +64,7 @@ class GraphInfo(_Sized):
     _fields_ = [("struct_size", C.c_uint32), ("n_vertices", C.c_int32), ("n_edges", C.c_int64), ("n_relax_entries", C.c_int64),
                 ("directed", C.c_int32), ("prefer_direct", C.c_int32), ("complete", C.c_int32),
                 ("parallel_latency_differs", C.c_int32), ("weight_floor_ok", C.c_int32), ("device", C.c_int32),
-                ("n_relax_vertices", C.c_int32)]
+                ("n_relax_vertices", C.c_int32), ("sums_exact", C.c_int32)]
 
 
 class TableOpts(_Sized):
@@ -126,7 +126,8 @@ EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_
            "spe_table_key", "spe_table_save", "spe_table_load", "spe_table_free",
            "spe_graph_set_edge_aux", "spe_table_download_aux", "spe_fw_apsp", "spe_fw_closure", "spe_graph_self_path",
            "spe_graph_adjacent", "spe_device_shares", "spe_graph_edge", "spe_table_source_tree",
-           "spe_device_split", "spe_lookup_batch_replica", "spe_table_replica_device", "spe_table_check"]
+           "spe_device_split", "spe_lookup_batch_replica", "spe_table_replica_device", "spe_table_check",
+           "spe_lookup_batch_host"]
 
 _lib = None
 
@@ -166,6 +167,7 @@ def lib():
         L.spe_lookup_batch.argtypes = [P, P, C.c_int64, P, P, P, P]
         L.spe_lookup_batch_replica.argtypes = [P, C.c_int32, P, C.c_int64, P, P, P, P]
         L.spe_table_replica_device.argtypes = [P, C.c_int32, P]
+        L.spe_lookup_batch_host.argtypes = [P, P, C.c_int64, P, P, P]
         L.spe_table_check.argtypes = [P, P]
         L.spe_device_split.argtypes = [C.c_int32, C.c_int32, C.c_double, P, P, P]
         L.spe_table_min_latency.argtypes = [P, P]
@@ -428,6 +430,16 @@ class PathTable:
         _check(lib().spe_lookup_batch_replica(self.h, int(replica), C.c_void_p(d_pairs), int(q), C.c_void_p(d_lat),
                                               C.c_void_p(d_rel), C.c_void_p(d_ok),
                                               C.c_void_p(stream) if stream else None), "spe_lookup_batch_replica")
+
+    def lookup_batch_host(self, pairs):
+        """spe_lookup_batch_host: (q, 2) int32 slot pairs (host) -> (lat, rel, ok) host arrays."""
+        pairs = np.ascontiguousarray(pairs, np.int32)
+        q = int(pairs.shape[0])
+        lat = np.empty(q, np.float64)
+        rel = np.empty(q, np.float64)
+        ok = np.empty(q, np.uint8)
+        _check(lib().spe_lookup_batch_host(self.h, _p(pairs), q, _p(lat), _p(rel), _p(ok)), "spe_lookup_batch_host")
+        return lat, rel, ok
 
     def check(self) -> dict:
         """spe_table_check: whole-table invariants counted on the device."""

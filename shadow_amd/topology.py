@@ -16,7 +16,8 @@ EXPORTS = ["topology_new", "topology_new_on_device", "topology_free", "topology_
            "topology_set_min_latency_callback", "topology_seal", "topology_vertex_count",
            "topology_attached_vertex", "topology_path_packet_count", "topology_min_path_latency",
            "topology_getPathInfo", "topology_set_log_level", "topology_set_answer_mode",
-           "topology_cached_path_count", "topology_check_graphml"]
+           "topology_cached_path_count", "topology_check_graphml", "topology_getPathInfoBatch",
+           "topology_incrementPathPacketCounterBatch"]
 ANSWER_ROWS, ANSWER_REFERENCE = 0, 1
 
 RANDOM_FN = C.CFUNCTYPE(C.c_double, C.c_void_p)
@@ -65,6 +66,9 @@ def lib():
         L.topology_set_answer_mode.restype = C.c_int32
         L.topology_check_graphml.argtypes = [C.c_char_p]
         L.topology_check_graphml.restype = C.c_int32
+        L.topology_getPathInfoBatch.argtypes = [P, C.c_int64, P, P, P, P, P]
+        L.topology_getPathInfoBatch.restype = C.c_int64
+        L.topology_incrementPathPacketCounterBatch.argtypes = [P, C.c_int64, P, P]
         L.topology_cached_path_count.argtypes = [P]
         L.topology_cached_path_count.restype = C.c_int64
         _lib = L
@@ -123,6 +127,28 @@ class Topology:
         lat, rel = C.c_double(0), C.c_double(0)
         ok = lib().topology_getPathInfo(self.h, a, b, C.byref(lat), C.byref(rel))
         return bool(ok), lat.value, rel.value
+
+    def path_info_batch(self, src, dst):
+        """topology_getPathInfoBatch: (routable u8, latency, reliability) arrays for
+        address arrays src / dst (in_addr_t values)."""
+        import numpy as np
+        s = np.ascontiguousarray(src, np.uint32)
+        d = np.ascontiguousarray(dst, np.uint32)
+        n = int(s.shape[0])
+        lat = np.empty(n, np.float64)
+        rel = np.empty(n, np.float64)
+        ok = np.empty(n, np.uint8)
+        r = lib().topology_getPathInfoBatch(self.h, n, s.ctypes.data, d.ctypes.data, lat.ctypes.data,
+                                            rel.ctypes.data, ok.ctypes.data)
+        if r < 0:
+            raise ValueError("topology_getPathInfoBatch: bad arguments")
+        return ok, lat, rel
+
+    def count_packets_batch(self, src, dst):
+        import numpy as np
+        s = np.ascontiguousarray(src, np.uint32)
+        d = np.ascontiguousarray(dst, np.uint32)
+        lib().topology_incrementPathPacketCounterBatch(self.h, int(s.shape[0]), s.ctypes.data, d.ctypes.data)
 
     def count_packet(self, a: int, b: int):
         lib().topology_incrementPathPacketCounter(self.h, a, b)

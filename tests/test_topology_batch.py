@@ -1,0 +1,136 @@
+"""The drop-in's batched entry points (include/shd_topology_spe.h):
+topology_getPathInfoBatch answers a round of packets with the same values and
+the same path-cache bookkeeping as per-packet topology_getPathInfo calls
+(shd-worker.c:235-247 asks three times per packet), reading the table with one
+device launch (spe_lookup_batch_host) when there is no whole-table host mirror;
+topology_incrementPathPacketCounterBatch counts like the per-packet call.  And
+the shim's default rows are bit-exact on decimal latencies, where Shadow's
+ceil(latency * 1e6) (shd-worker.c:244) would expose a last-ulp difference."""
+import math
+
+import numpy as np
+import pytest
+
+from shadow_amd import graphs
+
+pytestmark = pytest.mark.gpu
+
+
+def _topology(tmp_path, t, ips, name="g.graphml"):
+    from shadow_amd import topology as T
+    p = tmp_path / name
+    graphs.write_graphml(t, str(p), ips=ips)
+    return T.Topology(str(p))
+
+
+def _attach(top, ips, verts):
+    from shadow_amd import topology as T
+    addrs = []
+    for i, v in enumerate(verts):
+        a = T.ip(f"11.{i // 60000}.{(i // 250) % 240}.{i % 250 + 1}")
+        top.attach(a, ip_hint=ips[v])
+        addrs.append(a)
+    return np.array(addrs, np.uint32)
+
+
+def _case(seed=9, n=200, k=70):
+    t = graphs.gen_random_small(n, 3 * n, seed)
+    ips = [f"10.{v // 250}.{v % 250}.{1 + v % 7}" for v in range(t.n)]
+    verts = np.random.default_rng(seed).choice(t.n, k, replace=False)
+    return t, ips, verts
+
+
+@pytest.mark.parametrize("mirror", ["0", "default"])
+def test_batch_equals_single_queries_and_oracle(tmp_path, monkeypatch, mirror):
+    from oracle import Oracle
+    if mirror == "0":   # no host mirror at all: the batch reads the device table in one launch
+        monkeypatch.setenv("SHADOW_SPE_MIRROR_BYTES", "0")
+    t, ips, verts = _case()
+    top = _topology(tmp_path, t, ips)
+    addrs = _attach(top, ips, verts)
+    k = len(verts)
+    src = np.repeat(addrs, k)
+    dst = np.tile(addrs, k)
+    ok, lat, rel = top.path_info_batch(src, dst)
+    ref = Oracle(t).rows(verts, verts)
+    np.testing.assert_array_equal(lat.reshape(k, k), ref["lat"])
+    np.testing.assert_array_equal(rel.reshape(k, k), ref["rel"])
+    np.testing.assert_array_equal(ok.reshape(k, k), (ref["kind"] != 0).astype(np.uint8))
+    for i in range(0, k * k, 97):
+        assert top.path_info(int(src[i]), int(dst[i])) == (bool(ok[i]), lat[i], rel[i])
+    # unknown addresses answer -1 / not routable, like topology_getLatency
+    bad = np.array([addrs[0], 0x7F000009], np.uint32)
+    ok2, lat2, _ = top.path_info_batch(bad, bad[::-1])
+    assert list(ok2) == [0, 0] and list(lat2) == [-1.0, -1.0]
+    top.close()
+
+
+def test_batch_reference_mode_and_counts_match_single_calls(tmp_path, monkeypatch):
+    """Reference answer mode: the cached Path a query hits depends on query order;
+    a batch in order q_1..q_n equals single calls in that order.  Packet counts
+    of a batch increment equal those of single increments."""
+    monkeypatch.setenv("SHADOW_SPE_PATH_CACHE", "reference")
+    monkeypatch.setenv("SHADOW_SPE_MIRROR_BYTES", "0")
+    t, ips, verts = _case(seed=11)
+    rng = np.random.default_rng(4)
+    a = _topology(tmp_path, t, ips, "a.graphml")
+    b = _topology(tmp_path, t, ips, "b.graphml")
+    aa = _attach(a, ips, verts)
+    ab = _attach(b, ips, verts)
+    qi = rng.integers(0, len(verts), (3000, 2))
+    ok, lat, rel = a.path_info_batch(aa[qi[:, 0]], aa[qi[:, 1]])
+    single = [b.path_info(int(ab[x]), int(ab[y])) for x, y in qi]
+    assert [bool(x) for x in ok] == [s[0] for s in single]
+    np.testing.assert_array_equal(lat, [s[1] for s in single])
+    np.testing.assert_array_equal(rel, [s[2] for s in single])
+    assert a.cached_paths() == b.cached_paths()
+    ci = rng.integers(0, len(verts), (2000, 2))
+    a.count_packets_batch(aa[ci[:, 0]], aa[ci[:, 1]])
+    for x, y in ci:
+        b.count_packet(int(ab[x]), int(ab[y]))
+    for x in range(0, len(verts), 5):
+        for y in range(len(verts)):
+            assert a.packets(int(aa[x]), int(aa[y])) == b.packets(int(ab[x]), int(ab[y]))
+    a.close()
+    b.close()
+
+
+def _decimal_stub_topology(seed=5):
+    """A tiered topology (BA core + pendant stubs, several per anchor) with
+    latencies in hundredths of a millisecond, like the shipped topology's
+    (5.0 .. 2293.85 ms)."""
+    t = graphs.gen_tiered(n_core=400, n_stub=1600, n_attached=900, seed=seed)
+    rng = np.random.default_rng(seed)
+    loop = t.esrc == t.edst
+    t.elat = np.where(loop, t.elat, rng.integers(500, 229385, t.elat.shape[0]) / 100.0)
+    return t
+
+
+@pytest.mark.shared_trees   # the shim's own default (conftest pins nothing here)
+def test_shim_default_is_bit_exact_on_decimal_latencies(tmp_path, monkeypatch):
+    from oracle import Oracle
+    from shadow_amd import spe
+    t = _decimal_stub_topology()
+    ips = [f"10.{v // 250}.{v % 250}.{1 + v % 7}" for v in range(t.n)]
+    verts = graphs.tiered_attached(t, n_core=400, n_attached=900)[:700]
+    top = _topology(tmp_path, t, ips)
+    addrs = _attach(top, ips, verts)
+    k = len(verts)
+    ok, lat, rel = top.path_info_batch(np.repeat(addrs, k), np.tile(addrs, k))
+    ref = Oracle(t).rows(verts, verts)
+    okr = ref["kind"] != 0
+    lat = lat.reshape(k, k)
+    np.testing.assert_array_equal(lat[okr], ref["lat"][okr])   # bit for bit
+    ns = lambda x: np.ceil(x * 1e6)   # SimulationTime delay, shd-worker.c:244
+    assert (ns(lat[okr]) != ns(ref["lat"][okr])).sum() == 0
+    top.close()
+    # the library default (shared anchor trees) on the same graph: how many delivery
+    # times would move -- the reason the shim defaults to exact rows here
+    g = spe.Graph(t)
+    sh = spe.PathTable(g, verts, engine=spe.SPE_ENGINE_BATCH)
+    sh.build()
+    assert sh.layout()["shared_sources"] == 1
+    d = sh.download()
+    moved = int((ns(d["lat"][okr]) != ns(ref["lat"][okr])).sum())
+    print(f"shared-tree rows: {moved} of {int(okr.sum())} pairs change ceil(latency * 1e6)")
+    assert g.info()["sums_exact"] == 0
