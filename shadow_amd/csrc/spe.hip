@@ -425,6 +425,20 @@ __global__ __launch_bounds__(BLOCK) void k_seed(int32_t n, int32_t groups, const
 // are strictly better or worse, so most visits skip the 256-B P row.
 constexpr int32_t PK_UNREAD = -3;
 
+// Lexicographic key comparisons are written branch-free (bitwise & / | on bools,
+// then selects).  The short-circuit form `a < A || (a == A && (b < B || ...))`
+// followed by several assignments was miscompiled by the gfx950 backend (ROCm
+// 7.2): with a wave-uniform last key, the tie branch's lanes took the new
+// distance fields but kept the OLD parent entry / vertex, so a tie won on
+// (d[u], u) recorded the wrong parent (found on decimal-latency graphs, whose
+// f64 sums tie).  Selects leave the compiler no such branch to merge.
+__device__ __forceinline__ bool lex_less3(double a, double b, int32_t c, double A, double B, int32_t C) {
+    return (a < A) | ((a == A) & ((b < B) | ((b == B) & (c < C))));
+}
+__device__ __forceinline__ bool lex_less2(double b, int32_t c, double B, int32_t C) {
+    return (b < B) | ((b == B) & (c < C));
+}
+
 struct Best {
     double bd;     // best alt (= distance)
     int32_t bk;    // in-CSR index of the parent edge (PK_UNREAD: the stored one, not read yet)
@@ -453,16 +467,14 @@ __device__ __forceinline__ void offer(Best& b, const DevGraph& G, const State& s
         } else if (b.bk >= 0) {   // (bk = -2: fixed seed from a pendant source, never tied)
             if (b.bu < 0) b.bu = G.icol[b.bk];
             if (b.bdu < 0.0) b.bdu = st.D[sidx<L>(g, n, b.bu, j)];
-            better = (du < b.bdu) || (du == b.bdu && u < b.bu);
+            better = lex_less2(du, u, b.bdu, b.bu);
         }
     }
-    if (better) {
-        b.bd = alt;
-        b.bk = kk;
-        b.bu = u;
-        b.bdu = du;
-        b.need = true;
-    }
+    b.bd = better ? alt : b.bd;
+    b.bk = better ? kk : b.bk;
+    b.bu = better ? u : b.bu;
+    b.bdu = better ? du : b.bdu;
+    b.need = b.need | better;
 }
 
 // offer<L> on the contracted graph (the heavy combine): b.bu holds the parent-of-
@@ -487,21 +499,19 @@ __device__ __forceinline__ void offer_x(Best& b, const DevGraph& G, const State&
                 const double da = st.D[sidx<L>(g, n, po.x, j)];
                 b.bdu = (po.y & 0x40000000) ? da + __hiloint2double(po.w, po.z) : da;
             }
-            better = drec < b.bdu || (drec == b.bdu && key < b.bu);
+            better = lex_less2(drec, key, b.bdu, b.bu);
             if (drec == b.bdu && key == b.bu) {   // same x: x's own canonical parent decides
                 const int32_t an = G.ipack[kk].x, ao = po.x;
                 const double dn = st.D[sidx<L>(g, n, an, j)], dd = st.D[sidx<L>(g, n, ao, j)];
-                better = dn < dd || (dn == dd && an < ao);
+                better = lex_less2(dn, an, dd, ao);
             }
         }
     }
-    if (better) {
-        b.bd = alt;
-        b.bk = kk;
-        b.bu = key;
-        b.bdu = drec;
-        b.need = true;
-    }
+    b.bd = better ? alt : b.bd;
+    b.bk = better ? kk : b.bk;
+    b.bu = better ? key : b.bu;
+    b.bdu = better ? drec : b.bdu;
+    b.need = b.need | better;
 }
 
 // Flagged candidates of one L-entry chunk [c0, c0+L) of a vertex's in-list.
@@ -804,12 +814,11 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_partial(int32_t groups, int32_t
             const uint64_t sm = (__ballot(f) >> base) & Sub<L>::MASK;
             scan_chunk<L, INFL>(sm, c0, base, u_j, w_j, g, n, j, active, st,
                           [&](int32_t kk, int32_t u, double du, double alt) {
-                              if (alt < ba || (alt == ba && (du < bdu || (du == bdu && u < bu)))) {
-                                  ba = alt;
-                                  bdu = du;
-                                  bu = u;
-                                  bk = kk;
-                              }
+                              const bool better = lex_less3(alt, du, u, ba, bdu, bu);
+                              ba = better ? alt : ba;
+                              bdu = better ? du : bdu;
+                              bu = better ? u : bu;
+                              bk = better ? kk : bk;
                           });
         }
         if (item) {
@@ -1112,16 +1121,14 @@ __device__ __forceinline__ void offer_lean(Lean& b, const DevGraph& G, const Sta
         } else if (b.bk >= 0) {   // exact tie: canonical (d[u], u)
             if (b.bu < 0) b.bu = G.icol[b.bk];
             if (b.bdu < 0.0) b.bdu = st.D[sidx<L>(g, n, b.bu, j)];
-            better = (du < b.bdu) || (du == b.bdu && u < b.bu);
+            better = lex_less2(du, u, b.bdu, b.bu);
         }
     }
-    if (better) {
-        b.bd = alt;
-        b.bk = kk;
-        b.bu = u;
-        b.bdu = du;
-        b.fl |= LEAN_NEED;
-    }
+    b.bd = better ? alt : b.bd;
+    b.bk = better ? kk : b.bk;
+    b.bu = better ? u : b.bu;
+    b.bdu = better ? du : b.bdu;
+    b.fl |= better ? LEAN_NEED : 0u;
 }
 
 // finish_vertex_m on Lean lanes (same routes, same writes)
@@ -1201,17 +1208,15 @@ __device__ __forceinline__ void offer_leanx(LeanX& b, const DevGraph& G, const S
             }
             const double da = st.D[sidx<L>(g, n, b.bu, j)];
             if (b.bdu < 0.0) b.bdu = (pb.y & 0x40000000) ? da + __hiloint2double(pb.w, pb.z) : da;
-            better = (drec < b.bdu) || (drec == b.bdu && (key < b.bkey || (key == b.bkey && (du < da || (du == da && u < b.bu)))));
+            better = (drec < b.bdu) | ((drec == b.bdu) & ((key < b.bkey) | ((key == b.bkey) & lex_less2(du, u, da, b.bu))));
         }
     }
-    if (better) {
-        b.bd = alt;
-        b.bk = kk;
-        b.bu = u;
-        b.bkey = key;
-        b.bdu = drec;
-        b.fl |= LEAN_NEED;
-    }
+    b.bd = better ? alt : b.bd;
+    b.bk = better ? kk : b.bk;
+    b.bu = better ? u : b.bu;
+    b.bkey = better ? key : b.bkey;
+    b.bdu = better ? drec : b.bdu;
+    b.fl |= better ? LEAN_NEED : 0u;
 }
 
 template <int M>
@@ -1510,29 +1515,27 @@ __global__ __launch_bounds__(BLOCK) void k_heavy_partial_m(int32_t groups, int32
                     const double du = dus[q][m];
                     const double dx = du + w1, alt = dx + w2, drec = sc ? dx : du;
                     if (!(active[m] && alt > du)) continue;
-                    if (alt < ba[m] ||
-                        (alt == ba[m] &&
-                         (drec < bdu[m] ||
-                          (drec == bdu[m] && (key < bu[m] || (key == bu[m] && (du < bda[m] || (du == bda[m] && u < bua[m])))))))) {
-                        ba[m] = alt;
-                        bdu[m] = drec;
-                        bu[m] = key;
-                        bk[m] = kb + b;
-                        bda[m] = du;
-                        bua[m] = u;
-                    }
+                    const bool better =
+                        (alt < ba[m]) |
+                        ((alt == ba[m]) & ((drec < bdu[m]) | ((drec == bdu[m]) & ((key < bu[m]) |
+                                                                                  ((key == bu[m]) & lex_less2(du, u, bda[m], bua[m]))))));
+                    ba[m] = better ? alt : ba[m];
+                    bdu[m] = better ? drec : bdu[m];
+                    bu[m] = better ? key : bu[m];
+                    bk[m] = better ? kb + b : bk[m];
+                    bda[m] = better ? du : bda[m];
+                    bua[m] = better ? u : bua[m];
                 }
                 }
             }
         } else {
             scan_chunk_m<M, INFL>(__ballot(f), kb, pk.x, __hiloint2double(pk.w, pk.z), g, n, lane, active, st,
                                   [&](int m, int32_t kk, int32_t u, double du, double alt) {
-                                      if (alt < ba[m] || (alt == ba[m] && (du < bdu[m] || (du == bdu[m] && u < bu[m])))) {
-                                          ba[m] = alt;
-                                          bdu[m] = du;
-                                          bu[m] = u;
-                                          bk[m] = kk;
-                                      }
+                                      const bool better = lex_less3(alt, du, u, ba[m], bdu[m], bu[m]);
+                                      ba[m] = better ? alt : ba[m];
+                                      bdu[m] = better ? du : bdu[m];
+                                      bu[m] = better ? u : bu[m];
+                                      bk[m] = better ? kk : bk[m];
                                   });
         }
 #pragma unroll
@@ -1786,16 +1789,14 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sssp(int32_t n, int32_t blocks, 
                     const double a0 = d0 + G.rw[3 * r], a1 = d1 + G.rw[3 * r + 1], a2 = d2 + G.rw[3 * r + 2];
                     int32_t q = d0 < INF ? 0 : -1;
                     double bd = d0 < INF ? a0 : INF, bu = d0;
-                    if (d1 < INF && (a1 < bd || (a1 == bd && d1 < bu))) {
-                        q = 1;
-                        bd = a1;
-                        bu = d1;
-                    }
-                    if (d2 < INF && (a2 < bd || (a2 == bd && d2 < bu))) {
-                        q = 2;
-                        bd = a2;
-                        bu = d2;
-                    }
+                    const bool t1 = (d1 < INF) & ((a1 < bd) | ((a1 == bd) & (d1 < bu)));   // (branch-free: lex_less3)
+                    q = t1 ? 1 : q;
+                    bd = t1 ? a1 : bd;
+                    bu = t1 ? d1 : bu;
+                    const bool t2 = (d2 < INF) & ((a2 < bd) | ((a2 == bd) & (d2 < bu)));
+                    q = t2 ? 2 : q;
+                    bd = t2 ? a2 : bd;
+                    bu = t2 ? d2 : bu;
                     if (q >= 0) {
                         const Route rc = st.RT[sidx<L>(g, n, G.rnb[3 * r + q], j)];
                         x.dc = bd;
@@ -2088,15 +2089,13 @@ __device__ __forceinline__ RootVal root_val(const DevGraph& G, const State& st, 
     const double a0 = d0 + G.rw[3 * r], a1 = d1 + G.rw[3 * r + 1], a2 = d2 + G.rw[3 * r + 2];
     int32_t q = d0 < INF ? 0 : -1;
     double bd = d0 < INF ? a0 : INF, bu = d0;
-    if (d1 < INF && (a1 < bd || (a1 == bd && d1 < bu))) {
-        q = 1;
-        bd = a1;
-        bu = d1;
-    }
-    if (d2 < INF && (a2 < bd || (a2 == bd && d2 < bu))) {
-        q = 2;
-        bd = a2;
-    }
+    const bool t1 = (d1 < INF) & ((a1 < bd) | ((a1 == bd) & (d1 < bu)));   // (branch-free: lex_less3)
+    q = t1 ? 1 : q;
+    bd = t1 ? a1 : bd;
+    bu = t1 ? d1 : bu;
+    const bool t2 = (d2 < INF) & ((a2 < bd) | ((a2 == bd) & (d2 < bu)));
+    q = t2 ? 2 : q;
+    bd = t2 ? a2 : bd;
     o.d = bd;
     o.q = q;
     o.ri = q == 0 ? i0 : (q == 1 ? i1 : i2);

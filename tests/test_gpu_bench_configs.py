@@ -109,6 +109,40 @@ def test_c3_bench_build_every_launch(spe):
     assert r["hop_checked"] > 0.9 * r["pairs"]   # every vertex is attached: most next hops are too
 
 
+@pytest.mark.shared_trees
+def test_c3_derived_rows_full_size(spe):
+    """C3 (50k BA) full table with the library default, as bench.py builds it: the
+    20k contracted degree-3 sources take no relaxation lane, their rows derived from
+    their three neighbours' roots.  Routes (routability, next hop,
+    hops) equal the oracle's exactly, latency / reliability within 1e-12 relative;
+    kept (core) sources bit-exact; 96 sampled rows (half of them derived) plus the
+    whole-table invariants over all 2.5e9 entries."""
+    top = graphs.gen_ba(50000, 3, 3)
+    att = np.arange(top.n, dtype=np.int32)
+    g, t, order = bench_table(spe, top, att)
+    lay = t.layout()
+    assert lay["shared_sources"] == 1 and lay["contracted_vertices"] > 0, lay
+    st = t.stats()
+    assert st["derived_sources"] > 15000, st
+    assert st["relaxed_lanes"] < 35000 + 64 * st["fallback_blocks"], st
+    print(f"C3 derived rows: {st['derived_sources']} derived sources, {st['relaxed_lanes']} relaxation lanes, "
+          f"{st['fallback_blocks']} fallback blocks")
+    nl = top.esrc != top.edst
+    deg = np.bincount(np.concatenate([top.esrc[nl], top.edst[nl]]), minlength=top.n)
+    rng = np.random.default_rng(33)
+    d3 = np.flatnonzero(deg[order] == 3)
+    kept = np.flatnonzero(deg[order] > 3)
+    slots = np.unique(np.r_[rng.choice(d3, 48, replace=False), rng.choice(kept, 48, replace=False)])
+    check_sampled_rows(t, top, order, slots, "C3 derived", rtol=1e-12)
+    ora = Oracle(top).rows(order[kept[:8]], order, nthreads=ORACLE_THREADS)
+    for i, s in enumerate(kept[:8]):   # a kept source is its own root: bit-exact
+        got = t.download(int(s), int(s) + 1)
+        ok = ora["kind"][i] != 0
+        np.testing.assert_array_equal(got["lat"][0][ok], ora["lat"][i][ok])
+        np.testing.assert_array_equal(got["rel"][0][ok], ora["rel"][i][ok])
+    check_whole_table(t, t.A, "C3 derived")
+
+
 def test_c2_bench_build_lds_engine(spe):
     """C2 (10k RGG) full table, bench settings (AUTO picks the LDS engine)."""
     top = graphs.gen_rgg(10000, 2)
@@ -135,9 +169,11 @@ def test_c4_one_gpu_full_table_every_launch(spe):
     assert lay["shared_sources"] == 1
     st = t.stats()
     assert st["relaxed_lanes"] < t.A // 4, st   # ~20k anchors for 100k stubs
-    slots = launch_sample_slots(t.A, lay["groups_per_launch"], extra_per_launch=14, seed=4)
-    nlaunch = -(-t.nblocks // lay["groups_per_launch"])
-    assert len(slots) >= 8 * nlaunch
+    # 64 source rows spread evenly over the SOURCE blocks (groups_per_launch counts
+    # root blocks under shared trees), the first and last slot, and 32 random ones
+    rng = np.random.default_rng(4)
+    slots = np.unique(np.r_[np.linspace(0, t.A - 1, 64).astype(np.int64), rng.integers(0, t.A, 32)])
+    assert len(slots) >= 64
     check_sampled_rows(t, top, order, slots, "C4", rtol=1e-12)
     # next hops of stub sources are their (unattached) anchors: no hop rule here
     check_whole_table(t, t.A, "C4", hop_rule=False)
