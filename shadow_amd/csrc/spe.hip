@@ -5049,6 +5049,7 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
     std::fill(tag.begin(), tag.end(), -1);
     std::vector<int32_t> roots, deferred;
     std::vector<uint8_t> bad((size_t)std::max(1, h.nc), 0);
+    std::vector<uint8_t> dk((size_t)(block_end - block_begin) * WAVE, 0);   // per slot of the batch: derived
     const spe::HostGraph::Share& sh = h.share;
     for (int32_t b = block_begin, bid = 0; b < block_end; ++bid) {
         HIP_TRY(hipStreamSynchronize(s));   // the pinned staging is reused per batch
@@ -5061,26 +5062,56 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
                 roots.push_back(c);
             }
         };
-        while (e < block_end) {
-            const size_t before = roots.size();
-            for (int32_t l = 0; l < WAVE; ++l) {
-                const int32_t slot = e * WAVE + l;
-                if (slot >= t->A) break;
-                const int32_t c = root_of(slot);
-                if (c == -3) {   // a derived source: its neighbours must be roots of this batch
-                    const int32_t x = h.core_id[(size_t)t->attached[(size_t)slot]];
+        // The roots of the blocks' other sources first (the cut counts those), then each
+        // derivable source of the batch: derived when at most one of its neighbours is
+        // not yet a root of the batch (that one becomes a root: no more lanes than the
+        // source's own), else on its own lane -- small batches would otherwise re-relax
+        // hubs batch after batch.  A batch the second step would overflow is cut before
+        // the block that overflows and assembled again (one block always fits: each of
+        // its sources costs at most one lane).
+        const int32_t limit = bid + 1 >= nb ? cap : std::min(target, cap);
+        int32_t e_max = block_end;
+        for (;;) {
+            roots.clear();
+            e = b;
+            while (e < e_max) {
+                const size_t before = roots.size();
+                for (int32_t l = 0; l < WAVE; ++l) {
+                    const int32_t slot = e * WAVE + l;
+                    if (slot >= t->A) break;
+                    const int32_t c = root_of(slot);
+                    if (c != -3) add(c);
+                }
+                // this block starts the next batch (the last planned batch takes the rest up to `cap`)
+                if (e > b && (int32_t)roots.size() > limit) {
+                    for (size_t i = before; i < roots.size(); ++i) tag[(size_t)roots[i]] = -1;
+                    roots.resize(before);
+                    break;
+                }
+                ++e;
+            }
+            std::fill(dk.begin(), dk.begin() + (size_t)(e - b) * WAVE, 0);
+            int32_t over = -1;
+            for (int32_t i = 0; i < (e - b) * WAVE && over < 0; ++i) {
+                const int32_t slot = b * WAVE + i;
+                if (slot >= t->A || root_of(slot) != -3) continue;
+                const int32_t x = h.core_id[(size_t)t->attached[(size_t)slot]];
+                int32_t miss = 0;
+                for (int q = 0; q < 3; ++q) miss += tag[(size_t)nbr(x, q)] != bid;
+                if (miss > 0 && (int32_t)roots.size() >= cap) {
+                    over = b + i / WAVE;
+                    break;
+                }
+                if (miss <= 1) {
                     for (int q = 0; q < 3; ++q) add(nbr(x, q));
+                    dk[(size_t)i] = 1;
                 } else {
-                    add(c);
+                    add(x);
                 }
             }
-            // this block starts the next batch (the last planned batch takes the rest up to `cap`)
-            if (e > b && (int32_t)roots.size() > (bid + 1 >= nb ? cap : std::min(target, cap))) {
-                for (size_t i = before; i < roots.size(); ++i) tag[(size_t)roots[i]] = -1;
-                roots.resize(before);
-                break;
-            }
-            ++e;
+            if (over < 0) break;
+            for (int32_t c : roots) tag[(size_t)c] = -1;
+            e_max = std::max(b + 1, over);
         }
         const int32_t R = (int32_t)roots.size();
         if (R > cap) return fail(SPE_ESTATE, "shared batch exceeds the state (one block's roots > groups * 64)");
@@ -5105,7 +5136,8 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
         int32_t nder = 0;
         for (int32_t i = 0; i < nblk * WAVE; ++i) {
             const int32_t slot = b * WAVE + i;
-            const int32_t c = slot < t->A ? root_of(slot) : -1;
+            int32_t c = slot < t->A ? root_of(slot) : -1;
+            if (c == -3 && !dk[(size_t)i]) c = h.core_id[(size_t)t->attached[(size_t)slot]];   // on its own lane
             const int32_t v = (slot < t->A && c != -1) ? t->attached[(size_t)slot] : -1;
             hr[i] = v;
             hw[i] = make_double2(0.0, 1.0);
@@ -5214,7 +5246,8 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
                     const size_t i = (size_t)(slot - b * WAVE);
                     bool d = any_sunsafe && t->h_sunsafe[i];
                     const int32_t v = t->attached[(size_t)slot];
-                    const int32_t c = root_of(slot);
+                    int32_t c = root_of(slot);
+                    if (c == -3 && !dk[i]) c = h.core_id[(size_t)v];
                     if (!d && any_bad) {
                         // an offset source of a flagged root (a core source is its own root: exact)
                         if (c == -3) {

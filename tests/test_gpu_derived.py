@@ -107,7 +107,7 @@ def test_derived_rows_match_oracle_and_exact_build(spe, name, groups):
     lay = t.layout()
     assert lay["shared_sources"] == 1 and lay["contracted_vertices"] > 0, (name, lay)
     assert st["derived_sources"] > 0, (name, st)
-    if name != "decimal":   # (decimal latencies: most blocks fall back, their lanes counted too)
+    if name not in ("decimal", "integer"):   # (ties: most blocks fall back, their lanes counted too)
         assert st["relaxed_lanes"] < len(A), (name, st)
     if all_derivable and groups == 0:   # one batch: every contracted source derived, no lane of its own
         n_removed = g.info()["n_relax_vertices"] - lay["contracted_vertices"]

@@ -43,6 +43,8 @@ SHAPES = {
 @pytest.mark.parametrize("shape", sorted(SHAPES))
 def test_decimal_ties_at_hubs_follow_the_canonical_parent(case, shape, contract):
     spe, top, A, ref = case
+    if contract and not shape.startswith("ring"):
+        pytest.skip("the degree-3 contraction runs on the LDS-ring relaxation only (spe_table_create)")
     g = spe.Graph(top)
     t = spe.PathTable(g, A, engine=spe.SPE_ENGINE_BATCH, exact_sources=True, no_contract=not contract,
                       **SHAPES[shape])
