@@ -125,7 +125,7 @@ def pmc_traffic(args, kernel, config=None):
     rocprofv3 --pmc passes of this same bench command), or None."""
     path = args.pmc_json
     if path is None:   # the newest committed summary of this config
-        for rnd in ("r03", "r02", "r01"):
+        for rnd in ("r04", "r03", "r02", "r01"):
             cand = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{config or args.config}.json")
             if os.path.exists(cand):
                 path = cand

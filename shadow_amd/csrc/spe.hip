@@ -2050,9 +2050,15 @@ __global__ __launch_bounds__(BLOCK) void k_rows_shared_lds(int32_t n, int32_t bl
 // XCD-contiguous: an XCD's resident waves work on the same few targets, so the
 // state columns the derived sources gather (every root lane at those vertices)
 // stay in that XCD's L2, and each wave writes TT consecutive 1-KB segments.
+// One record per derived source, every per-source constant of its three first legs
+// (coalesced 16-B loads; no per-lane gathers from G.rw / G.ra / the lane -> vertex map)
 struct alignas(16) DerivedSrc {
     int32_t lane[3];   // root lanes of the three neighbours, in G.rnb order
     int32_t rid;       // removed index of the source (G.rnb / rw / ra at 3 rid + i)
+    int32_t hop[3];    // the neighbours' original ids (the first hop through each)
+    int32_t pad;
+    double w[3];       // latency of the edge x -> neighbour (G.rw[3 rid + i])
+    double a[3];       // its 1 - p (G.ra[3 rid + i])
 };
 
 // A root lane's value at a target: the relaxation vertex c's distance, or for a
@@ -2110,8 +2116,13 @@ __device__ __forceinline__ RootVal root_val(const DevGraph& G, const State& st, 
 }
 
 #ifndef SPE_DERIVED_TT
-#define SPE_DERIVED_TT 2
+#define SPE_DERIVED_TT 4
 #endif
+// Each item's TT targets go through the load chain together -- slot constants
+// (scalar), then every root-lane distance, then the chosen route records, then the
+// stores -- so a wave waits for three memory round trips per item, not three per
+// target (the stores could alias the state as far as the compiler knows, so
+// target-at-a-time code serialises every target's chain behind the last one's stores).
 template <int L, int TT>
 __global__ __launch_bounds__(BLOCK) void k_rows_derived(int32_t n, int32_t blocks, int32_t sb0,
                                                         const int32_t* __restrict__ srcv,
@@ -2120,7 +2131,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_derived(int32_t n, int32_t block
                                                         const int2* __restrict__ rli,
                                                         const double2* __restrict__ rwa,
                                                         const DerivedSrc* __restrict__ der,
-                                                        const int32_t* __restrict__ lane_v, double wmin,
+                                                        double wmin,
                                                         double omax, double hmax, int32_t exact,
                                                         uint8_t* __restrict__ sunsafe) {
     const int32_t lane = threadIdx.x & (WAVE - 1);
@@ -2139,97 +2150,124 @@ __global__ __launch_bounds__(BLOCK) void k_rows_derived(int32_t n, int32_t block
         const int32_t s = srcv[b * WAVE + lane];
         const int2 ri = rli[b * WAVE + lane];
         const bool pend = ri.y >= 0, derv = ri.y <= -2;
-        double2 wa = make_double2(0.0, 1.0);
-        if (pend) wa = rwa[b * WAVE + lane];
-        DerivedSrc dx{{0, 0, 0}, 0};
-        double w0 = 0.0, w1 = 0.0, w2 = 0.0;
+        // the source's candidate first legs: a kept source reads its root lane with
+        // offset 0 (core) or its pendant edge; a derived one its three neighbours' lanes
+        int32_t rl[3] = {ri.x, -1, -1};
+        double wq[3] = {0.0, INF, INF};
+        double aq[3] = {1.0, 1.0, 1.0};
+        int32_t hq[3] = {-1, -1, -1};
+        if (pend) {
+            const double2 wa = rwa[b * WAVE + lane];
+            wq[0] = wa.x;
+            aq[0] = wa.y;
+            hq[0] = ri.y;
+        }
         if (derv) {
-            dx = der[-2 - ri.y];
-            w0 = G.rw[3 * dx.rid];
-            w1 = G.rw[3 * dx.rid + 1];
-            w2 = G.rw[3 * dx.rid + 2];
+            const DerivedSrc dx = der[-2 - ri.y];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                rl[k] = dx.lane[k];
+                wq[k] = dx.w[k];
+                aq[k] = dx.a[k];
+                hq[k] = dx.hop[k];
+            }
         }
         const bool chk = (pend || derv) && !exact;
         bool bad = false;
-        for (int32_t tl = 0; tl < TT; ++tl) {
+        SlotInfo si[TT];
+        bool live[TT];
+#pragma unroll
+        for (int tl = 0; tl < TT; ++tl) {
+            const int32_t jt = tt * TT + tl;
+            si[tl] = slots[jt < tb.A ? jt : tb.A - 1];
+            live[tl] = jt < tb.A && s >= 0 && si[tl].t != s;
+        }
+        RootVal v[TT][3];
+#pragma unroll
+        for (int tl = 0; tl < TT; ++tl)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                if (live[tl] && rl[k] >= 0) {
+                    v[tl][k] = root_val<L>(G, st, n, rl[k], si[tl].c, chk, wmin, omax, hmax);
+                } else {
+                    v[tl][k].d = INF;
+                    v[tl][k].ri = 0;
+                    v[tl][k].q = -1;
+                    v[tl][k].tight = false;
+                }
+            }
+        // the first leg: min_k fl(w_k + d_k) (strict: the first of equal sums; a tie
+        // flags the source anyway)
+        double dd[TT];
+        int32_t bk[TT];
+#pragma unroll
+        for (int tl = 0; tl < TT; ++tl) {
+            const double o0 = wq[0] + v[tl][0].d, o1 = wq[1] + v[tl][1].d, o2 = wq[2] + v[tl][2].d;
+            const bool t1 = o1 < o0;
+            int32_t bi = t1 ? 1 : 0;
+            double bo = t1 ? o1 : o0;
+            const bool t2 = o2 < bo;
+            bi = t2 ? 2 : bi;
+            bo = t2 ? o2 : bo;
+            if (bo < INF) {
+                if (derv) {   // u* must beat the other first hops by more than rounding (exact sums: strictly)
+                    if (exact) {
+                        bad |= (bi != 0 && o0 <= bo) || (bi != 1 && o1 <= bo) || (bi != 2 && o2 <= bo);
+                    } else {
+                        if (bi != 0 && o0 < INF) bad |= near_tie(bo, o0, wmin, omax, hmax);
+                        if (bi != 1 && o1 < INF) bad |= near_tie(bo, o1, wmin, omax, hmax);
+                        if (bi != 2 && o2 < INF) bad |= near_tie(bo, o2, wmin, omax, hmax);
+                    }
+                }
+                bad |= (bi == 0 ? v[tl][0].tight : (bi == 1 ? v[tl][1].tight : v[tl][2].tight));
+            }
+            dd[tl] = bo;
+            bk[tl] = bi;
+        }
+        Route rc[TT];
+#pragma unroll
+        for (int tl = 0; tl < TT; ++tl) {
+            const int32_t bi = bk[tl];
+            const size_t x = bi == 0 ? v[tl][0].ri : (bi == 1 ? v[tl][1].ri : v[tl][2].ri);
+            rc[tl] = Route{1.0, 0, -1};
+            if (dd[tl] < INF) rc[tl] = st.RT[x];
+        }
+#pragma unroll
+        for (int tl = 0; tl < TT; ++tl) {
             const int32_t jt = tt * TT + tl;
             if (jt >= tb.A) break;
-            const SlotInfo si = slots[jt];
+            const SlotInfo& sv = si[tl];
             double Lt = -1.0, R = -1.0;
             int32_t N = -1, H = 0;
             if (s >= 0) {
-                if (si.t == s) {
+                if (sv.t == s) {
                     self_entry(G, md, s, Lt, R, N, H);
-                } else {
-                    double d = INF;
-                    Route rt{1.0, 0, -1};
-                    RootVal v;
-                    int32_t hop = -1;
-                    double apre = 1.0;
-                    if (!derv) {
-                        v = root_val<L>(G, st, n, ri.x, si.c, chk, wmin, omax, hmax);
-                        d = v.d;
-                        if (pend && d < INF) {
-                            d = wa.x + d;
-                            apre = wa.y;
-                            hop = ri.y;
-                        }
-                    } else {
-                        const RootVal v0 = root_val<L>(G, st, n, dx.lane[0], si.c, chk, wmin, omax, hmax);
-                        const RootVal v1 = root_val<L>(G, st, n, dx.lane[1], si.c, chk, wmin, omax, hmax);
-                        const RootVal v2 = root_val<L>(G, st, n, dx.lane[2], si.c, chk, wmin, omax, hmax);
-                        const double o0 = w0 + v0.d, o1 = w1 + v1.d, o2 = w2 + v2.d;
-                        int32_t bi = 0;
-                        double bo = o0;
-                        if (o1 < bo) {
-                            bi = 1;
-                            bo = o1;
-                        }
-                        if (o2 < bo) {
-                            bi = 2;
-                            bo = o2;
-                        }
-                        if (bo < INF) {
-                            // u* must beat the other first hops by more than rounding (exact
-                            // sums: strictly; a tie needs x's own tree)
-                            if (exact) {
-                                bad |= (bi != 0 && o0 <= bo) || (bi != 1 && o1 <= bo) || (bi != 2 && o2 <= bo);
-                            } else {
-                                if (bi != 0 && o0 < INF) bad |= near_tie(bo, o0, wmin, omax, hmax);
-                                if (bi != 1 && o1 < INF) bad |= near_tie(bo, o1, wmin, omax, hmax);
-                                if (bi != 2 && o2 < INF) bad |= near_tie(bo, o2, wmin, omax, hmax);
-                            }
-                            v = bi == 0 ? v0 : (bi == 1 ? v1 : v2);
-                            d = bo;
-                            apre = G.ra[3 * dx.rid + bi];
-                            hop = lane_v[dx.lane[bi]];
-                        }
+                } else if (dd[tl] < INF) {
+                    const int32_t bi = bk[tl];
+                    const int32_t q = bi == 0 ? v[tl][0].q : (bi == 1 ? v[tl][1].q : v[tl][2].q);
+                    double d = dd[tl];
+                    Route rt = rc[tl];
+                    if (q >= 0) {   // removed target: one edge past the neighbour taken
+                        rt.r = rc[tl].r * G.ra[3 * (-2 - sv.c) + q];
+                        rt.h = rc[tl].h + 1;
+                        rt.f = (rc[tl].h == 0) ? sv.t : rc[tl].f;
                     }
-                    if (d < INF) {
-                        bad |= v.tight;
-                        const Route rc = st.RT[v.ri];
-                        rt = rc;
-                        if (v.q >= 0) {   // removed target: one edge past the neighbour taken
-                            rt.r = rc.r * G.ra[3 * (-2 - si.c) + v.q];
-                            rt.h = rc.h + 1;
-                            rt.f = (rc.h == 0) ? si.t : rc.f;
-                        }
-                        if (hop >= 0) {   // an offset source: its first edge in front
-                            rt.r = apre * rt.r;
-                            rt.h = rt.h + 1;
-                            rt.f = hop;
-                        }
-                        if (si.kt >= 0) {   // a pruned pendant target: one edge past its anchor
-                            d = d + si.pw;
-                            rt.r = rt.r * si.pa;
-                            rt.f = (rt.h == 0) ? si.t : rt.f;
-                            rt.h = rt.h + 1;
-                        }
-                        Lt = d == 0 ? 1.0 : d;   // shd-topology.c:1833-1837
-                        R = rt.r;
-                        N = rt.f;
-                        H = rt.h;
+                    const int32_t hop = bi == 0 ? hq[0] : (bi == 1 ? hq[1] : hq[2]);
+                    if (hop >= 0) {   // an offset source: its first edge in front
+                        rt.r = (bi == 0 ? aq[0] : (bi == 1 ? aq[1] : aq[2])) * rt.r;
+                        rt.h = rt.h + 1;
+                        rt.f = hop;
                     }
+                    if (sv.kt >= 0) {   // a pruned pendant target: one edge past its anchor
+                        d = d + sv.pw;
+                        rt.r = rt.r * sv.pa;
+                        rt.f = (rt.h == 0) ? sv.t : rt.f;
+                        rt.h = rt.h + 1;
+                    }
+                    Lt = d == 0 ? 1.0 : d;   // shd-topology.c:1833-1837
+                    R = rt.r;
+                    N = rt.f;
+                    H = rt.h;
                 }
             }
             const size_t o = tidx(sb0 + b, tb.A, jt, lane);
@@ -5144,8 +5182,14 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
             if (c == -3) {
                 const int32_t x = h.core_id[(size_t)v];
                 DerivedSrc d;
-                for (int q = 0; q < 3; ++q) d.lane[q] = lane_of[(size_t)nbr(x, q)];
                 d.rid = h.cx.rid[(size_t)x];
+                d.pad = 0;
+                for (int q = 0; q < 3; ++q) {
+                    d.lane[q] = lane_of[(size_t)nbr(x, q)];
+                    d.hop[q] = h.corev[(size_t)nbr(x, q)];
+                    d.w[q] = h.cx.rw[3 * (size_t)d.rid + q];
+                    d.a[q] = h.cx.ra[3 * (size_t)d.rid + q];
+                }
                 t->h_der[nder] = d;
                 hl[i] = make_int2(d.lane[0], -2 - nder);
                 ++nder;
@@ -5220,7 +5264,7 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
                 const double hmax = (double)h.n + 2.0;
                 k_rows_derived<128, SPE_DERIVED_TT><<<grid, BLOCK, 0, s>>>(
                     t->bn, nblk, sb0, d_rsrc, t->d_slots, *t->bG, t->md, t->st, t->tb, d_rli, d_rwa, t->d_der,
-                    t->d_srcv, sh.wmin, sh.omax, hmax, sh.exact ? 1 : 0, t->d_sunsafe);
+                    sh.wmin, sh.omax, hmax, sh.exact ? 1 : 0, t->d_sunsafe);
             } else {
                 launch_rows_shared(t, grid_for((int64_t)nblk * t->A * WAVE, BLOCK, 8192), nblk, sb0, s, d_rsrc,
                                    d_rli, d_rwa, d_rng);

@@ -1,6 +1,6 @@
 # copy the judged artefacts of a tools/gpu_profiles.sh run (+ gpu_tests.sh) into profiles/
 set -e
-R=${ROUND:-r03}
+R=${ROUND:-r04}
 O=gpurun_out/$R
 for C in c1 c2 c3 c4 c5 c5_on_c4 c2fw; do
   [ -f $O/bench_$C.log ] && tail -1 $O/bench_$C.log > profiles/${R}_bench_$C.json

@@ -8,4 +8,4 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_
 timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TA_BUSY_avr TA_TA_BUSY_sum -d $O/p2 -o run --output-format csv -- python bench.py $A > $O/p2.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT -d $O/p3 -o run --output-format csv -- python bench.py $A > $O/p3.log 2>&1
 python tools/pmc_summary.py $O > $O/summary.txt
-grep -A30 "k_relax_s" $O/summary.txt | head -32
+cat $O/summary.txt

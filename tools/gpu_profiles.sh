@@ -4,7 +4,7 @@
 # (which reads the PMC summary back as roofline.traffic).
 # Configs: c3 c2 c4 c5 (on the C3 table) c5_on_c4 (on the C4 table) c1 c2fw.
 set -e
-R=${ROUND:-r03}
+R=${ROUND:-r04}
 O=gpurun_out/$R
 mkdir -p $O
 export TMPDIR=/tmp
