@@ -2050,23 +2050,24 @@ __global__ __launch_bounds__(BLOCK) void k_rows_shared_lds(int32_t n, int32_t bl
 // XCD-contiguous: an XCD's resident waves work on the same few targets, so the
 // state columns the derived sources gather (every root lane at those vertices)
 // stay in that XCD's L2, and each wave writes TT consecutive 1-KB segments.
-// One record per derived source, every per-source constant of its three first legs
-// (coalesced 16-B loads; no per-lane gathers from G.rw / G.ra / the lane -> vertex map)
+// One record per derived source, every per-source constant of its first legs
+// (coalesced 16-B loads; no per-lane gathers from the graph or the lane -> vertex
+// map).  A removed source has three legs, a degree-4 one four (lane -1: none).
+constexpr int DER_K = 4;
 struct alignas(16) DerivedSrc {
-    int32_t lane[3];   // root lanes of the three neighbours, in G.rnb order
-    int32_t rid;       // removed index of the source (G.rnb / rw / ra at 3 rid + i)
-    int32_t hop[3];    // the neighbours' original ids (the first hop through each)
-    int32_t pad;
-    double w[3];       // latency of the edge x -> neighbour (G.rw[3 rid + i])
-    double a[3];       // its 1 - p (G.ra[3 rid + i])
+    int32_t lane[DER_K];   // root lanes of the neighbours, in core in-list order
+    int32_t hop[DER_K];    // the neighbours' original ids (the first hop through each)
+    double w[DER_K];       // latency of the edge x -> neighbour
+    double a[DER_K];       // its 1 - p
 };
 
 // A root lane's value at a target: the relaxation vertex c's distance, or for a
 // removed target (c = -2 - r) the best of its three neighbours; `tight` when an
 // offset could change that choice (runner-up within the margin of k_share_check).
+// (Kept small: a row item holds TT x DER_K of them; the state index whose route
+// record the row continues is recomputed for the winner only, root_idx.)
 struct RootVal {
     double d;
-    size_t ri;      // state index whose route record the row continues
     int32_t q;      // removed target: the neighbour taken, -1 otherwise
     bool tight;
 };
@@ -2084,8 +2085,7 @@ __device__ __forceinline__ RootVal root_val(const DevGraph& G, const State& st, 
     o.q = -1;
     o.tight = false;
     if (c >= 0) {
-        o.ri = sidx<L>(g, n, c, j);
-        o.d = st.D[o.ri];
+        o.d = st.D[sidx<L>(g, n, c, j)];
         return o;
     }
     const int32_t r = -2 - c;
@@ -2104,7 +2104,6 @@ __device__ __forceinline__ RootVal root_val(const DevGraph& G, const State& st, 
     bd = t2 ? a2 : bd;
     o.d = bd;
     o.q = q;
-    o.ri = q == 0 ? i0 : (q == 1 ? i1 : i2);
     if (check && q >= 0) {
         bool t = false;
         if (q != 0 && d0 < INF) t |= near_tie(bd, a0, wmin, omax, hmax);
@@ -2115,6 +2114,12 @@ __device__ __forceinline__ RootVal root_val(const DevGraph& G, const State& st, 
     return o;
 }
 
+template <int L>
+__device__ __forceinline__ size_t root_idx(const DevGraph& G, int32_t n, int32_t sl, int32_t c, int32_t q) {
+    const int32_t g = sl / L, j = sl - (sl / L) * L;
+    return sidx<L>(g, n, c >= 0 ? c : G.rnb[3 * (-2 - c) + (q < 0 ? 0 : q)], j);
+}
+
 #ifndef SPE_DERIVED_TT
 #define SPE_DERIVED_TT 4
 #endif
@@ -2123,8 +2128,11 @@ __device__ __forceinline__ RootVal root_val(const DevGraph& G, const State& st, 
 // stores -- so a wave waits for three memory round trips per item, not three per
 // target (the stores could alias the state as far as the compiler knows, so
 // target-at-a-time code serialises every target's chain behind the last one's stores).
+#ifndef SPE_DERIVED_OCC
+#define SPE_DERIVED_OCC 1
+#endif
 template <int L, int TT>
-__global__ __launch_bounds__(BLOCK) void k_rows_derived(int32_t n, int32_t blocks, int32_t sb0,
+__global__ __launch_bounds__(BLOCK, SPE_DERIVED_OCC) void k_rows_derived(int32_t n, int32_t blocks, int32_t sb0,
                                                         const int32_t* __restrict__ srcv,
                                                         const SlotInfo* __restrict__ slots, DevGraph G,
                                                         RowMode md, State st, Table tb,
@@ -2151,11 +2159,16 @@ __global__ __launch_bounds__(BLOCK) void k_rows_derived(int32_t n, int32_t block
         const int2 ri = rli[b * WAVE + lane];
         const bool pend = ri.y >= 0, derv = ri.y <= -2;
         // the source's candidate first legs: a kept source reads its root lane with
-        // offset 0 (core) or its pendant edge; a derived one its three neighbours' lanes
-        int32_t rl[3] = {ri.x, -1, -1};
-        double wq[3] = {0.0, INF, INF};
-        double aq[3] = {1.0, 1.0, 1.0};
-        int32_t hq[3] = {-1, -1, -1};
+        // offset 0 (core) or its pendant edge; a derived one its neighbours' lanes
+        int32_t rl[DER_K], hq[DER_K];
+        double wq[DER_K], aq[DER_K];
+#pragma unroll
+        for (int k = 0; k < DER_K; ++k) {
+            rl[k] = k == 0 ? ri.x : -1;
+            wq[k] = k == 0 ? 0.0 : INF;
+            aq[k] = 1.0;
+            hq[k] = -1;
+        }
         if (pend) {
             const double2 wa = rwa[b * WAVE + lane];
             wq[0] = wa.x;
@@ -2165,7 +2178,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_derived(int32_t n, int32_t block
         if (derv) {
             const DerivedSrc dx = der[-2 - ri.y];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
+            for (int k = 0; k < DER_K; ++k) {
                 rl[k] = dx.lane[k];
                 wq[k] = dx.w[k];
                 aq[k] = dx.a[k];
@@ -2175,62 +2188,75 @@ __global__ __launch_bounds__(BLOCK) void k_rows_derived(int32_t n, int32_t block
         const bool chk = (pend || derv) && !exact;
         bool bad = false;
         SlotInfo si[TT];
+        int32_t sc[TT];
         bool live[TT];
 #pragma unroll
         for (int tl = 0; tl < TT; ++tl) {
             const int32_t jt = tt * TT + tl;
             si[tl] = slots[jt < tb.A ? jt : tb.A - 1];
+            sc[tl] = si[tl].c;
             live[tl] = jt < tb.A && s >= 0 && si[tl].t != s;
         }
-        RootVal v[TT][3];
+        RootVal v[TT][DER_K];
 #pragma unroll
         for (int tl = 0; tl < TT; ++tl)
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
+            for (int k = 0; k < DER_K; ++k) {
                 if (live[tl] && rl[k] >= 0) {
-                    v[tl][k] = root_val<L>(G, st, n, rl[k], si[tl].c, chk, wmin, omax, hmax);
+                    v[tl][k] = root_val<L>(G, st, n, rl[k], sc[tl], chk, wmin, omax, hmax);
                 } else {
                     v[tl][k].d = INF;
-                    v[tl][k].ri = 0;
                     v[tl][k].q = -1;
                     v[tl][k].tight = false;
                 }
             }
         // the first leg: min_k fl(w_k + d_k) (strict: the first of equal sums; a tie
-        // flags the source anyway)
+        // flags the source anyway).  The winner's fields by selects (constant indices).
         double dd[TT];
-        int32_t bk[TT];
+        int32_t bk[TT], bq[TT];
+        size_t bx[TT];
 #pragma unroll
         for (int tl = 0; tl < TT; ++tl) {
-            const double o0 = wq[0] + v[tl][0].d, o1 = wq[1] + v[tl][1].d, o2 = wq[2] + v[tl][2].d;
-            const bool t1 = o1 < o0;
-            int32_t bi = t1 ? 1 : 0;
-            double bo = t1 ? o1 : o0;
-            const bool t2 = o2 < bo;
-            bi = t2 ? 2 : bi;
-            bo = t2 ? o2 : bo;
+            double o[DER_K];
+#pragma unroll
+            for (int k = 0; k < DER_K; ++k) o[k] = wq[k] + v[tl][k].d;
+            int32_t bi = 0;
+            double bo = o[0];
+#pragma unroll
+            for (int k = 1; k < DER_K; ++k) {
+                const bool tk = o[k] < bo;
+                bi = tk ? k : bi;
+                bo = tk ? o[k] : bo;
+            }
+            int32_t q = -1, sl = 0;
+            bool tg = false;
+#pragma unroll
+            for (int k = 0; k < DER_K; ++k) {
+                sl = k == bi ? rl[k] : sl;
+                q = k == bi ? v[tl][k].q : q;
+                tg = k == bi ? v[tl][k].tight : tg;
+            }
+            const size_t x = root_idx<L>(G, n, sl < 0 ? 0 : sl, sc[tl], q);
             if (bo < INF) {
                 if (derv) {   // u* must beat the other first hops by more than rounding (exact sums: strictly)
-                    if (exact) {
-                        bad |= (bi != 0 && o0 <= bo) || (bi != 1 && o1 <= bo) || (bi != 2 && o2 <= bo);
-                    } else {
-                        if (bi != 0 && o0 < INF) bad |= near_tie(bo, o0, wmin, omax, hmax);
-                        if (bi != 1 && o1 < INF) bad |= near_tie(bo, o1, wmin, omax, hmax);
-                        if (bi != 2 && o2 < INF) bad |= near_tie(bo, o2, wmin, omax, hmax);
+#pragma unroll
+                    for (int k = 0; k < DER_K; ++k) {
+                        if (exact) bad |= (k != bi) & (o[k] <= bo);
+                        else if (k != bi && o[k] < INF) bad |= near_tie(bo, o[k], wmin, omax, hmax);
                     }
                 }
-                bad |= (bi == 0 ? v[tl][0].tight : (bi == 1 ? v[tl][1].tight : v[tl][2].tight));
+                bad |= tg;
             }
             dd[tl] = bo;
             bk[tl] = bi;
+            bq[tl] = q;
+            bx[tl] = x;
         }
         Route rc[TT];
 #pragma unroll
         for (int tl = 0; tl < TT; ++tl) {
-            const int32_t bi = bk[tl];
-            const size_t x = bi == 0 ? v[tl][0].ri : (bi == 1 ? v[tl][1].ri : v[tl][2].ri);
             rc[tl] = Route{1.0, 0, -1};
-            if (dd[tl] < INF) rc[tl] = st.RT[x];
+            if (dd[tl] < INF) rc[tl] = st.RT[bx[tl]];
         }
 #pragma unroll
         for (int tl = 0; tl < TT; ++tl) {
@@ -2244,7 +2270,7 @@ __global__ __launch_bounds__(BLOCK) void k_rows_derived(int32_t n, int32_t block
                     self_entry(G, md, s, Lt, R, N, H);
                 } else if (dd[tl] < INF) {
                     const int32_t bi = bk[tl];
-                    const int32_t q = bi == 0 ? v[tl][0].q : (bi == 1 ? v[tl][1].q : v[tl][2].q);
+                    const int32_t q = bq[tl];
                     double d = dd[tl];
                     Route rt = rc[tl];
                     if (q >= 0) {   // removed target: one edge past the neighbour taken
@@ -2252,9 +2278,15 @@ __global__ __launch_bounds__(BLOCK) void k_rows_derived(int32_t n, int32_t block
                         rt.h = rc[tl].h + 1;
                         rt.f = (rc[tl].h == 0) ? sv.t : rc[tl].f;
                     }
-                    const int32_t hop = bi == 0 ? hq[0] : (bi == 1 ? hq[1] : hq[2]);
+                    int32_t hop = -1;
+                    double apre = 1.0;
+#pragma unroll
+                    for (int k = 0; k < DER_K; ++k) {
+                        hop = k == bi ? hq[k] : hop;
+                        apre = k == bi ? aq[k] : apre;
+                    }
                     if (hop >= 0) {   // an offset source: its first edge in front
-                        rt.r = (bi == 0 ? aq[0] : (bi == 1 ? aq[1] : aq[2])) * rt.r;
+                        rt.r = apre * rt.r;
                         rt.h = rt.h + 1;
                         rt.f = hop;
                     }
@@ -4465,7 +4497,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         bool any = false;
         for (int32_t i = t->blk0 * WAVE; i < std::min(n_attached, t->blk1 * WAVE) && !any; ++i) {
             const int32_t c = g->hg.core_id[(size_t)attached[i]];
-            any = c < 0 || (t->cx && g->hg.cx.rid[(size_t)c] >= 0);
+            any = c < 0 || (t->cx && g->hg.cx.der[(size_t)c]);
         }
         t->share = any;
     }
@@ -4484,7 +4516,7 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
             const int32_t v = attached[i];
             int32_t c = h.core_id[(size_t)v];
             if (c < 0) c = h.anchor_core[(size_t)v];
-            else if (t->cx && h.cx.rid[(size_t)c] >= 0) continue;
+            else if (t->cx && h.cx.der[(size_t)c]) continue;
             if (c >= 0 && !isroot[(size_t)c]) {
                 isroot[(size_t)c] = 1;
                 ++roots;
@@ -4493,10 +4525,9 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         if (t->cx)
             for (int32_t i = s0; i < s1; ++i) {
                 const int32_t c = h.core_id[(size_t)attached[i]];
-                if (c < 0 || h.cx.rid[(size_t)c] < 0) continue;
-                const int32_t r = h.cx.rid[(size_t)c];
+                if (c < 0 || !h.cx.der[(size_t)c]) continue;
                 bool all = true;
-                for (int q = 0; q < 3; ++q) all &= isroot[(size_t)h.cx.kcore[(size_t)h.cx.rnb[3 * (size_t)r + q]]] != 0;
+                for (int32_t k = h.iptr[(size_t)c]; k < h.iptr[(size_t)c + 1]; ++k) all &= isroot[(size_t)h.icol[(size_t)k]] != 0;
                 if (!all) ++roots;
             }
         const int32_t need = (int32_t)std::max<int64_t>(1, (roots + WAVE - 1) / WAVE);
@@ -5051,10 +5082,11 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
     const int32_t s_end = std::min(t->A, block_end * WAVE);
     // per slot: root core id (core source, pendant anchor, or a removed source itself),
     // or -3 for a derived source, -1 padding
-    auto removed = [&](int32_t c) { return t->derive && c >= 0 && h.cx.rid[(size_t)c] >= 0; };
-    auto nbr = [&](int32_t c, int q) {   // core id of removed vertex c's neighbour q (G.rnb order)
-        return h.cx.kcore[(size_t)h.cx.rnb[3 * (size_t)h.cx.rid[(size_t)c] + q]];
-    };
+    // derivable sources (h.cx.der: removed vertices, degree-4 kept ones); neighbour q
+    // of such a source = entry q of its core in-list (G.rnb order for a removed one)
+    auto removed = [&](int32_t c) { return t->derive && c >= 0 && h.cx.der[(size_t)c]; };
+    auto ndeg = [&](int32_t c) { return h.iptr[(size_t)c + 1] - h.iptr[(size_t)c]; };
+    auto nbr = [&](int32_t c, int q) { return h.icol[(size_t)h.iptr[(size_t)c] + q]; };
     std::vector<int32_t> tag((size_t)std::max(1, h.nc), -1), lane_of((size_t)std::max(1, h.nc), -1);
     // the call's non-derived roots: a removed source is derivable iff its three neighbours are among them
     int32_t total = 0;
@@ -5072,7 +5104,7 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
         const int32_t c = h.core_id[(size_t)t->attached[(size_t)i]];
         if (!removed(c)) continue;
         bool all = true;
-        for (int q = 0; q < 3; ++q) all &= tag[(size_t)nbr(c, q)] == 0;
+        for (int q = 0; q < ndeg(c); ++q) all &= tag[(size_t)nbr(c, q)] == 0;
         derivable[(size_t)(i - block_begin * WAVE)] = all;
         if (!all) ++total;
     }
@@ -5135,13 +5167,13 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
                 if (slot >= t->A || root_of(slot) != -3) continue;
                 const int32_t x = h.core_id[(size_t)t->attached[(size_t)slot]];
                 int32_t miss = 0;
-                for (int q = 0; q < 3; ++q) miss += tag[(size_t)nbr(x, q)] != bid;
+                for (int q = 0; q < ndeg(x); ++q) miss += tag[(size_t)nbr(x, q)] != bid;
                 if (miss > 0 && (int32_t)roots.size() >= cap) {
                     over = b + i / WAVE;
                     break;
                 }
                 if (miss <= 1) {
-                    for (int q = 0; q < 3; ++q) add(nbr(x, q));
+                    for (int q = 0; q < ndeg(x); ++q) add(nbr(x, q));
                     dk[(size_t)i] = 1;
                 } else {
                     add(x);
@@ -5182,13 +5214,13 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
             if (c == -3) {
                 const int32_t x = h.core_id[(size_t)v];
                 DerivedSrc d;
-                d.rid = h.cx.rid[(size_t)x];
-                d.pad = 0;
-                for (int q = 0; q < 3; ++q) {
-                    d.lane[q] = lane_of[(size_t)nbr(x, q)];
-                    d.hop[q] = h.corev[(size_t)nbr(x, q)];
-                    d.w[q] = h.cx.rw[3 * (size_t)d.rid + q];
-                    d.a[q] = h.cx.ra[3 * (size_t)d.rid + q];
+                for (int q = 0; q < DER_K; ++q) {
+                    const bool on = q < ndeg(x);
+                    const size_t k = on ? (size_t)h.iptr[(size_t)x] + q : 0;
+                    d.lane[q] = on ? lane_of[(size_t)nbr(x, q)] : -1;
+                    d.hop[q] = on ? h.corev[(size_t)nbr(x, q)] : -1;
+                    d.w[q] = on ? h.iw[k] : INF;
+                    d.a[q] = on ? h.ia[k] : 1.0;
                 }
                 t->h_der[nder] = d;
                 hl[i] = make_int2(d.lane[0], -2 - nder);

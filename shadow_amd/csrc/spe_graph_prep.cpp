@@ -366,6 +366,21 @@ void contract_degree3(HostGraph* hg) {
         }
         cx.ptr.push_back((int32_t)cx.col.size());
     }
+    // derivable sources: the removed vertices, then (greedy, core order) kept vertices
+    // of in-degree 4 with no removed or derivable neighbour and no pendant
+    cx.der.assign(nc, 0);
+    for (int32_t x : cx.rcore) cx.der[x] = 1;
+    for (int32_t x = 0; x < nc; ++x) {
+        if (cx.rid[x] >= 0 || pendants[x] || hg->iptr[x + 1] - hg->iptr[x] != 4) continue;
+        bool ok = true;
+        for (int32_t k = hg->iptr[x]; k < hg->iptr[x + 1]; ++k) {
+            const int32_t u = hg->icol[k];
+            ok &= u != x && cx.rid[u] < 0 && !cx.der[u];
+        }
+        if (!ok) continue;
+        cx.der[x] = 1;
+        ++cx.nd4;
+    }
     // reverse entries: (a -> v via x) <-> (v -> a via x)
     cx.rev.assign(cx.col.size(), -1);
     for (int32_t kv = 0; kv < cx.nk; ++kv)
@@ -403,8 +418,10 @@ void share_prep(HostGraph* hg) {
         omax = std::max(omax, w);
         ws.push_back(w);
     }
-    if (hg->cx.active)   // a derived source's offset is the edge to one of its three neighbours
-        for (double w : hg->cx.rw) omax = std::max(omax, w);
+    if (hg->cx.active)   // a derived source's offset is the edge to one of its neighbours
+        for (int32_t x = 0; x < hg->nc; ++x)
+            if (hg->cx.der[(size_t)x])
+                for (int32_t k = hg->iptr[(size_t)x]; k < hg->iptr[(size_t)x + 1]; ++k) omax = std::max(omax, hg->iw[(size_t)k]);
     double wmin = INFINITY, wmax = 0.0;
     for (double w : hg->iw) wmin = std::min(wmin, w);
     for (double w : ws) {

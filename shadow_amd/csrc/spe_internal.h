@@ -70,6 +70,13 @@ struct HostGraph {
         std::vector<double> w1, w2, a1, a2;   // plain: (w, 0, a, 1); shortcut: (w(a,x), w(x,v), a(a,x), a(x,v))
         std::vector<int32_t> key;          // core id of the entry's parent (x for a shortcut, a for a plain edge)
         std::vector<int32_t> via;          // original id of x, -1 for a plain edge
+        // Sources whose rows a shared table may derive from their neighbours' lanes
+        // (k_rows_derived): every removed vertex, and an independent set of kept
+        // vertices with exactly four neighbours, none removed, no pendant anchored
+        // (they stay relaxation vertices; only their own lane goes).  The neighbours
+        // are the core in-list (iptr / icol / iw / ia): 3 or 4 entries.
+        std::vector<uint8_t> der;          // [nc]
+        int32_t nd4 = 0;
     } cx;
 
     // Shared anchor trees for the batch engine (share_prep): a pruned

@@ -112,8 +112,8 @@ def test_c3_bench_build_every_launch(spe):
 @pytest.mark.shared_trees
 def test_c3_derived_rows_full_size(spe):
     """C3 (50k BA) full table with the library default, as bench.py builds it: the
-    20k contracted degree-3 sources take no relaxation lane, their rows derived from
-    their three neighbours' roots.  Routes (routability, next hop,
+    20k contracted degree-3 sources and ~2.9k degree-4 ones take no relaxation lane,
+    their rows derived from their neighbours' roots.  Routes (routability, next hop,
     hops) equal the oracle's exactly, latency / reliability within 1e-12 relative;
     kept (core) sources bit-exact; 96 sampled rows (half of them derived) plus the
     whole-table invariants over all 2.5e9 entries."""
@@ -123,15 +123,15 @@ def test_c3_derived_rows_full_size(spe):
     lay = t.layout()
     assert lay["shared_sources"] == 1 and lay["contracted_vertices"] > 0, lay
     st = t.stats()
-    assert st["derived_sources"] > 15000, st
-    assert st["relaxed_lanes"] < 35000 + 64 * st["fallback_blocks"], st
+    assert st["derived_sources"] > 20000, st
+    assert st["relaxed_lanes"] < 30000 + 64 * st["fallback_blocks"], st
     print(f"C3 derived rows: {st['derived_sources']} derived sources, {st['relaxed_lanes']} relaxation lanes, "
           f"{st['fallback_blocks']} fallback blocks")
     nl = top.esrc != top.edst
     deg = np.bincount(np.concatenate([top.esrc[nl], top.edst[nl]]), minlength=top.n)
     rng = np.random.default_rng(33)
-    d3 = np.flatnonzero(deg[order] == 3)
-    kept = np.flatnonzero(deg[order] > 3)
+    d3 = np.flatnonzero(deg[order] <= 4)   # derivable: every degree-3 source, some degree-4 ones
+    kept = np.flatnonzero(deg[order] > 4)
     slots = np.unique(np.r_[rng.choice(d3, 48, replace=False), rng.choice(kept, 48, replace=False)])
     check_sampled_rows(t, top, order, slots, "C3 derived", rtol=1e-12)
     ora = Oracle(top).rows(order[kept[:8]], order, nthreads=ORACLE_THREADS)
@@ -160,7 +160,7 @@ def test_c4_one_gpu_full_table_every_launch(spe):
     """C4 (200k tiered, A = 100k stubs): the whole 10^10-pair table (220 GB) built on
     ONE GPU with the bench settings -- the library default, so the stubs on one
     anchor share its relaxation: routes exact, latency / reliability
-    within 1e-12 relative; 16 rows of every 64-block span vs the oracle."""
+    within 1e-12 relative; >= 64 source rows spread over the table vs the oracle."""
     top = graphs.gen_tiered()
     att = graphs.tiered_attached(top)
     g, t, order = bench_table(spe, top, att)

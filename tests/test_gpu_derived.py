@@ -1,6 +1,7 @@
 """GPU parity of the derived rows, the batch engine's default for
-contracted sources on shared tables: a removed degree-3 vertex x whose three
-neighbours are relaxation roots of its batch takes no lane; its row is
+contracted sources on shared tables: a removed degree-3 vertex x (or a kept
+degree-4 one with no removed neighbour) whose neighbours are relaxation roots of
+its batch takes no lane; its row is
 min_i fl(w(x, u_i) + d_{u_i}(t)) with first hop u*, one more hop, reliability
 a(x, u*) r_{u*}(t).
 
@@ -160,8 +161,8 @@ def test_derived_rows_kept_sources_bit_exact(spe):
     nl = top.esrc != top.edst
     deg = np.bincount(np.concatenate([top.esrc[nl], top.edst[nl]]), minlength=top.n)
     lat_diff = (got["lat"] != ex["lat"]).any(axis=1)
-    # every differing row is a degree-3 (contractible) source
-    assert (deg[A[lat_diff]] == 3).all()
+    # every differing row is a derivable source: degree 3 (contracted) or 4
+    assert (deg[A[lat_diff]] <= 4).all()
     np.testing.assert_allclose(got["lat"], ex["lat"], rtol=RTOL, atol=0)
 
 

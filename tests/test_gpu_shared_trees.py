@@ -108,10 +108,10 @@ def test_shared_rows_match_oracle_and_exact_build(spe, name, groups):
     for k in ("ok", "next", "hops"):
         np.testing.assert_array_equal(got[k], ex[k], err_msg=f"{name}: {k} vs exact build")
     # a core source is its own root: its row is the exact build's bit for bit (degree-3
-    # core sources may be contracted and derived from their neighbours: not counted)
+    # and degree-4 core sources may be derived from their neighbours: not counted)
     deg = np.bincount(np.concatenate([top.esrc[top.esrc != top.edst], top.edst[top.esrc != top.edst]]),
                       minlength=top.n)
-    rows_core = np.flatnonzero(deg[A] > 3)
+    rows_core = np.flatnonzero(deg[A] > 4)
     assert rows_core.size > 0 and core > 0
     for k in ("lat", "rel"):
         np.testing.assert_array_equal(got[k][rows_core], ex[k][rows_core], err_msg=f"{name}: core-source {k}")
