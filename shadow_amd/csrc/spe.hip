@@ -2061,63 +2061,120 @@ struct alignas(16) DerivedSrc {
     double a[DER_K];       // its 1 - p
 };
 
-// A root lane's value at a target: the relaxation vertex c's distance, or for a
-// removed target (c = -2 - r) the best of its three neighbours; `tight` when an
-// offset could change that choice (runner-up within the margin of k_share_check).
-// (Kept small: a row item holds TT x DER_K of them; the state index whose route
-// record the row continues is recomputed for the winner only, root_idx.)
-struct RootVal {
-    double d;
-    int32_t q;      // removed target: the neighbour taken, -1 otherwise
-    bool tight;
-};
-
 __device__ __forceinline__ bool near_tie(double best, double alt, double wmin, double omax, double hmax) {
     const double h = wmin > 0.0 ? fmin(hmax, alt / wmin + 3.0) : hmax;
     return alt - best <= 4.5 * h * 0x1p-53 * (omax + alt);
 }
 
+// A root lane's value at a target: the relaxation vertex c's distance, or for a
+// removed target (c = -2 - r) the expanded entry k_expand_removed wrote (the best
+// of its three neighbours, its sign the margin flag); `tight` when an offset could
+// change that choice (runner-up within the margin of k_share_check) -- only asked
+// for sources with an offset.
+struct RootVal {
+    double d;
+    bool tight;
+};
+
 template <int L>
-__device__ __forceinline__ RootVal root_val(const DevGraph& G, const State& st, int32_t n, int32_t sl, int32_t c,
-                                            bool check, double wmin, double omax, double hmax) {
+__device__ __forceinline__ RootVal root_val(const State& st, const double* __restrict__ DX, int32_t n, int32_t nr,
+                                            int32_t sl, int32_t c, bool check) {
     RootVal o;
     const int32_t g = sl / L, j = sl - (sl / L) * L;
-    o.q = -1;
-    o.tight = false;
     if (c >= 0) {
         o.d = st.D[sidx<L>(g, n, c, j)];
-        return o;
-    }
-    const int32_t r = -2 - c;
-    const size_t i0 = sidx<L>(g, n, G.rnb[3 * r], j), i1 = sidx<L>(g, n, G.rnb[3 * r + 1], j),
-                 i2 = sidx<L>(g, n, G.rnb[3 * r + 2], j);
-    const double d0 = st.D[i0], d1 = st.D[i1], d2 = st.D[i2];
-    const double a0 = d0 + G.rw[3 * r], a1 = d1 + G.rw[3 * r + 1], a2 = d2 + G.rw[3 * r + 2];
-    int32_t q = d0 < INF ? 0 : -1;
-    double bd = d0 < INF ? a0 : INF, bu = d0;
-    const bool t1 = (d1 < INF) & ((a1 < bd) | ((a1 == bd) & (d1 < bu)));   // (branch-free: lex_less3)
-    q = t1 ? 1 : q;
-    bd = t1 ? a1 : bd;
-    bu = t1 ? d1 : bu;
-    const bool t2 = (d2 < INF) & ((a2 < bd) | ((a2 == bd) & (d2 < bu)));
-    q = t2 ? 2 : q;
-    bd = t2 ? a2 : bd;
-    o.d = bd;
-    o.q = q;
-    if (check && q >= 0) {
-        bool t = false;
-        if (q != 0 && d0 < INF) t |= near_tie(bd, a0, wmin, omax, hmax);
-        if (q != 1 && d1 < INF) t |= near_tie(bd, a1, wmin, omax, hmax);
-        if (q != 2 && d2 < INF) t |= near_tie(bd, a2, wmin, omax, hmax);
-        o.tight = t;
+        o.tight = false;
+    } else {
+        const double x = DX[sidx<L>(g, nr, -2 - c, j)];
+        o.d = __builtin_fabs(x);
+        o.tight = check && __builtin_signbit(x);
     }
     return o;
 }
 
+// the route record a row continues: the relaxation state's, or a removed target's
+// expanded one (the edge past the neighbour already folded in)
 template <int L>
-__device__ __forceinline__ size_t root_idx(const DevGraph& G, int32_t n, int32_t sl, int32_t c, int32_t q) {
+__device__ __forceinline__ const Route* root_route(const State& st, const Route* __restrict__ RTX, int32_t n,
+                                                   int32_t nr, int32_t sl, int32_t c) {
     const int32_t g = sl / L, j = sl - (sl / L) * L;
-    return sidx<L>(g, n, c >= 0 ? c : G.rnb[3 * (-2 - c) + (q < 0 ? 0 : q)], j);
+    return c >= 0 ? st.RT + sidx<L>(g, n, c, j) : RTX + sidx<L>(g, nr, -2 - c, j);
+}
+
+// Contracted shared tables: every (root lane, removed vertex) entry once, before the
+// rows -- the best of the removed vertex's three neighbours by (d, d[u], u) as
+// k_rows_sssp chooses it, with the route one edge past that neighbour, and (sums
+// not exact) the sign bit set when a runner-up is within the margin of an offset
+// source (near_tie).  The rows kernel then reads one entry where every source that
+// reads the lane (its own, and each derived source next to it: a hub's lane is read
+// by thousands) re-did three gathers and the choice.  One wave per (lane group,
+// removed vertex): three coalesced neighbour rows in, one row of DX and of RTX out.
+template <int L>
+__global__ __launch_bounds__(BLOCK) void k_expand_removed(int32_t groups, int32_t n, int32_t nr, DevGraph G, State st,
+                                                          double* __restrict__ DX, Route* __restrict__ RTX,
+                                                          const int32_t* __restrict__ rorig, int32_t check,
+                                                          double wmin, double omax, double hmax) {
+    constexpr int M = L / WAVE;
+    const int32_t lane = threadIdx.x & (WAVE - 1);
+    const int64_t items = (int64_t)groups * nr;
+    const int64_t nw = ((int64_t)gridDim.x * BLOCK) >> 6;
+    for (int64_t it = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6; it < items; it += nw) {   // wave-uniform
+        const int32_t g = (int32_t)(it / nr), r = (int32_t)(it - (it / nr) * nr);
+        const int32_t u0 = G.rnb[3 * r], u1 = G.rnb[3 * r + 1], u2 = G.rnb[3 * r + 2];
+        const double w0 = G.rw[3 * r], w1 = G.rw[3 * r + 1], w2 = G.rw[3 * r + 2];
+        double d0[M], d1[M], d2[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const int32_t j = lane + m * WAVE;
+            d0[m] = st.D[sidx<L>(g, n, u0, j)];
+            d1[m] = st.D[sidx<L>(g, n, u1, j)];
+            d2[m] = st.D[sidx<L>(g, n, u2, j)];
+        }
+        int32_t qq[M];
+        double bb[M];
+        bool tt[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const double a0 = d0[m] + w0, a1 = d1[m] + w1, a2 = d2[m] + w2;
+            int32_t q = d0[m] < INF ? 0 : -1;
+            double bd = d0[m] < INF ? a0 : INF, bu = d0[m];
+            const bool t1 = (d1[m] < INF) & ((a1 < bd) | ((a1 == bd) & (d1[m] < bu)));   // (branch-free: lex_less3)
+            q = t1 ? 1 : q;
+            bd = t1 ? a1 : bd;
+            bu = t1 ? d1[m] : bu;
+            const bool t2 = (d2[m] < INF) & ((a2 < bd) | ((a2 == bd) & (d2[m] < bu)));
+            q = t2 ? 2 : q;
+            bd = t2 ? a2 : bd;
+            bool t = false;
+            if (check && q >= 0) {
+                if (q != 0 && d0[m] < INF) t |= near_tie(bd, a0, wmin, omax, hmax);
+                if (q != 1 && d1[m] < INF) t |= near_tie(bd, a1, wmin, omax, hmax);
+                if (q != 2 && d2[m] < INF) t |= near_tie(bd, a2, wmin, omax, hmax);
+            }
+            qq[m] = q;
+            bb[m] = bd;
+            tt[m] = t;
+        }
+        Route rc[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            rc[m] = Route{1.0, 0, -1};
+            if (qq[m] >= 0) rc[m] = st.RT[sidx<L>(g, n, qq[m] == 0 ? u0 : (qq[m] == 1 ? u1 : u2), lane + m * WAVE)];
+        }
+        const int32_t yo = rorig[r];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const size_t o = sidx<L>(g, nr, r, lane + m * WAVE);
+            Route x = rc[m];
+            if (qq[m] >= 0) {   // one edge past the neighbour taken
+                x.r = rc[m].r * G.ra[3 * r + qq[m]];
+                x.h = rc[m].h + 1;
+                x.f = (rc[m].h == 0) ? yo : rc[m].f;   // the neighbour is the lane's root itself
+            }
+            DX[o] = qq[m] < 0 ? INF : (tt[m] ? -bb[m] : bb[m]);
+            RTX[o] = x;
+        }
+    }
 }
 
 #ifndef SPE_DERIVED_TT
@@ -2139,7 +2196,8 @@ __global__ __launch_bounds__(BLOCK, SPE_DERIVED_OCC) void k_rows_derived(int32_t
                                                         const int2* __restrict__ rli,
                                                         const double2* __restrict__ rwa,
                                                         const DerivedSrc* __restrict__ der,
-                                                        double wmin,
+                                                        const double* __restrict__ DX,
+                                                        const Route* __restrict__ RTX, int32_t nr, double wmin,
                                                         double omax, double hmax, int32_t exact,
                                                         uint8_t* __restrict__ sunsafe) {
     const int32_t lane = threadIdx.x & (WAVE - 1);
@@ -2203,18 +2261,16 @@ __global__ __launch_bounds__(BLOCK, SPE_DERIVED_OCC) void k_rows_derived(int32_t
 #pragma unroll
             for (int k = 0; k < DER_K; ++k) {
                 if (live[tl] && rl[k] >= 0) {
-                    v[tl][k] = root_val<L>(G, st, n, rl[k], sc[tl], chk, wmin, omax, hmax);
+                    v[tl][k] = root_val<L>(st, DX, n, nr, rl[k], sc[tl], chk);
                 } else {
                     v[tl][k].d = INF;
-                    v[tl][k].q = -1;
                     v[tl][k].tight = false;
                 }
             }
         // the first leg: min_k fl(w_k + d_k) (strict: the first of equal sums; a tie
         // flags the source anyway).  The winner's fields by selects (constant indices).
         double dd[TT];
-        int32_t bk[TT], bq[TT];
-        size_t bx[TT];
+        int32_t bk[TT], bl[TT];
 #pragma unroll
         for (int tl = 0; tl < TT; ++tl) {
             double o[DER_K];
@@ -2228,15 +2284,13 @@ __global__ __launch_bounds__(BLOCK, SPE_DERIVED_OCC) void k_rows_derived(int32_t
                 bi = tk ? k : bi;
                 bo = tk ? o[k] : bo;
             }
-            int32_t q = -1, sl = 0;
+            int32_t sl = 0;
             bool tg = false;
 #pragma unroll
             for (int k = 0; k < DER_K; ++k) {
                 sl = k == bi ? rl[k] : sl;
-                q = k == bi ? v[tl][k].q : q;
                 tg = k == bi ? v[tl][k].tight : tg;
             }
-            const size_t x = root_idx<L>(G, n, sl < 0 ? 0 : sl, sc[tl], q);
             if (bo < INF) {
                 if (derv) {   // u* must beat the other first hops by more than rounding (exact sums: strictly)
 #pragma unroll
@@ -2249,14 +2303,13 @@ __global__ __launch_bounds__(BLOCK, SPE_DERIVED_OCC) void k_rows_derived(int32_t
             }
             dd[tl] = bo;
             bk[tl] = bi;
-            bq[tl] = q;
-            bx[tl] = x;
+            bl[tl] = sl < 0 ? 0 : sl;
         }
         Route rc[TT];
 #pragma unroll
         for (int tl = 0; tl < TT; ++tl) {
             rc[tl] = Route{1.0, 0, -1};
-            if (dd[tl] < INF) rc[tl] = st.RT[bx[tl]];
+            if (dd[tl] < INF) rc[tl] = *root_route<L>(st, RTX, n, nr, bl[tl], sc[tl]);
         }
 #pragma unroll
         for (int tl = 0; tl < TT; ++tl) {
@@ -2270,14 +2323,8 @@ __global__ __launch_bounds__(BLOCK, SPE_DERIVED_OCC) void k_rows_derived(int32_t
                     self_entry(G, md, s, Lt, R, N, H);
                 } else if (dd[tl] < INF) {
                     const int32_t bi = bk[tl];
-                    const int32_t q = bq[tl];
                     double d = dd[tl];
                     Route rt = rc[tl];
-                    if (q >= 0) {   // removed target: one edge past the neighbour taken
-                        rt.r = rc[tl].r * G.ra[3 * (-2 - sv.c) + q];
-                        rt.h = rc[tl].h + 1;
-                        rt.f = (rc[tl].h == 0) ? sv.t : rc[tl].f;
-                    }
                     int32_t hop = -1;
                     double apre = 1.0;
 #pragma unroll
@@ -3732,6 +3779,10 @@ struct spe_table {
     DerivedSrc* d_der = nullptr;   // per derived source of the batch
     DerivedSrc* h_der = nullptr;   // pinned staging
     uint8_t* d_sunsafe = nullptr;  // per source slot of the batch: a derived row's margin failed
+    double* d_dx = nullptr;        // [lane group][removed vertex][L]: expanded entries (k_expand_removed)
+    Route* d_rtx = nullptr;
+    const int32_t* d_rorig = nullptr;   // [removed] original id
+    int32_t nr = 0;
     uint8_t* h_sunsafe = nullptr;
     bool derive = false;           // contracted sources take their neighbours' roots (no lane)
     // spe_lookup_batch_host / spe_table_get: device + pinned staging, grown on demand,
@@ -4531,7 +4582,8 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
                 if (!all) ++roots;
             }
         const int32_t need = (int32_t)std::max<int64_t>(1, (roots + WAVE - 1) / WAVE);
-        const double per_group = (double)t->bn * WAVE * 28.0 + 4.0 * t->bn + 2.0 * std::max(1, t->bm);
+        const double per_group = (double)t->bn * WAVE * 28.0 + 4.0 * t->bn + 2.0 * std::max(1, t->bm) +
+                                 (t->derive ? (double)h.cx.rcore.size() * WAVE * 24.0 : 0.0);
         double cap = (double)need;
         size_t free_b = 0, total_b = 0;
         if (hipSetDevice(g->device) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
@@ -4686,6 +4738,14 @@ int spe_table_create(spe_graph* g, const int32_t* attached, int32_t n_attached, 
         if (t->derive) {
             TRY(dev_alloc(t->allocs, &t->d_der, owned_slots));
             TRY(dev_alloc(t->allocs, &t->d_sunsafe, owned_slots));
+            const spe::HostGraph& h = g->hg;
+            t->nr = (int32_t)h.cx.rcore.size();
+            const size_t sx = GW * (size_t)std::max(1, t->nr);
+            TRY(dev_alloc(t->allocs, &t->d_dx, sx));
+            TRY(dev_alloc(t->allocs, &t->d_rtx, sx));
+            std::vector<int32_t> ro((size_t)std::max(1, t->nr), -1);
+            for (int32_t r = 0; r < t->nr; ++r) ro[(size_t)r] = h.corev[(size_t)h.cx.rcore[(size_t)r]];
+            TRY(dev_upload(t->allocs, ro, &t->d_rorig));
         }
     }
 #undef TRY
@@ -5291,12 +5351,19 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
             LaunchTimer lt(t, s, SPE_K_ROWS);
             if (t->derive) {
                 HIP_TRY(hipMemsetAsync(t->d_sunsafe, 0, ns, s));
+                const double hmax = (double)h.n + 2.0;
+                if (t->nr > 0) {
+                    const int32_t groups = pb / bpg;   // (L = 128: contracted tables)
+                    const int grid = grid_for((int64_t)groups * t->nr * WAVE, BLOCK, 8192);
+                    k_expand_removed<128><<<grid, BLOCK, 0, s>>>(groups, t->bn, t->nr, *t->bG, t->st, t->d_dx,
+                                                                 t->d_rtx, t->d_rorig, sh.exact ? 0 : 1, sh.wmin,
+                                                                 sh.omax, hmax);
+                }
                 const int64_t items = (int64_t)((t->A + SPE_DERIVED_TT - 1) / SPE_DERIVED_TT) * nblk;
                 const int grid = (grid_for(items * WAVE, BLOCK, 8192) + 7) & ~7;
-                const double hmax = (double)h.n + 2.0;
                 k_rows_derived<128, SPE_DERIVED_TT><<<grid, BLOCK, 0, s>>>(
                     t->bn, nblk, sb0, d_rsrc, t->d_slots, *t->bG, t->md, t->st, t->tb, d_rli, d_rwa, t->d_der,
-                    sh.wmin, sh.omax, hmax, sh.exact ? 1 : 0, t->d_sunsafe);
+                    t->d_dx, t->d_rtx, t->nr, sh.wmin, sh.omax, hmax, sh.exact ? 1 : 0, t->d_sunsafe);
             } else {
                 launch_rows_shared(t, grid_for((int64_t)nblk * t->A * WAVE, BLOCK, 8192), nblk, sb0, s, d_rsrc,
                                    d_rli, d_rwa, d_rng);
