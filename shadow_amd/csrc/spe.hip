@@ -2178,7 +2178,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_removed(int32_t groups, int32_
 }
 
 #ifndef SPE_DERIVED_TT
-#define SPE_DERIVED_TT 4
+#define SPE_DERIVED_TT 3
 #endif
 // Each item's TT targets go through the load chain together -- slot constants
 // (scalar), then every root-lane distance, then the chosen route records, then the
