@@ -314,6 +314,7 @@ def bench_shim(args, config: str):
         t0 = time.perf_counter()
         top = T.Topology(path)
         new_s = time.perf_counter() - t0
+        print(f"[shim] graphml {write_s:.1f} s, topology_new {new_s:.1f} s", file=sys.stderr, flush=True)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     A = int(att.shape[0])
@@ -322,20 +323,25 @@ def bench_shim(args, config: str):
     for i in range(A):
         top.attach(int(hosts[i]), ip_hint=ips[int(att[i])])
     attach_s = time.perf_counter() - t0
+    print(f"[shim] attach {A} hosts {attach_s:.1f} s", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     rc = top.seal()
     seal_s = time.perf_counter() - t0
+    print(f"[shim] seal {seal_s:.1f} s", file=sys.stderr, flush=True)
     assert rc == 0, f"topology_seal failed ({rc})"
     q = min(args.queries, 20_000_000)
     rng = np.random.default_rng(5)
     pi = rng.integers(0, A, (q, 2))
     src, dst = hosts[pi[:, 0]], hosts[pi[:, 1]]
+    t0 = time.perf_counter()
     ok, lat, rel = top.path_info_batch(src[:1 << 16], dst[:1 << 16])   # warm-up (code objects, staging)
+    print(f"[shim] warm-up batch of {1 << 16} queries {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
     steps = args.steps if args.steps > 0 else 3
     t0 = time.perf_counter()
     for _ in range(steps):
         ok, lat, rel = top.path_info_batch(src, dst)
     el = time.perf_counter() - t0
+    print(f"[shim] {steps} batches of {q} queries {el:.1f} s", file=sys.stderr, flush=True)
     assert ok.all(), "every pair of the synthetic topologies is routable"
     # the same pairs one call at a time (topology_getPathInfo), a bounded sample
     # (a 64-source block of the C4 table is 102 MB: single queries outside the host mirror
@@ -345,6 +351,7 @@ def bench_shim(args, config: str):
     for i in range(ns):
         top.path_info(int(src[i]), int(dst[i]))
     single_s = time.perf_counter() - t1
+    print(f"[shim] {ns} single calls {single_s:.1f} s", file=sys.stderr, flush=True)
     top.close()
     value = q * steps / el
     cpu = None if args.no_cpu_baseline else cpu_lookup_baseline(A, args.cpu_seconds)

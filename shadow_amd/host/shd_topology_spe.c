@@ -807,7 +807,20 @@ int32_t topology_vertex_count(const Topology* top) { return top ? top->n : 0; }
 
 /* ----------------------------------------------------- IP -> vertex map */
 
-static uint64_t hash_ip(uint32_t ip) { return (uint64_t)ip * 0x9E3779B97F4A7C15ull; }
+/* 64-bit finaliser (every input bit reaches the low bits the tables index by):
+ * in_addr_t values are in network byte order, so on a little-endian host a
+ * plain multiplicative hash's low bits saw only the first octets -- every host of
+ * a 10.x.y.z plan in one probe chain */
+static uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xFF51AFD7ED558CCDull;
+    x ^= x >> 33;
+    x *= 0xC4CEB9FE1A85EC53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+static uint64_t hash_ip(uint32_t ip) { return mix64(ip); }
 
 static void ip_put(Topology* top, uint32_t ip, int32_t v) {
     if ((top->ip_size + 1) * 2 > top->ip_cap) {
@@ -1288,7 +1301,7 @@ static PairRec* rec_locked(Shard* sh, uint64_t key, int insert) {
         PairRec* nt = calloc(nc, sizeof(PairRec));
         for (size_t i = 0; i < sh->cap; ++i)
             if (sh->tab[i].key) {
-                size_t j = (size_t)(sh->tab[i].key * 0xD6E8FEB86659FD93ull) & (nc - 1);
+                size_t j = (size_t)mix64(sh->tab[i].key) & (nc - 1);
                 while (nt[j].key) j = (j + 1) & (nc - 1);
                 nt[j] = sh->tab[i];
             }
@@ -1297,7 +1310,7 @@ static PairRec* rec_locked(Shard* sh, uint64_t key, int insert) {
         sh->cap = nc;
     }
     if (!sh->cap) return NULL;
-    size_t j = (size_t)(key * 0xD6E8FEB86659FD93ull) & (sh->cap - 1);
+    size_t j = (size_t)mix64(key) & (sh->cap - 1);
     while (sh->tab[j].key) {
         if (sh->tab[j].key == key) return &sh->tab[j];
         j = (j + 1) & (sh->cap - 1);
@@ -1675,8 +1688,11 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
         latency[i] = reliability[i] = -1.0;
         routable[i] = 0;
     }
+    const int timing = getenv("SHADOW_SPE_BATCH_TIMING") != NULL;
+    const double t0 = timing ? now_s() : 0.0;
     Snap* sn = batch_snapshot(top, n, srcAddress, dstAddress);
     if (!sn) return -1;
+    const double t1 = timing ? now_s() : 0.0;
     /* the cache model per query (which Path answers it, the stores a miss makes,
      * the log lines), then every table read of the batch at once: from the host
      * mirror, or one device lookup launch for the lot (spe_lookup_batch_host) */
@@ -1721,6 +1737,7 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
             snap_value(top, sn, s, t, &latency[i], &reliability[i]);
         }
     }
+    const double t2 = timing ? now_s() : 0.0;
     if (nd > 0) {
         double* lr = malloc((size_t)nd * 2 * sizeof(double));
         uint8_t* okd = malloc((size_t)nd);
@@ -1738,6 +1755,9 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
         free(okd);
     }
     pthread_rwlock_unlock(&top->state_lock);
+    if (timing)
+        fprintf(stderr, "[topology] batch of %lld: snapshot %.3f s, cache model %.3f s, table reads %.3f s\n",
+                (long long)n, t1 - t0, t2 - t1, now_s() - t2);
     free(pairs);
     free(at);
     batch_min_callback(top, min_updated);
