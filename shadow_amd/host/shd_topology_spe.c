@@ -32,6 +32,7 @@
 #include <string.h>
 #include <strings.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <libxml/parser.h>
 #include <libxml/tree.h>
@@ -145,7 +146,12 @@ struct _Topology {
      * sequence of v's first Dijkstra row run; explicit entries and packet counts
      * in sharded maps; cache_mu serialises misses (the reference's store path) */
     pthread_mutex_t cache_mu;
+    pthread_mutex_t batch_mu;  /* the cached batch scratch below (one batch at a time uses it) */
+    void* bscr;
+    size_t bscr_bytes;
     _Atomic uint64_t* run_seq;
+    _Atomic uint8_t* xflag;    /* [n] 1: some explicit entry (x, .) exists -- readers skip the
+                                  shard (and its mutex) for every other x */
     _Atomic uint64_t seq;
     _Atomic int64_t n_explicit;
     Shard shards[NSHARD];
@@ -681,6 +687,7 @@ static void topo_release(Topology* top) {
     free(top->ip_keys); free(top->ip_vals); free(top->ip_used);
     free(top->is_attached); free(top->attached);
     free((void*)top->run_seq);
+    free((void*)top->xflag);
     for (int i = 0; i < NSHARD; ++i) {
         free(top->shards[i].tab);
         pthread_mutex_destroy(&top->shards[i].mu);
@@ -688,6 +695,8 @@ static void topo_release(Topology* top) {
     pthread_rwlock_destroy(&top->state_lock);
     pthread_mutex_destroy(&top->seal_lock);
     pthread_mutex_destroy(&top->cache_mu);
+    pthread_mutex_destroy(&top->batch_mu);
+    free(top->bscr);
     free(top);
 }
 
@@ -706,6 +715,7 @@ Topology* topology_new_on_device(const char* graphPath, int32_t device) {
     }
     pthread_mutex_init(&top->seal_lock, NULL);
     pthread_mutex_init(&top->cache_mu, NULL);
+    pthread_mutex_init(&top->batch_mu, NULL);
     for (int i = 0; i < NSHARD; ++i) pthread_mutex_init(&top->shards[i].mu, NULL);
     const char* mode = getenv("SHADOW_SPE_PATH_CACHE");
     top->cache_mode = (mode && !strcasecmp(mode, "reference")) ? TOPOLOGY_ANSWER_REFERENCE : TOPOLOGY_ANSWER_ROWS;
@@ -759,6 +769,7 @@ Topology* topology_new_on_device(const char* graphPath, int32_t device) {
     top->is_attached = calloc((size_t)top->n + 1, 1);
     top->attached = malloc(((size_t)top->n + 1) * sizeof(int32_t));
     top->run_seq = calloc((size_t)top->n + 1, sizeof(uint64_t));
+    top->xflag = calloc((size_t)top->n + 1, sizeof(uint8_t));
     return top;
 }
 
@@ -769,6 +780,7 @@ int32_t topology_check_graphml(const char* graphPath) {
     pthread_rwlock_init(&top->state_lock, NULL);
     pthread_mutex_init(&top->seal_lock, NULL);
     pthread_mutex_init(&top->cache_mu, NULL);
+    pthread_mutex_init(&top->batch_mu, NULL);
     for (int i = 0; i < NSHARD; ++i) pthread_mutex_init(&top->shards[i].mu, NULL);
     const int ok = load_graphml(top, graphPath) && strongly_connected(top);
     topo_release(top);
@@ -1326,6 +1338,10 @@ static uint64_t pair_key(int32_t x, int32_t y) { return (((uint64_t)(uint32_t)x 
 /* explicit entry (x, y): its store sequence (0 = none) and kind */
 static uint64_t explicit_seq(Topology* top, int32_t x, int32_t y, int32_t* kind) {
     if (atomic_load_explicit(&top->n_explicit, memory_order_acquire) == 0) return 0;
+    if (!atomic_load_explicit(&top->xflag[x], memory_order_acquire)) {
+        if (kind) *kind = K_NONE;
+        return 0;
+    }
     const uint64_t key = pair_key(x, y);
     Shard* sh = shard_of(top, key);
     pthread_mutex_lock(&sh->mu);
@@ -1339,6 +1355,7 @@ static uint64_t explicit_seq(Topology* top, int32_t x, int32_t y, int32_t* kind)
 static void explicit_store(Topology* top, int32_t x, int32_t y, int32_t kind, uint64_t seq) {
     const uint64_t key = pair_key(x, y);
     Shard* sh = shard_of(top, key);
+    atomic_store_explicit(&top->xflag[x], 1, memory_order_release);   /* (before the entry is visible) */
     pthread_mutex_lock(&sh->mu);
     PairRec* r = rec_locked(sh, key, 1);
     if (!r->seq) {
@@ -1643,24 +1660,191 @@ void topology_incrementPathPacketCounter(Topology* top, spe_in_addr_t srcAddress
     query(top, srcAddress, dstAddress, 1, &l, &r, NULL);   /* path->packetCount++, shd-path.c:53-56 */
 }
 
-/* Batches (worker_sendPacket's lookups for a whole round of packets).  Under
- * state_lock shared: every address resolved, and a published table that holds
- * them all (else the lock is dropped, a covering table sealed, and the batch
- * retried).  Returns the snapshot, or NULL with the lock released when a seal
- * failed. */
-static Snap* batch_snapshot(Topology* top, int64_t n, const spe_in_addr_t* src, const spe_in_addr_t* dst) {
+/* Batches (worker_sendPacket's lookups for a whole round of packets).
+ *
+ * Phase 1, in parallel (up to SHADOW_SPE_BATCH_THREADS threads, default 16, for
+ * batches of 64k queries and more), under state_lock shared: both addresses of
+ * every query resolved, the published table checked to hold them (else the lock
+ * is dropped, a covering table sealed and the phase redone), and the cache entry
+ * answering each query looked up read-only (find_entry).  Phase 2, in query
+ * order on the calling thread: every query phase 1 found no entry for runs the
+ * full cache model (cache_lookup, which may store).  The model only ever adds
+ * entries, first writer wins, and an entry found stays the one found: a store
+ * made by an earlier query of the batch can turn a later miss into a hit but never
+ * change a hit -- so the batch answers, counts and stores exactly as the same
+ * queries made one by one in order would (tests/test_topology_batch.py).  Then
+ * every table read of the batch at once: from the host mirror, or one device
+ * lookup launch for the lot (spe_lookup_batch_host). */
+enum { BQ_BAD = 0, BQ_HIT = 1, BQ_MISS = 2 };
+
+typedef struct {
+    Topology* top;
+    Snap* sn;
+    const spe_in_addr_t* src;
+    const spe_in_addr_t* dst;
+    int64_t a, b;
+    int32_t* sv;   /* resolved vertices (-1: unknown address) */
+    int32_t* dv;
+    int32_t* x;    /* the answering entry (x, y) of a hit */
+    int32_t* y;
+    uint8_t* st;   /* BQ_* */
+    int8_t* kind;
+    int uncovered;
+    /* the gather / finish passes */
+    int32_t* pairs;
+    const double* lat;
+    uint8_t* routable;
+    int64_t count;
+} BatchJob;
+
+static void* batch_phase1(void* p) {
+    BatchJob* j = p;
+    Topology* top = j->top;
+    Snap* sn = j->sn;
+    for (int64_t i = j->a; i < j->b; ++i) {
+        const int32_t sv = ip_get(top, j->src[i]), dv = ip_get(top, j->dst[i]);
+        j->sv[i] = sv;
+        j->dv[i] = dv;
+        if (sv < 0 || dv < 0) {
+            j->st[i] = BQ_BAD;
+            continue;
+        }
+        if (sn->slot_of_vertex[sv] < 0 || sn->slot_of_vertex[dv] < 0) {
+            j->uncovered = 1;
+            return NULL;
+        }
+        int32_t x, y, kind = K_NONE;
+        if (find_entry(top, sv, dv, !top->directed, &x, &y, &kind)) {
+            j->st[i] = BQ_HIT;
+            j->x[i] = x;
+            j->y[i] = y;
+            j->kind[i] = (int8_t)kind;
+        } else {
+            j->st[i] = BQ_MISS;
+        }
+    }
+    return NULL;
+}
+
+/* default answer mode, device reads: query i reads slot pair i (bad addresses -1) */
+static void* batch_gather(void* p) {
+    BatchJob* j = p;
+    const Snap* sn = j->sn;
+    for (int64_t i = j->a; i < j->b; ++i) {
+        const int bad = j->st[i] == BQ_BAD;
+        j->pairs[2 * i] = bad ? -1 : sn->slot_of_vertex[j->sv[i]];
+        j->pairs[2 * i + 1] = bad ? -1 : sn->slot_of_vertex[j->dv[i]];
+        j->count += bad;
+    }
+    return NULL;
+}
+
+static void* batch_finish(void* p) {
+    BatchJob* j = p;
+    for (int64_t i = j->a; i < j->b; ++i) {
+        j->routable[i] = j->lat[i] > -1.0;
+        j->count += j->routable[i];
+    }
+    return NULL;
+}
+
+/* jobs[0 .. T) of one pass: jobs[1 ..] on their own threads, jobs[0] on this one */
+static void batch_run(int T, BatchJob* jobs, void* (*fn)(void*)) {
+    pthread_t th[64];
+    int created[64] = {0};
+    for (int k = 1; k < T; ++k) created[k] = pthread_create(&th[k], NULL, fn, &jobs[k]) == 0;
+    fn(&jobs[0]);
+    for (int k = 1; k < T; ++k) {
+        if (created[k]) pthread_join(th[k], NULL);
+        else fn(&jobs[k]);   /* no thread: this one does the share */
+    }
+}
+
+static int batch_threads(int64_t n) {
+    if (n < 65536) return 1;
+    int t = 16;
+    const char* e = getenv("SHADOW_SPE_BATCH_THREADS");
+    if (e && atoi(e) > 0) t = atoi(e);
+    const long nc = sysconf(_SC_NPROCESSORS_ONLN);
+    if (nc > 0 && t > nc) t = (int)nc;
+    if ((int64_t)t > n / 16384) t = (int)(n / 16384);
+    return t < 1 ? 1 : (t > 64 ? 64 : t);
+}
+
+typedef struct {
+    int32_t *sv, *dv, *x, *y;
+    int32_t* pairs;   /* the device reads (slot pairs) and the query each answers */
+    int64_t* at;
+    uint8_t* st;
+    int8_t* kind;
+    void* mem;        /* one block for all the arrays */
+    Topology* held;   /* the Topology whose cached scratch (batch_mu) this is, else NULL */
+} BatchRes;
+
+static void batch_res_free(BatchRes* r) {
+    if (r->held) pthread_mutex_unlock(&r->held->batch_mu);
+    else free(r->mem);
+    memset(r, 0, sizeof *r);
+}
+
+/* 34 B per query in one block: the Topology's cached scratch when no other batch
+ * holds it (already faulted in: a fresh 360-MB block per 20M-query batch spent
+ * most of the batch in page faults, serialised across the threads), else a fresh one */
+static int batch_res_alloc(Topology* top, int64_t n, BatchRes* r) {
+    memset(r, 0, sizeof *r);
+    const size_t bytes = (size_t)n * (6 * sizeof(int32_t) + sizeof(int64_t) + 2) + 64;
+    if (pthread_mutex_trylock(&top->batch_mu) == 0) {
+        if (top->bscr_bytes < bytes) {
+            free(top->bscr);
+            top->bscr = malloc(bytes);
+            top->bscr_bytes = top->bscr ? bytes : 0;
+            if (top->bscr) memset(top->bscr, 0, bytes);
+        }
+        if (top->bscr) {
+            r->mem = top->bscr;
+            r->held = top;
+        } else {
+            pthread_mutex_unlock(&top->batch_mu);
+        }
+    }
+    if (!r->mem) r->mem = malloc(bytes);
+    if (!r->mem) return 0;
+    r->at = (int64_t*)r->mem;
+    r->sv = (int32_t*)(r->at + n);
+    r->dv = r->sv + n;
+    r->x = r->dv + n;
+    r->y = r->x + n;
+    r->pairs = r->y + n;
+    r->st = (uint8_t*)(r->pairs + 2 * n);
+    r->kind = (int8_t*)(r->st + n);
+    return 1;
+}
+
+/* Phase 1.  Returns the snapshot with state_lock held shared, or NULL (lock
+ * released) when no covering table could be sealed or memory ran out. */
+static Snap* batch_prepare(Topology* top, int64_t n, const spe_in_addr_t* src, const spe_in_addr_t* dst, BatchRes* r) {
+    if (!batch_res_alloc(top, n, r)) {
+        batch_res_free(r);
+        return NULL;
+    }
+    const int T = batch_threads(n);
+    BatchJob jobs[64];
     for (int attempt = 0; attempt < 64; ++attempt) {
         pthread_rwlock_rdlock(&top->state_lock);
         Snap* sn = top->snap;
         int covered = sn != NULL;
-        for (int64_t i = 0; i < n && covered; ++i) {
-            const int32_t sv = ip_get(top, src[i]), dv = ip_get(top, dst[i]);
-            if (sv >= 0 && dv >= 0) covered = sn->slot_of_vertex[sv] >= 0 && sn->slot_of_vertex[dv] >= 0;
+        if (covered) {
+            for (int k = 0; k < T; ++k)
+                jobs[k] = (BatchJob){top, sn, src, dst, n * k / T, n * (k + 1) / T,
+                                     r->sv, r->dv, r->x, r->y, r->st, r->kind, 0, NULL, NULL, NULL, 0};
+            batch_run(T, jobs, batch_phase1);
+            for (int k = 0; k < T; ++k) covered &= !jobs[k].uncovered;
         }
         if (covered) return sn;
         pthread_rwlock_unlock(&top->state_lock);
-        if (topology_seal(top) != SPE_OK) return NULL;
+        if (topology_seal(top) != SPE_OK) break;
     }
+    batch_res_free(r);
     return NULL;
 }
 
@@ -1679,55 +1863,87 @@ static void batch_min_callback(Topology* top, int min_updated) {
     }
 }
 
+/* Phase 2: the misses in query order (stores happen here), bad addresses logged
+ * in order; afterwards st[i] is BQ_HIT with (x, y, kind) or a failure. */
+static void batch_phase2(Topology* top, Snap* sn, int64_t n, const spe_in_addr_t* src, const spe_in_addr_t* dst,
+                         BatchRes* r, int* min_updated) {
+    for (int64_t i = 0; i < n; ++i) {
+        if (r->st[i] == BQ_BAD) {
+            batch_bad_address(top, r->sv[i], src[i], dst[i]);
+        } else if (r->st[i] == BQ_MISS) {
+            int32_t x, y, kind = K_NONE;
+            if (cache_lookup(top, sn, r->sv[i], r->dv[i], &x, &y, &kind, min_updated)) {
+                r->st[i] = BQ_HIT;
+                r->x[i] = x;
+                r->y[i] = y;
+                r->kind[i] = (int8_t)kind;
+            }
+        }
+    }
+}
+
 int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t* srcAddress,
                                   const spe_in_addr_t* dstAddress, double* latency, double* reliability,
                                   uint8_t* routable) {
     if (!top || n < 0 || (n > 0 && (!srcAddress || !dstAddress || !latency || !reliability || !routable))) return -1;
     if (n == 0) return 0;
-    for (int64_t i = 0; i < n; ++i) {
-        latency[i] = reliability[i] = -1.0;
-        routable[i] = 0;
-    }
     const int timing = getenv("SHADOW_SPE_BATCH_TIMING") != NULL;
     const double t0 = timing ? now_s() : 0.0;
-    Snap* sn = batch_snapshot(top, n, srcAddress, dstAddress);
+    BatchRes r;
+    Snap* sn = batch_prepare(top, n, srcAddress, dstAddress, &r);
     if (!sn) return -1;
     const double t1 = timing ? now_s() : 0.0;
-    /* the cache model per query (which Path answers it, the stores a miss makes,
-     * the log lines), then every table read of the batch at once: from the host
-     * mirror, or one device lookup launch for the lot (spe_lookup_batch_host) */
+    int min_updated = 0;
+    batch_phase2(top, sn, n, srcAddress, dstAddress, &r, &min_updated);
+    const double t2 = timing ? now_s() : 0.0;
     /* (random reads of a whole-table host mirror cost ~100 ns each; one device launch
      * for a large batch costs ~25 B of PCIe traffic per query) */
     const int dev = n >= (sn->mlat ? 4096 : 256);
-    int32_t* pairs = dev ? malloc((size_t)n * 2 * sizeof(int32_t)) : NULL;
-    int64_t* at = dev ? malloc((size_t)n * sizeof(int64_t)) : NULL;
-    int64_t nd = 0;
-    int min_updated = 0;
     const int ref = top->cache_mode == TOPOLOGY_ANSWER_REFERENCE;
-    for (int64_t i = 0; i < n; ++i) {
-        const int32_t sv = ip_get(top, srcAddress[i]), dv = ip_get(top, dstAddress[i]);
-        if (sv < 0 || dv < 0) {
-            batch_bad_address(top, sv, srcAddress[i], dstAddress[i]);
-            continue;
+    int32_t* pairs = r.pairs;
+    int64_t* at = r.at;
+    int64_t nd = 0;
+    const int T = batch_threads(n);
+    BatchJob jobs[64];
+    if (dev && !ref) {   /* every query reads its own (s, t): slot pairs in parallel */
+        for (int k = 0; k < T; ++k)
+            jobs[k] = (BatchJob){top, sn, NULL, NULL, n * k / T, n * (k + 1) / T, r.sv, r.dv, NULL, NULL, r.st,
+                                 NULL, 0, pairs, NULL, NULL, 0};
+        batch_run(T, jobs, batch_gather);
+        int64_t nbad = 0;
+        for (int k = 0; k < T; ++k) nbad += jobs[k].count;
+        if (nbad == 0) {
+            nd = n;
+        } else {   /* compact the readable ones */
+            for (int64_t i = 0; i < n; ++i) {
+                latency[i] = reliability[i] = -1.0;
+                if (pairs[2 * i] < 0) continue;
+                pairs[2 * nd] = pairs[2 * i];
+                pairs[2 * nd + 1] = pairs[2 * i + 1];
+                at[nd++] = i;
+            }
         }
-        int32_t x, y, kind = K_NONE;
-        const int found = cache_lookup(top, sn, sv, dv, &x, &y, &kind, &min_updated);
-        int32_t s = sn->slot_of_vertex[sv], t = sn->slot_of_vertex[dv];
+    }
+    for (int64_t i = 0; i < n && !(dev && !ref); ++i) {
+        latency[i] = reliability[i] = -1.0;
+        if (r.st[i] == BQ_BAD) continue;
+        const int hit = r.st[i] == BQ_HIT;
+        int32_t s = sn->slot_of_vertex[r.sv[i]], t = sn->slot_of_vertex[r.dv[i]];
         if (ref) {
-            if (!found) {   /* :2023-2029 */
-                tlog(top, LOG_ERROR, "unable to find path between vertex %d (%s) and vertex %d (%s)", sv,
-                     top->vstr[VS_ID][sv], dv, top->vstr[VS_ID][dv]);
+            if (!hit) {   /* :2023-2029 */
+                tlog(top, LOG_ERROR, "unable to find path between vertex %d (%s) and vertex %d (%s)", r.sv[i],
+                     top->vstr[VS_ID][r.sv[i]], r.dv[i], top->vstr[VS_ID][r.dv[i]]);
                 continue;
             }
-            if (kind == K_SELF) {
+            if (r.kind[i] == K_SELF) {
                 spe_entry e;
-                spe_graph_self_path(top->graph, x, &e);
+                spe_graph_self_path(top->graph, r.x[i], &e);
                 latency[i] = e.latency;
                 reliability[i] = e.reliability;
                 continue;
             }
-            s = sn->slot_of_vertex[x];
-            t = sn->slot_of_vertex[y];
+            s = sn->slot_of_vertex[r.x[i]];
+            t = sn->slot_of_vertex[r.y[i]];
         }
         if (dev) {
             pairs[2 * nd] = s;
@@ -1737,8 +1953,13 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
             snap_value(top, sn, s, t, &latency[i], &reliability[i]);
         }
     }
-    const double t2 = timing ? now_s() : 0.0;
-    if (nd > 0) {
+    const double t3 = timing ? now_s() : 0.0;
+    if (nd == n) {   /* every query reads the table: answers straight into the outputs */
+        if (spe_lookup_batch_host(sn->table, pairs, nd, latency, reliability, routable) != SPE_OK) {
+            tlog(top, LOG_WARNING, "batched path table read failed (%s): reading per query", spe_last_error());
+            for (int64_t k = 0; k < nd; ++k) snap_value(top, sn, pairs[2 * k], pairs[2 * k + 1], &latency[k], &reliability[k]);
+        }
+    } else if (nd > 0) {
         double* lr = malloc((size_t)nd * 2 * sizeof(double));
         uint8_t* okd = malloc((size_t)nd);
         if (lr && okd && spe_lookup_batch_host(sn->table, pairs, nd, lr, lr + nd, okd) == SPE_OK) {
@@ -1756,35 +1977,33 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
     }
     pthread_rwlock_unlock(&top->state_lock);
     if (timing)
-        fprintf(stderr, "[topology] batch of %lld: snapshot %.3f s, cache model %.3f s, table reads %.3f s\n",
-                (long long)n, t1 - t0, t2 - t1, now_s() - t2);
-    free(pairs);
-    free(at);
+        fprintf(stderr,
+                "[topology] batch of %lld: resolve + cached entries %.3f s, misses in order %.3f s, "
+                "gather %.3f s, table reads %.3f s\n",
+                (long long)n, t1 - t0, t2 - t1, t3 - t2, now_s() - t3);
+    batch_res_free(&r);
     batch_min_callback(top, min_updated);
+    for (int k = 0; k < T; ++k)
+        jobs[k] = (BatchJob){top, NULL, NULL, NULL, n * k / T, n * (k + 1) / T, NULL, NULL, NULL, NULL, NULL, NULL,
+                             0, NULL, latency, routable, 0};
+    batch_run(T, jobs, batch_finish);
     int64_t nok = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        routable[i] = latency[i] > -1.0;
-        nok += routable[i];
-    }
+    for (int k = 0; k < T; ++k) nok += jobs[k].count;
     return nok;
 }
 
 void topology_incrementPathPacketCounterBatch(Topology* top, int64_t n, const spe_in_addr_t* srcAddress,
                                               const spe_in_addr_t* dstAddress) {
     if (!top || n <= 0 || !srcAddress || !dstAddress) return;
-    Snap* sn = batch_snapshot(top, n, srcAddress, dstAddress);
+    BatchRes r;
+    Snap* sn = batch_prepare(top, n, srcAddress, dstAddress, &r);
     if (!sn) return;
     int min_updated = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        const int32_t sv = ip_get(top, srcAddress[i]), dv = ip_get(top, dstAddress[i]);
-        if (sv < 0 || dv < 0) {
-            batch_bad_address(top, sv, srcAddress[i], dstAddress[i]);
-            continue;
-        }
-        int32_t x, y, kind = K_NONE;
-        if (cache_lookup(top, sn, sv, dv, &x, &y, &kind, &min_updated)) pair_count(top, x, y, 1);
-    }
+    batch_phase2(top, sn, n, srcAddress, dstAddress, &r, &min_updated);
+    for (int64_t i = 0; i < n; ++i)   /* (counts commute: order is immaterial here) */
+        if (r.st[i] == BQ_HIT) pair_count(top, r.x[i], r.y[i], 1);
     pthread_rwlock_unlock(&top->state_lock);
+    batch_res_free(&r);
     batch_min_callback(top, min_updated);
 }
 
