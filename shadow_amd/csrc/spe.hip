@@ -5395,7 +5395,7 @@ static int build_shared(spe_table* t, int32_t block_begin, int32_t block_end, hi
                         // an offset source of a flagged root (a core source is its own root: exact)
                         if (c == -3) {
                             const int32_t x = h.core_id[(size_t)v];
-                            for (int q = 0; q < 3; ++q) d |= bad[(size_t)nbr(x, q)] != 0;
+                            for (int q = 0; q < ndeg(x); ++q) d |= bad[(size_t)nbr(x, q)] != 0;
                         } else if (c >= 0 && h.core_id[(size_t)v] != c) {
                             d = bad[(size_t)c] != 0;
                         }
