@@ -134,3 +134,38 @@ def test_shim_default_is_bit_exact_on_decimal_latencies(tmp_path, monkeypatch):
     moved = int((ns(d["lat"][okr]) != ns(ref["lat"][okr])).sum())
     print(f"shared-tree rows: {moved} of {int(okr.sum())} pairs change ceil(latency * 1e6)")
     assert g.info()["sums_exact"] == 0
+
+
+@pytest.mark.parametrize("threads", ["1", "8"])
+def test_threaded_batch_equals_single_calls_in_order(tmp_path, monkeypatch, threads):
+    """A batch large enough for the threaded path (>= 64k queries): phase 1 looks
+    cache entries up on several threads, phase 2 replays the misses in order.  In
+    reference answer mode the answers, the cached entries and the packet counts
+    must equal the same queries made one by one in order (the model only adds
+    entries, first writer wins: a found entry never changes)."""
+    monkeypatch.setenv("SHADOW_SPE_PATH_CACHE", "reference")
+    monkeypatch.setenv("SHADOW_SPE_MIRROR_BYTES", "0")
+    monkeypatch.setenv("SHADOW_SPE_BATCH_THREADS", threads)
+    t, ips, verts = _case(seed=13, n=300, k=120)
+    a = _topology(tmp_path, t, ips, "a.graphml")
+    b = _topology(tmp_path, t, ips, "b.graphml")
+    aa = _attach(a, ips, verts)
+    ab = _attach(b, ips, verts)
+    rng = np.random.default_rng(8)
+    qi = rng.integers(0, len(verts), (70000, 2))
+    qi[::997, 1] = qi[::997, 0]   # some (s, s) queries: SELF entries
+    ok, lat, rel = a.path_info_batch(aa[qi[:, 0]], aa[qi[:, 1]])
+    single = [b.path_info(int(ab[x]), int(ab[y])) for x, y in qi]
+    assert [bool(x) for x in ok] == [s[0] for s in single]
+    np.testing.assert_array_equal(lat, [s[1] for s in single])
+    np.testing.assert_array_equal(rel, [s[2] for s in single])
+    assert a.cached_paths() == b.cached_paths()
+    ci = rng.integers(0, len(verts), (70000, 2))
+    a.count_packets_batch(aa[ci[:, 0]], aa[ci[:, 1]])
+    for x, y in ci:
+        b.count_packet(int(ab[x]), int(ab[y]))
+    for x in range(0, len(verts), 7):
+        for y in range(0, len(verts), 3):
+            assert a.packets(int(aa[x]), int(aa[y])) == b.packets(int(ab[x]), int(ab[y]))
+    a.close()
+    b.close()
