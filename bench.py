@@ -684,9 +684,18 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
                 "shared_anchor_trees": bool(lay.get("shared_sources", 0)),
                 "lanes_per_group": lay["lanes_per_group"],
                 "bytes_basis": "relaxation graph: 12 m_relax + 28 n_relax + 8 (SURVEY 8d B_s minus the row stage)"}
+        if relaxed != done and relax_s > 0:
+            # the same relaxation time priced on every source row it serves (derived rows
+            # and shared anchors included): what the reference's per-source Dijkstra
+            # would move for all of them.  `frac` above stays on the lanes relaxed.
+            ps = b_relax * done / relax_s / 1e9
+            roof["per_source_basis"] = {"achieved": round(ps, 1), "frac": round(ps / HBM_PEAK_GBS, 4),
+                                        "sources_per_step": round(done / steps)}
         rw = kp["rows"]
         rows_s = rw["ms"] / 1e3
-        extra["roofline_rows"] = {"kernel": "k_rows_sssp", "achieved": round(b_rows * done / rows_s / 1e9, 1)
+        rows_k = ("k_rows_derived (+ k_expand_removed)" if derived_run[0] > 0 else
+                  "k_rows_shared_lds" if lay.get("shared_sources", 0) else "k_rows_sssp")
+        extra["roofline_rows"] = {"kernel": rows_k, "achieved": round(b_rows * done / rows_s / 1e9, 1)
                                   if rows_s > 0 else 0.0, "unit": "GB/s", "launches": rw["launches"],
                                   "launch_avg_us": round(1e3 * rw["ms"] / max(1, rw["launches"]), 2),
                                   "algorithmic_bytes_per_source": b_rows}
