@@ -1739,6 +1739,13 @@ static void* batch_gather(void* p) {
     return NULL;
 }
 
+static void* batch_count(void* p) {   /* packet counts of the hits (they commute: any order) */
+    BatchJob* j = p;
+    for (int64_t i = j->a; i < j->b; ++i)
+        if (j->st[i] == BQ_HIT) pair_count(j->top, j->x[i], j->y[i], 1);
+    return NULL;
+}
+
 static void* batch_finish(void* p) {
     BatchJob* j = p;
     for (int64_t i = j->a; i < j->b; ++i) {
@@ -2000,8 +2007,12 @@ void topology_incrementPathPacketCounterBatch(Topology* top, int64_t n, const sp
     if (!sn) return;
     int min_updated = 0;
     batch_phase2(top, sn, n, srcAddress, dstAddress, &r, &min_updated);
-    for (int64_t i = 0; i < n; ++i)   /* (counts commute: order is immaterial here) */
-        if (r.st[i] == BQ_HIT) pair_count(top, r.x[i], r.y[i], 1);
+    const int T = batch_threads(n);
+    BatchJob jobs[64];
+    for (int k = 0; k < T; ++k)
+        jobs[k] = (BatchJob){top, sn, NULL, NULL, n * k / T, n * (k + 1) / T, NULL, NULL, r.x, r.y, r.st, NULL, 0,
+                             NULL, NULL, NULL, 0};
+    batch_run(T, jobs, batch_count);
     pthread_rwlock_unlock(&top->state_lock);
     batch_res_free(&r);
     batch_min_callback(top, min_updated);
