@@ -265,7 +265,8 @@ typedef struct spe_build_stats {
                                      * roots) the last build ran, padding excluded */
     int32_t fallback_blocks;        /* shared anchor trees: source blocks rebuilt lane per source */
     int64_t derived_sources;        /* contracted shared tables: sources whose rows came from their
-                                     * three neighbours' roots, without a relaxation lane */
+                                     * neighbours' roots (three for a contracted vertex, four for a
+                                     * degree-4 one), without a relaxation lane */
 } spe_build_stats;
 
 const char* spe_last_error(void);
