@@ -10,13 +10,16 @@
  *   master:  topology_free                               shd-master.c:100
  * Here the three per-packet calls are topology_getPathInfo (one table read);
  * every 64th packet is re-asked through the three separate getters, which must
- * agree bit for bit.  With late_hosts > 0 the main thread attaches that many
+ * agree bit for bit.  With batch > 0 a worker instead collects rounds of `batch`
+ * packets and answers each round with one topology_getPathInfoBatch call (and
+ * counts the routable ones with one topology_incrementPathPacketCounterBatch),
+ * every 64th packet of a round re-asked through topology_getPathInfo.  With late_hosts > 0 the main thread attaches that many
  * more hosts AFTER the table is sealed while the workers are querying (a
  * replacement table is built and swapped in under them), and the workers also
  * address the late hosts once attached.  At the end the packet counters of
  * every cached path must add up to the number of counted packets exactly.
  *
- *   shd_topology_demo <graph.graphml> <hosts> <packets> [threads] [seed] [late_hosts]
+ *   shd_topology_demo <graph.graphml> <hosts> <packets> [threads] [seed] [late_hosts] [batch]
  * prints one JSON line; exit 0 ok, 1 disagreement, 2 setup failure. */
 #include <arpa/inet.h>
 #include <pthread.h>
@@ -43,13 +46,60 @@ typedef struct {
     Topology* top;
     int32_t hosts;         /* hosts addressed: the first ones plus the late ones */
     int64_t packets;
+    int64_t batch;         /* packets per round through the batch calls (0: per packet) */
     unsigned seed;
     int64_t routable, mismatches, skipped;
     double latency_sum;
 } Worker;
 
+static void worker_batches(Worker* w) {
+    spe_in_addr_t* src = (spe_in_addr_t*)malloc((size_t)w->batch * sizeof(spe_in_addr_t));
+    spe_in_addr_t* dst = (spe_in_addr_t*)malloc((size_t)w->batch * sizeof(spe_in_addr_t));
+    spe_in_addr_t* csrc = (spe_in_addr_t*)malloc((size_t)w->batch * sizeof(spe_in_addr_t));
+    spe_in_addr_t* cdst = (spe_in_addr_t*)malloc((size_t)w->batch * sizeof(spe_in_addr_t));
+    double* lat = (double*)malloc((size_t)w->batch * sizeof(double));
+    double* rel = (double*)malloc((size_t)w->batch * sizeof(double));
+    uint8_t* ok = (uint8_t*)malloc((size_t)w->batch);
+    for (int64_t p0 = 0; p0 < w->packets; p0 += w->batch) {
+        int64_t n = 0;
+        for (int64_t p = p0; p < p0 + w->batch && p < w->packets; ++p) {
+            const spe_in_addr_t s = host_addr(rand_r(&w->seed) % w->hosts);
+            const spe_in_addr_t d = host_addr(rand_r(&w->seed) % w->hosts);
+            if (topology_attached_vertex(w->top, s) < 0 || topology_attached_vertex(w->top, d) < 0) {
+                ++w->skipped;
+                continue;
+            }
+            src[n] = s;
+            dst[n] = d;
+            ++n;
+        }
+        topology_getPathInfoBatch(w->top, n, src, dst, lat, rel, ok);
+        int64_t nc = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            if (ok[i]) {
+                ++w->routable;
+                w->latency_sum += lat[i];
+                csrc[nc] = src[i];
+                cdst[nc] = dst[i];
+                ++nc;
+            }
+            if ((i & 63) == 0) {
+                double l1 = 0.0, r1 = 0.0;
+                const int32_t ok1 = topology_getPathInfo(w->top, src[i], dst[i], &l1, &r1);
+                if (ok1 != (ok[i] != 0) || (ok1 && (l1 != lat[i] || r1 != rel[i]))) ++w->mismatches;
+            }
+        }
+        topology_incrementPathPacketCounterBatch(w->top, nc, csrc, cdst);
+    }
+    free(src); free(dst); free(csrc); free(cdst); free(lat); free(rel); free(ok);
+}
+
 static void* worker_run(void* arg) {
     Worker* w = (Worker*)arg;
+    if (w->batch > 0) {
+        worker_batches(w);
+        return NULL;
+    }
     for (int64_t p = 0; p < w->packets; ++p) {
         const spe_in_addr_t s = host_addr(rand_r(&w->seed) % w->hosts);
         const spe_in_addr_t d = host_addr(rand_r(&w->seed) % w->hosts);
@@ -76,7 +126,8 @@ static void* worker_run(void* arg) {
 
 int main(int argc, char** argv) {
     if (argc < 4) {
-        fprintf(stderr, "usage: %s <graph.graphml> <hosts> <packets> [threads] [seed] [late_hosts]\n", argv[0]);
+        fprintf(stderr, "usage: %s <graph.graphml> <hosts> <packets> [threads] [seed] [late_hosts] [batch]\n",
+                argv[0]);
         return 2;
     }
     const int32_t hosts = atoi(argv[2]);
@@ -84,7 +135,8 @@ int main(int argc, char** argv) {
     const int32_t threads = argc > 4 ? atoi(argv[4]) : 4;
     unsigned seed = argc > 5 ? (unsigned)atoi(argv[5]) : 1u;
     const int32_t late = argc > 6 ? atoi(argv[6]) : 0;
-    if (hosts < 1 || packets < 0 || threads < 1 || late < 0) return 2;
+    const int64_t batch = argc > 7 ? atoll(argv[7]) : 0;
+    if (hosts < 1 || packets < 0 || threads < 1 || late < 0 || batch < 0) return 2;
 
     const double t0 = now_s();
     Topology* top = topology_new(argv[1]);
@@ -124,6 +176,7 @@ int main(int argc, char** argv) {
         ws[k].top = top;
         ws[k].hosts = hosts + late;
         ws[k].packets = packets / threads + (k < packets % threads ? 1 : 0);
+        ws[k].batch = batch;
         ws[k].seed = seed + 7919u * (unsigned)(k + 1);
         pthread_create(&th[k], NULL, worker_run, &ws[k]);
     }
@@ -163,10 +216,11 @@ int main(int argc, char** argv) {
            "\"load_s\": %.4f, \"attach_s\": %.4f, \"seal_s\": %.4f, \"packets\": %lld, \"threads\": %d, "
            "\"packets_per_s\": %.1f, \"routable\": %lld, \"latency_sum\": %.6f, \"min_path_latency\": %.6f, "
            "\"count_pair_0_0\": %llu, \"late_hosts\": %d, \"skipped\": %lld, \"counted\": %llu, "
-           "\"mismatches\": %lld}\n",
+           "\"mismatches\": %lld, \"batch\": %lld}\n",
            argv[1], topology_vertex_count(top), hosts, distinct, t1 - t0, t2 - t1, t3 - t2, (long long)packets,
            threads, packets > 0 ? (double)packets / (t4 - t3) : 0.0, (long long)routable, latency_sum, min_lat,
-           (unsigned long long)c00, late, (long long)skipped, (unsigned long long)counted, (long long)mismatches);
+           (unsigned long long)c00, late, (long long)skipped, (unsigned long long)counted, (long long)mismatches,
+           (long long)batch);
     free(th);
     free(ws);
     topology_free(top);

@@ -79,8 +79,8 @@ def test_demo_rejects_invalid_graph(tmp_path):
     assert r.returncode == 2 and "topology_new failed" in r.stderr
 
 
-def _run_demo(path, hosts, packets, threads=4, seed=1, late=0):
-    r = subprocess.run([DEMO, str(path), str(hosts), str(packets), str(threads), str(seed), str(late)],
+def _run_demo(path, hosts, packets, threads=4, seed=1, late=0, batch=0):
+    r = subprocess.run([DEMO, str(path), str(hosts), str(packets), str(threads), str(seed), str(late), str(batch)],
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout + r.stderr
     return json.loads(r.stdout.strip().splitlines()[-1])
@@ -129,4 +129,20 @@ def test_demo_attach_after_seal_under_concurrent_readers(tmp_path):
     graphs.write_graphml(t, str(p))
     d = _run_demo(p, 100, 300_000, threads=4, late=200)
     assert d["mismatches"] == 0 and d["late_hosts"] == 200
+    assert d["counted"] == d["routable"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.engine_fixed
+def test_demo_batched_rounds_with_late_hosts(tmp_path):
+    """Workers answer rounds of 80k packets with topology_getPathInfoBatch (the
+    threaded path) and count them with topology_incrementPathPacketCounterBatch,
+    while the main thread attaches hosts after sealing: every 64th packet of a
+    round agrees bit for bit with topology_getPathInfo, and the counters of all
+    cached paths add up to the packets counted."""
+    t = graphs.gen_random_small(2000, 6000, 13)
+    p = tmp_path / "batch.graphml"
+    graphs.write_graphml(t, str(p))
+    d = _run_demo(p, 300, 640_000, threads=4, late=100, batch=80_000)
+    assert d["mismatches"] == 0 and d["batch"] == 80_000
     assert d["counted"] == d["routable"] > 0
