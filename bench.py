@@ -33,6 +33,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "SSSP sources/sec + full path-table time, % HBM roofline, at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# FP64 vector: 78.6 TFLOP/s counts an FMA as two flops; an add or a min is one
+# instruction, so (min, +) work issues at most 39.3 T single-op instructions/s
+FP64_OP_PEAK_TOPS = 39.3
 
 
 def workload(name: str):
@@ -72,6 +75,24 @@ def workload(name: str):
     return top, att, desc
 
 
+def host_cores():
+    """Every host core this process may run on (sched_getaffinity: on the GPU box
+    the whole machine, 256 threads), plus the cgroup CPU quota when one is set --
+    the all-cores CPU legs run one thread per core and state both."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(float(q) / float(per), 2)
+    except (OSError, ValueError):
+        pass
+    return n, quota
+
+
 def cpu_baseline(top, att, seconds: float, sources: int = 0, seed: int = 6):
     """Oracle (C restatement of igraph Dijkstra + Shadow row rules, -O2) timed on a
     sample of this workload's sources: 1 core (the reference serialises its
@@ -104,11 +125,11 @@ def cpu_baseline(top, att, seconds: float, sources: int = 0, seed: int = 6):
                 break
     except OSError:
         pass
-    nt = min(16, os.cpu_count() or 1)
+    nt, quota = host_cores()
     done_all, t1 = 0, time.perf_counter()
     while time.perf_counter() - t1 < seconds / 4:
-        o.rows(take(done + done_all, 8 * nt), att, nthreads=nt)
-        done_all += 8 * nt
+        o.rows(take(done + done_all, 2 * nt), att, nthreads=nt)
+        done_all += 2 * nt
     el_all = time.perf_counter() - t1
     dij = (f"Dijkstra-only {done / dj:.1f} sources/s" if dj > 0
            else "no Dijkstra runs: every pair is DIRECT (complete graph, shd-topology.c:2002-2008)")
@@ -116,16 +137,26 @@ def cpu_baseline(top, att, seconds: float, sources: int = 0, seed: int = 6):
             "sample": f"{done} seeded-random source rows (seed {seed}, cycling over A = {A}) x {A} targets, full "
                       f"row build, {el:.1f} s; {dij}",
             "optimistic_all_cores": {"value": round(done_all / el_all, 1), "threads": nt,
+                                     "cgroup_cpu_quota": quota,
                                      "sample": f"{done_all} source rows, {el_all:.1f} s"},
             "cpu_model": model, "host_nproc": os.cpu_count()}
 
 
-def pmc_traffic(args, kernel, config=None):
-    """HBM bytes per dispatch of `kernel` from a committed PMC summary (separate
-    rocprofv3 --pmc passes of this same bench command), or None."""
+def pmc_key(config: str, world: int, groups: int, exact: bool = False) -> str:
+    """What a PMC summary must have been measured on to be this line's traffic:
+    the config, the GPU count and the build shape (groups per launch, exact mode)."""
+    return f"{config}|n{world}|g{groups}|{'exact' if exact else 'default'}"
+
+
+def pmc_traffic(args, kernel, config=None, key=None):
+    """HBM bytes per dispatch of `kernel` from a PMC summary (separate rocprofv3
+    --pmc passes of this same bench command, tools/pmc_to_json.py), or None.  A
+    summary is attached only when it records the same pmc_key as this run (config,
+    N, groups per launch, build mode): traffic measured on another shape is not
+    this line's traffic."""
     path = args.pmc_json
     if path is None:   # the newest committed summary of this config
-        for rnd in ("r04", "r03", "r02", "r01"):
+        for rnd in ("r05", "r04", "r03", "r02", "r01"):
             cand = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{config or args.config}.json")
             if os.path.exists(cand):
                 path = cand
@@ -133,11 +164,14 @@ def pmc_traffic(args, kernel, config=None):
     if not path:
         return None
     try:
-        k = json.load(open(path))["kernels"][kernel]
+        doc = json.load(open(path))
+        if key is not None and doc.get("pmc_key") != key:
+            return None
+        k = doc["kernels"][kernel]
         return {"hbm_bytes_per_launch": round(k["hbm_bytes_per_dispatch"]),
                 "fetch_bytes_per_launch": round(k["fetch_bytes_per_dispatch"]),
                 "write_bytes_per_launch": round(k["write_bytes_per_dispatch"]),
-                "source": os.path.relpath(path, ROOT)}
+                "source": os.path.relpath(path, ROOT), "pmc_key": doc.get("pmc_key")}
     except (KeyError, OSError, ValueError):
         return None
 
@@ -198,6 +232,7 @@ def bench_lookup(args, rank=0, world=1, local=0, dist=None):
         el = float(x.item())
     if rank != 0:
         return
+    c5name = "c5" if args.c5_table == "c3" else "c5_on_c4"
     value = world * q * steps / el
     ach = 41.0 * q / kern_s / 1e9
     cpu = None
@@ -210,9 +245,9 @@ def bench_lookup(args, rank=0, world=1, local=0, dist=None):
             "config": {"workload": f"C5: {q} uniform (s,t) slot pairs per GPU (seed 5 + rank) on the {desc} table",
                        "parallelism": f"{world} replica(s) of the table, each GPU answering its own queries (no communication)"},
             "roofline": {"bound": "hbm", "kernel": "k_lookup", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, "k_lookup", "c5" if args.c5_table == "c3" else "c5_on_c4"),
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, "k_lookup", c5name, pmc_key(c5name, world, 0)),
                          "algorithmic_bytes_per_query": 41},
-            "cpu_baseline": cpu}
+            "cpu_baseline": cpu, "pmc_key": pmc_key(c5name, world, 0)}
     if cpu:
         line["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)
     print(json.dumps(line), flush=True)
@@ -236,15 +271,18 @@ def cpu_lookup_baseline(A: int, seconds: float, seed: int = 5):
         c.lookup(sip, dip, nthreads=1)
         done += npairs
     el = time.perf_counter() - t0
-    nt = min(16, os.cpu_count() or 1)
-    t1 = time.perf_counter()
-    c.lookup(sip, dip, nthreads=nt)
-    c.lookup(sip, dip, nthreads=nt)
+    nt, quota = host_cores()
+    c.lookup(sip, dip, nthreads=nt)   # threads started
+    reps, t1 = 0, time.perf_counter()
+    while reps < 2 or time.perf_counter() - t1 < seconds / 4:
+        c.lookup(sip, dip, nthreads=nt)
+        reps += 1
     el_all = time.perf_counter() - t1
     return {"value": round(done / el, 1), "unit": "queries/s", "cores": 1, "kind": "port",
             "sample": f"{done} lookups over a 4M-pair cache (seed {seed}): 2 IP->slot probes + src and (src,dst) "
                       f"cache probes per query, {el:.1f} s",
-            "optimistic_all_cores": {"value": round(2 * npairs / el_all, 1), "threads": nt}}
+            "optimistic_all_cores": {"value": round(reps * npairs / el_all, 1), "threads": nt,
+                                     "cgroup_cpu_quota": quota}}
 
 
 def bench_complete(args):
@@ -422,15 +460,18 @@ def bench_fw(args):
             "dtype": "f64", "data": "synthetic", "full_table_time_s": round(el, 4),
             "config": {"workload": desc, "n_relax": n, "ld": ld, "attached": A},
             "roofline": {"bound": "fp64-valu", "kernel": "k_fw3_rest (closure carrying the triple)",
-                         "achieved": round(2 * relax / closure / 1e12, 2), "peak": 78.6, "unit": "TFLOP/s",
-                         "frac": round(2 * relax / closure / 1e12 / 78.6, 4),
-                         "note": "2 FP64 ops (add, min) per (min,+) relaxation, ld^3 relaxations; carrying R and "
-                                 "N adds a multiply and three selects per relaxation",
-                         "traffic": pmc_traffic(args, "k_fw3_rest")},
+                         "achieved": round(2 * relax / closure / 1e12, 2), "peak": FP64_OP_PEAK_TOPS,
+                         "unit": "Tops/s", "frac": round(2 * relax / closure / 1e12 / FP64_OP_PEAK_TOPS, 4),
+                         "note": "2 FP64 vector instructions (v_add_f64, v_min_f64) per (min,+) relaxation, ld^3 "
+                                 "relaxations, against the FP64 vector instruction peak: 78.6 TFLOP/s counts an FMA "
+                                 "as 2 flops, so single-op instructions issue at 39.3 T/s; carrying R and N adds a "
+                                 "multiply and three selects per relaxation (not counted)",
+                         "distance_only_frac": round(2 * relax / dist_only / 1e12 / FP64_OP_PEAK_TOPS, 4),
+                         "traffic": pmc_traffic(args, "k_fw3_rest", "c2fw", pmc_key("c2fw", 1, 0))},
             "closure_triple_s": round(closure, 4), "closure_distance_only_s": round(dist_only, 4),
             "fw_kernels_ms_in_table_build": round(fw_ms, 2), "rows_ms": round(kp["rows"]["ms"], 2),
             "lds_engine_table_s": round(lds_s, 4),
-            "all_runs_s": [round(r[0], 4) for r in runs]}
+            "all_runs_s": [round(r[0], 4) for r in runs], "pmc_key": pmc_key("c2fw", 1, 0)}
     print(json.dumps(line), flush=True)
 
 
@@ -549,7 +590,7 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
     # into the caller's buffers (spe_table_build_blocks_into); lr doubles as its
     # nominal external storage
     t = spe.PathTable(g, att, blocks=(0, nblk), ext=[lr.data_ptr(), lr.data_ptr(), lr.data_ptr()], groups=gpl,
-                      engine=args.engine)
+                      engine=args.engine, exact_sources=bool(args.exact))
     if gpl == 0:
         gpl = t.layout()["groups_per_launch"]
     calib = None
@@ -657,6 +698,7 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
     lds = kp is not None and kp["lds"]["launches"] > 0
     direct = kp is not None and kp["direct"]["launches"] > 0 and kp["relax"]["launches"] == 0 and not lds
     b_relax, b_rows = relax_bytes(info, A, lds, direct)
+    key = pmc_key(config, world, gpl, args.exact)
     roof, extra = None, {}
     if kp is not None:
         # the batch engine's relaxation kernel: k_relax (64 sources per row), k_relax_s
@@ -675,7 +717,7 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
         roof = {"bound": "hbm", "kernel": kname + (" (SSSP + rows, LDS-resident state)" if lds else
                                                    (" (DIRECT rows)" if direct else " (SSSP stage)")),
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(args, kname, config), "launches": rl["launches"],
+                "traffic": pmc_traffic(args, kname, config, key), "launches": rl["launches"],
                 "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
                 "algorithmic_bytes_per_source": b_relax,
                 "relaxed_lanes_per_step": round(relaxed / steps),
@@ -684,13 +726,6 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
                 "shared_anchor_trees": bool(lay.get("shared_sources", 0)),
                 "lanes_per_group": lay["lanes_per_group"],
                 "bytes_basis": "relaxation graph: 12 m_relax + 28 n_relax + 8 (SURVEY 8d B_s minus the row stage)"}
-        if relaxed != done and relax_s > 0:
-            # the same relaxation time priced on every source row it serves (derived rows
-            # and shared anchors included): what the reference's per-source Dijkstra
-            # would move for all of them.  `frac` above stays on the lanes relaxed.
-            ps = b_relax * done / relax_s / 1e9
-            roof["per_source_basis"] = {"achieved": round(ps, 1), "frac": round(ps / HBM_PEAK_GBS, 4),
-                                        "sources_per_step": round(done / steps)}
         rw = kp["rows"]
         rows_s = rw["ms"] / 1e3
         rows_k = ("k_rows_derived (+ k_expand_removed)" if derived_run[0] > 0 else
@@ -714,6 +749,11 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
             "config": {"workload": desc, "n": info["n_vertices"], "n_relax": info["n_relax_vertices"],
                        "m_relax": info["n_relax_entries"], "attached": A, "slot_order": "spe_order_sources",
                        "slot_order_ms": round(1e3 * t_ord, 1),
+                       "build": ("exact_sources=1: every source on its own relaxation lane, latency / reliability "
+                                 "the path-order folds bit for bit (what topology_seal builds on non-dyadic "
+                                 "latencies)" if args.exact else
+                                 "library default: derived / shared-anchor rows (routes exact, latency / "
+                                 "reliability within 1e-12 relative)"),
                        "step": "one whole path table (every source row)" + (
                            f"; emulated share {args.share_index} of {shares} (no gather)" if emulated else ""),
                        "chunk_blocks": max(sizes) if sizes else 0, "rounds": len(sizes), "chunk_schedule": sizes,
@@ -732,7 +772,7 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
             "gather_bytes_per_gpu_per_step": gathered,
             "relax_rounds_per_step": round(it_total / max(1, steps), 1),
             "rank0_step_s": [round(x, 4) for x in step_s],
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "pmc_key": key,
         }
         if gather:
             line["split"] = {"shared_fraction": round(frac, 4), "shared_blocks": min(S, nblk), "local_blocks": l1 - l0,
@@ -747,6 +787,43 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
     return None
 
 
+def default_vs_exact(config: str, parts: int = 0):
+    """Entry-by-entry differences between the default build (derived / shared-anchor
+    rows) and the exact build (spe_table_compare on the device): route mismatches
+    (must be 0), latency / reliability bit differences, the largest relative
+    difference, and ceil(latency * 1e6) flips -- Shadow's packet delay in ns
+    (shd-worker.c:244).  C4 in quarters of the source blocks (two 55-GB tables at
+    a time)."""
+    from shadow_amd import spe
+    top, att, desc = workload(config)
+    g = spe.Graph(top)
+    order = g.order_sources(att)
+    nblk = (len(order) + 63) // 64
+    parts = parts or (4 if config == "c4" else 1)
+    cuts = np.linspace(0, nblk, parts + 1).astype(int)
+    tot = {}
+    t0 = time.perf_counter()
+    for b0, b1 in zip(cuts[:-1], cuts[1:]):
+        d = spe.PathTable(g, order, blocks=(int(b0), int(b1)), exact_sources=False)
+        d.build()
+        x = spe.PathTable(g, order, blocks=(int(b0), int(b1)), exact_sources=True)
+        x.build()
+        r = d.compare(x, 1e-9)
+        d.close()
+        x.close()
+        for k, v in r.items():
+            if k.startswith("max_"):
+                tot[k] = max(tot.get(k, 0.0), v)
+            elif not k.startswith("first_"):
+                tot[k] = tot.get(k, 0) + v
+    tot["tolerance"] = 1e-9
+    tot["parts"] = parts
+    tot["seconds"] = round(time.perf_counter() - t0, 1)
+    tot["note"] = ("default build vs exact_sources=1 on every entry (spe_table_compare): routes must match; "
+                   "delivery_flips = pairs whose ceil(latency * 1e6) ns packet delay differs (shd-worker.c:244)")
+    return tot
+
+
 # The default run (C3 at N = 1) also measures BASELINE's other configurations
 # (and C2 on the FW engine),
 # each in a child process of its own once the C3 table is freed (C4's table alone
@@ -757,6 +834,10 @@ SIDE_CONFIGS = (
     ("c5", ["--config", "c5", "--steps", "10", "--warmup", "2", "--cpu-seconds", "6"]),
     ("c2", ["--config", "c2", "--cpu-seconds", "6", "--cpu-sources", "0"]),
     ("c4", ["--config", "c4", "--steps", "2", "--cpu-seconds", "6"]),   # 1,000-source 1-core CPU sample (~50 s)
+    # the tables topology_seal builds for these graphs (non-dyadic latencies: one lane per
+    # source, bit-exact), with their entry-by-entry differences from the default build
+    ("c3_exact", ["--config", "c3", "--exact", "--steps", "3", "--no-cpu-baseline"]),
+    ("c4_exact", ["--config", "c4", "--exact", "--steps", "2", "--no-cpu-baseline"]),
     ("c1", ["--config", "c1", "--cpu-seconds", "4", "--cpu-sources", "0"]),
     ("c2fw", ["--config", "c2fw", "--steps", "1"]),   # the FW engine's whole C2 table
     ("c5_on_c4", ["--config", "c5", "--c5-table", "c4", "--steps", "10", "--warmup", "2", "--cpu-seconds", "6"]),
@@ -962,6 +1043,9 @@ def main():
     ap.add_argument("--no-north-star", action="store_true",
                     help="N > 1: skip the C4 line measured after the C3 line in the same ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exact", action="store_true",
+                    help="build with spe_table_opts.exact_sources = 1 (the drop-in's table on non-dyadic latencies) "
+                         "and report its differences from the default build (spe_table_compare)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the all-gather (build only)")
     ap.add_argument("--queries", type=int, default=100_000_000, help="c5: lookups per step")
@@ -1041,6 +1125,10 @@ def main():
                 c4 = bench_table(args, rank, world, local, dist, config="c4")
                 if line is not None:
                     line["side_configs"] = {"c4": c4}
+        if line is not None and args.exact and world == 1 and args.config in ("c3", "c4"):
+            gc.collect()
+            torch.cuda.empty_cache()
+            line["vs_default_build"] = default_vs_exact(args.config)
         if line is not None:
             if world == 1 and args.config == "c3" and not args.no_side and args.shares == 1:
                 gc.collect()

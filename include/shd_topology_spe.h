@@ -85,7 +85,9 @@ int32_t SHD_TOPO(topology_getPathInfo)(Topology* top, spe_in_addr_t srcAddress, 
  * batch of n >= 256 (n >= 4096 when the whole table is mirrored on the host) go to
  * ONE device lookup launch (spe_lookup_batch_host), smaller ones to the host
  * mirror / single reads.  Returns the number of
- * routable pairs, -1 on bad arguments. */
+ * routable pairs; -1 on bad arguments, or when no table covering the queried
+ * hosts could be sealed (device or memory failure) -- then every output is
+ * filled as unroutable (latency = reliability = -1, routable = 0). */
 int64_t SHD_TOPO(topology_getPathInfoBatch)(Topology* top, int64_t n, const spe_in_addr_t* srcAddress,
                                   const spe_in_addr_t* dstAddress, double* latency, double* reliability,
                                   uint8_t* routable);

@@ -109,8 +109,13 @@ typedef struct spe_graph_info {
                                      * vertices (one neighbour) are one edge off their anchor
                                      * and need no relaxation state */
     int32_t sums_exact;             /* every latency is k / 2^q with every path sum below 2^53:
-                                     * every f64 path sum is exact, so shared / derived rows
-                                     * (spe_table_opts.exact_sources = 0) are bit-exact too */
+                                     * every f64 path sum is exact, so the LATENCIES of shared /
+                                     * derived rows (spe_table_opts.exact_sources = 0) are the
+                                     * path-order sums bit for bit (and no margin check is needed) */
+    int32_t shared_rows_exact;      /* sums_exact and every edge factor 1 - p is 1.0: shared / derived
+                                     * rows' reliabilities (a(s, c) r_c(t) instead of the path-order
+                                     * product from the source, shd-topology.c:1415-1484) are exact
+                                     * too, so the default build equals exact_sources = 1 bit for bit */
 } spe_graph_info;
 
 typedef struct spe_table_opts {
@@ -421,6 +426,32 @@ typedef struct spe_check_report {
     int32_t first_bad_t;
 } spe_check_report;
 int spe_table_check(const spe_table* t, spe_check_report* out);
+/* Entry-by-entry comparison of two built single-device tables over the same
+ * attached slots, owned block range and device (e.g. the library default --
+ * shared / derived rows -- against exact_sources = 1, which is what the topology
+ * shim seals on non-dyadic latencies), on the device, every (s, t) entry:
+ *   route_mismatch      routability, next hop or hop count differ (must be 0:
+ *                       routes are exact in every mode);
+ *   latency_differs / reliability_differs   bit differences of routable entries;
+ *   beyond_tolerance    |a - b| > rel_tol |b| in latency or reliability;
+ *   delivery_flips      ceil(latency * 1e6) differs: the packet delay in ns
+ *                       Shadow's worker derives from getLatency (shd-worker.c:244,
+ *                       SIMTIME_ONE_MILLISECOND = 1e6), i.e. simulated behaviour. */
+typedef struct spe_compare_report {
+    uint32_t struct_size;           /* sizeof(spe_compare_report) as the caller compiled it */
+    int64_t pairs;
+    int64_t routable;               /* routable in table b */
+    int64_t route_mismatch;
+    int64_t latency_differs;
+    int64_t reliability_differs;
+    int64_t beyond_tolerance;
+    int64_t delivery_flips;
+    double max_latency_rel_err;
+    double max_reliability_rel_err;
+    int32_t first_bad_s;            /* first route mismatch or out-of-tolerance pair (slots), -1 none */
+    int32_t first_bad_t;
+} spe_compare_report;
+int spe_table_compare(const spe_table* a, const spe_table* b, double rel_tol, spe_compare_report* out);
 /* Minimum latency over every owned routable entry (minimumPathLatency). */
 /* On-disk path-table cache (the reference recomputes its paths
  * every run).  The key hashes everything that determines the rows: the graph

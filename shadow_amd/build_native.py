@@ -3,6 +3,7 @@ the C demo in-tree with hipcc / gcc.  Used by __graft_entry__.build(); the
 CMake build (CMakeLists.txt) produces the same artefacts for a Shadow build."""
 from __future__ import annotations
 
+import glob
 import os
 import subprocess
 import sys
@@ -35,6 +36,8 @@ def _stale(out, srcs):
 def build_spe(force: bool = False) -> str:
     srcs = [os.path.join(CSRC, f) for f in ("spe.hip", "spe_graph_prep.cpp", "spe_multi.cpp", "spe_internal.h")]
     srcs.append(os.path.join(ROOT, "include", "spe.h"))
+    # spe.hip #includes its kernels and host code from csrc/spe/*.inc
+    srcs += sorted(glob.glob(os.path.join(CSRC, "spe", "*.inc")))
     if force or _stale(LIB_SPE, srcs):
         _run([HIPCC, *HIP_FLAGS, "-shared", "-o", LIB_SPE,
               os.path.join(CSRC, "spe.hip"), os.path.join(CSRC, "spe_graph_prep.cpp"),
@@ -63,10 +66,23 @@ def build_demo(force: bool = False) -> str:
     return DEMO
 
 
+LEXREPRO_SRC = os.path.join(ROOT, "tests", "native", "lexrepro.hip")
+LEXREPRO = os.path.join(ROOT, "tests", "native", "liblexrepro.so")
+
+
+def build_lexrepro(force: bool = False) -> str:
+    """Test-only: the gfx950 compare reproducer tests/test_gpu_lexrepro.py runs
+    (not part of the product; built beforehand so no GPU run compiles)."""
+    if force or _stale(LEXREPRO, [LEXREPRO_SRC]):
+        _run([HIPCC, *HIP_FLAGS, "-shared", "-o", LEXREPRO, LEXREPRO_SRC])
+    return LEXREPRO
+
+
 def build_all(force: bool = False) -> None:
     build_spe(force)
     build_topo(force)
     build_demo(force)
+    build_lexrepro(force)
 
 
 if __name__ == "__main__":

@@ -429,6 +429,14 @@ void share_prep(HostGraph* hg) {
         wmax = std::max(wmax, w);
     }
     sh.eligible = true;
+    // a shared / derived row multiplies a(s, c) * r_c(t) where the reference folds
+    // ((1 a(s, c)) a_1) a_2 ... from the source (shd-topology.c:1415-1484): the same
+    // bits only when every factor is 1 (no edge loss anywhere)
+    sh.prod_exact = true;
+    for (double a : hg->ia) sh.prod_exact = sh.prod_exact && a == 1.0;
+    for (double a : hg->fia) sh.prod_exact = sh.prod_exact && a == 1.0;
+    if (hg->cx.active)
+        for (double a : hg->cx.a2) sh.prod_exact = sh.prod_exact && a == 1.0;
     sh.wmin = std::isfinite(wmin) ? wmin : 0.0;
     sh.omax = omax;
     for (int q = 0; q <= 20 && !sh.exact; ++q) {

@@ -86,6 +86,7 @@ struct HostGraph {
     struct Share {
         bool eligible = false;     // undirected, pruned, no vertex factor other than 1 / absent
         bool exact = false;        // every weight k / 2^q and every path sum below 2^53: fl sums exact
+        bool prod_exact = false;   // every edge factor 1 - p is 1.0: every reliability product exact
         double wmin = 0.0;         // smallest relaxation weight (bounds a path's edge count)
         double omax = 0.0;         // largest pendant-edge weight (a source's offset)
     } share;

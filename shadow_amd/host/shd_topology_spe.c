@@ -115,7 +115,7 @@ struct _Topology {
     int32_t directed;
     int32_t prefer_direct;
     int32_t complete;
-    int32_t sums_exact;            /* spe_graph_info.sums_exact: shared rows are bit-exact too */
+    int32_t shared_rows_exact;     /* spe_graph_info.shared_rows_exact: shared / derived rows are bit-exact */
     /* graph, edge list form (GraphML order) */
     int32_t *esrc, *edst;
     double *elat, *eloss;
@@ -744,7 +744,7 @@ Topology* topology_new_on_device(const char* graphPath, int32_t device) {
     spe_graph_info info = SPE_STRUCT_INIT(spe_graph_info);
     spe_graph_info_get(top->graph, &info);
     top->complete = info.complete;
-    top->sums_exact = info.sums_exact;
+    top->shared_rows_exact = info.shared_rows_exact;
     if (!info.weight_floor_ok)   /* outside the bit-exactness argument */
         tlog(top, LOG_WARNING, "some edge latency is below ulp(path latency)/2: a relaxation could leave a "
                                "distance unchanged (fl(d + w) == d); routes are exact only when every "
@@ -1137,11 +1137,14 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
      * one: 5.0 .. 2293.85 ms), whose products sit on or next to an integer: the few
      * ulps by which a shared / derived row differs from the path-order sum
      *  would move a delivery by 1 ns.  So the drop-in's default is
-     * bit-exact: shared anchor trees and derived rows only where sums are exact
-     * (spe_graph_info.sums_exact; e.g. integer latencies), where they are bit-exact
-     * as well.  SHADOW_SPE_EXACT_SOURCES=0 / 1 overrides it either way. */
+     * bit-exact: shared anchor trees and derived rows only where every path sum AND
+     * every reliability product is exact (spe_graph_info.shared_rows_exact: latencies
+     * k / 2^q, e.g. integers, and no edge loss -- a shared row multiplies
+     * a(s, c) * r_c(t) where the reference folds from the source), where
+     * they equal the exact build bit for bit.  SHADOW_SPE_EXACT_SOURCES=0 / 1
+     * overrides it either way. */
     const char* ex = getenv("SHADOW_SPE_EXACT_SOURCES");
-    o.exact_sources = top->sums_exact ? 0 : 1;
+    o.exact_sources = top->shared_rows_exact ? 0 : 1;
     if (ex && *ex) o.exact_sources = strcmp(ex, "0") != 0;
     int rc = spe_table_create(top->graph, s->attached, A, &o, &s->table);
     if (rc == SPE_EUNSUPPORTED && o.engine != SPE_ENGINE_AUTO) {
@@ -1898,7 +1901,14 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
     const double t0 = timing ? now_s() : 0.0;
     BatchRes r;
     Snap* sn = batch_prepare(top, n, srcAddress, dstAddress, &r);
-    if (!sn) return -1;
+    if (!sn) {   /* no table could be sealed (or scratch failed): every query unanswered */
+        for (int64_t i = 0; i < n; ++i) {
+            latency[i] = -1.0;
+            reliability[i] = -1.0;
+            routable[i] = 0;
+        }
+        return -1;
+    }
     const double t1 = timing ? now_s() : 0.0;
     int min_updated = 0;
     batch_phase2(top, sn, n, srcAddress, dstAddress, &r, &min_updated);

@@ -64,7 +64,8 @@ class GraphInfo(_Sized):
     _fields_ = [("struct_size", C.c_uint32), ("n_vertices", C.c_int32), ("n_edges", C.c_int64), ("n_relax_entries", C.c_int64),
                 ("directed", C.c_int32), ("prefer_direct", C.c_int32), ("complete", C.c_int32),
                 ("parallel_latency_differs", C.c_int32), ("weight_floor_ok", C.c_int32), ("device", C.c_int32),
-                ("n_relax_vertices", C.c_int32), ("sums_exact", C.c_int32)]
+                ("n_relax_vertices", C.c_int32), ("sums_exact", C.c_int32),
+                ("shared_rows_exact", C.c_int32)]
 
 
 class TableOpts(_Sized):
@@ -104,6 +105,14 @@ class CheckReport(C.Structure):
                 ("first_bad_s", C.c_int32), ("first_bad_t", C.c_int32)]
 
 
+class CompareReport(_Sized):
+    _fields_ = [("struct_size", C.c_uint32), ("pairs", C.c_int64), ("routable", C.c_int64),
+                ("route_mismatch", C.c_int64), ("latency_differs", C.c_int64), ("reliability_differs", C.c_int64),
+                ("beyond_tolerance", C.c_int64), ("delivery_flips", C.c_int64),
+                ("max_latency_rel_err", C.c_double), ("max_reliability_rel_err", C.c_double),
+                ("first_bad_s", C.c_int32), ("first_bad_t", C.c_int32)]
+
+
 class KernelProfile(C.Structure):
     _fields_ = [("ms", C.c_double * 8), ("launches", C.c_int64 * 8)]
 
@@ -127,7 +136,7 @@ EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_
            "spe_graph_set_edge_aux", "spe_table_download_aux", "spe_fw_apsp", "spe_fw_closure", "spe_graph_self_path",
            "spe_graph_adjacent", "spe_device_shares", "spe_graph_edge", "spe_table_source_tree",
            "spe_device_split", "spe_lookup_batch_replica", "spe_table_replica_device", "spe_table_check",
-           "spe_lookup_batch_host"]
+           "spe_lookup_batch_host", "spe_table_compare"]
 
 _lib = None
 
@@ -169,6 +178,7 @@ def lib():
         L.spe_table_replica_device.argtypes = [P, C.c_int32, P]
         L.spe_lookup_batch_host.argtypes = [P, P, C.c_int64, P, P, P]
         L.spe_table_check.argtypes = [P, P]
+        L.spe_table_compare.argtypes = [P, P, C.c_double, P]
         L.spe_device_split.argtypes = [C.c_int32, C.c_int32, C.c_double, P, P, P]
         L.spe_table_min_latency.argtypes = [P, P]
         L.spe_table_key.argtypes = [P, P]
@@ -446,6 +456,14 @@ class PathTable:
         r = CheckReport()
         _check(lib().spe_table_check(self.h, C.byref(r)), "spe_table_check")
         return {f: getattr(r, f) for f, _ in CheckReport._fields_}
+
+    def compare(self, other: "PathTable", rel_tol: float = 1e-12) -> dict:
+        """spe_table_compare(self, other): entry-by-entry differences on the device
+        (route mismatches, latency / reliability bit differences, entries beyond
+        rel_tol relative to `other`, ceil(latency * 1e6) delivery-time flips)."""
+        r = CompareReport()
+        _check(lib().spe_table_compare(self.h, other.h, float(rel_tol), C.byref(r)), "spe_table_compare")
+        return {f: getattr(r, f) for f, _ in CompareReport._fields_ if f != "struct_size"}
 
     def replica_device(self, replica: int) -> int:
         d = C.c_int32(0)

@@ -134,6 +134,8 @@ class Topology:
         import numpy as np
         s = np.ascontiguousarray(src, np.uint32)
         d = np.ascontiguousarray(dst, np.uint32)
+        if s.ndim != 1 or s.shape != d.shape:
+            raise ValueError("path_info_batch: src and dst must be 1-D arrays of equal length")
         n = int(s.shape[0])
         lat = np.empty(n, np.float64)
         rel = np.empty(n, np.float64)
@@ -148,6 +150,8 @@ class Topology:
         import numpy as np
         s = np.ascontiguousarray(src, np.uint32)
         d = np.ascontiguousarray(dst, np.uint32)
+        if s.ndim != 1 or s.shape != d.shape:
+            raise ValueError("count_packets_batch: src and dst must be 1-D arrays of equal length")
         lib().topology_incrementPathPacketCounterBatch(self.h, int(s.shape[0]), s.ctypes.data, d.ctypes.data)
 
     def count_packet(self, a: int, b: int):

@@ -50,7 +50,8 @@ def test_struct_layouts_match_the_header(tmp_path):
     from shadow_amd import spe
     structs = {"spe_graph_desc": spe.GraphDesc, "spe_graph_info": spe.GraphInfo, "spe_table_opts": spe.TableOpts,
                "spe_table_layout": spe.TableLayout, "spe_build_stats": spe.BuildStats, "spe_entry": spe.Entry,
-               "spe_check_report": spe.CheckReport, "spe_kernel_profile": spe.KernelProfile}
+               "spe_check_report": spe.CheckReport, "spe_compare_report": spe.CompareReport,
+               "spe_kernel_profile": spe.KernelProfile}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "spe.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')

@@ -1,0 +1,91 @@
+"""Guard for the gfx950 code-generation fault behind round 4's wrong tie-breaks at
+hubs: a running lexicographic best (alt, d[u], u) over candidates
+whose vertex u is wave-uniform.  The short-circuit compare
+`alt < ba || (alt == ba && (du < bdu || (du == bdu && u < bu)))` followed by four
+assignments compiled (ROCm 7.2) to code whose tie-winning lanes took the new
+distances but kept the old parent entry.  libspe writes every such compare
+branch-free (lex_less3 / lex_less2, kernels_relax.inc:211-223).
+
+* test_branch_free_compare_on_the_gpu: the select form (form 1) of the reproducer
+  (tests/native/lexrepro.hip, the heavy partial's shape) matches a numpy argmin on
+  tie-heavy inputs, lane for lane;
+* the short-circuit form (form 0) is run on the same inputs and its result is
+  reported (`pytest -s` prints how many lanes kept a stale entry): it documents the
+  failing form without making the suite depend on the compiler's choice;
+* test_no_short_circuit_lexicographic_compares (CPU, tests/test_lint_kernels.py)
+  keeps the form out of the kernels."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.engine_fixed]
+
+LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "liblexrepro.so")
+
+
+def run(form, pack, D, cnt, nitems):
+    from shadow_amd import spe
+    assert spe.device_count() > 0, "no GPU visible"
+    lib = C.CDLL(LIB)
+    lib.lexrepro_run.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                                 C.c_void_p]
+    ne = nitems * 64
+    a = np.empty(ne, np.float64)
+    d = np.empty(ne, np.float64)
+    uk = np.empty((ne, 2), np.int32)
+    rc = lib.lexrepro_run(form, pack.ctypes.data, D.ctypes.data, cnt, nitems, a.ctypes.data, d.ctypes.data,
+                          uk.ctypes.data)
+    assert rc == 0, f"lexrepro_run: HIP error {rc}"
+    return a, d, uk
+
+
+def case(nitems=512, cnt=64, seed=3):
+    """Tie-heavy candidates: integer distances 0..3 and integer weights 1..2, so
+    (alt, d[u]) tie often and only u separates them; u is a permutation of the
+    in-list per item (wave-uniform per candidate)."""
+    rng = np.random.default_rng(seed)
+    u = np.stack([rng.permutation(64) for _ in range(nitems)]).astype(np.int32)      # [item][k]
+    w = rng.integers(1, 3, (nitems, 64)).astype(np.float64)
+    wb = w.view(np.int64)
+    pack = np.zeros((nitems, 64, 4), np.int32)
+    pack[:, :, 0] = u
+    pack[:, :, 2] = (wb & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
+    pack[:, :, 3] = (wb >> 32).astype(np.int32)
+    D = rng.integers(0, 4, (nitems, 64, 64)).astype(np.float64)   # [item][vertex][lane]
+    D[rng.random(D.shape) < 0.05] = np.inf
+    # expected: per (item, lane) the lexicographic argmin over k < cnt of (du + w, du, u)
+    du = np.take_along_axis(D, u[:, :cnt, None].repeat(64, axis=2), axis=1)        # [item][k][lane]
+    alt = du + w[:, :cnt, None]
+    key_u = np.broadcast_to(u[:, :cnt, None], du.shape)
+    first = np.lexsort((key_u, du, alt), axis=1)[:, 0, :]                          # [item][lane]
+    exp_k = np.where(np.isfinite(np.take_along_axis(du, first[:, None, :], axis=1)[:, 0, :]), first, -1)
+    return pack.reshape(-1), np.ascontiguousarray(D.reshape(-1)), exp_k, u, cnt, nitems
+
+
+@pytest.fixture(scope="module")
+def inputs():
+    return case()
+
+
+def test_branch_free_compare_on_the_gpu(inputs):
+    pack, D, exp_k, u, cnt, nitems = inputs
+    a, d, uk = run(1, pack, D, cnt, nitems)
+    k = uk[:, 1].reshape(nitems, 64)
+    bu = uk[:, 0].reshape(nitems, 64)
+    assert (k == exp_k).all(), f"select form: {(k != exp_k).sum()} lanes with the wrong argmin"
+    ok = exp_k >= 0
+    assert (bu[ok] == np.take_along_axis(u, np.maximum(exp_k, 0), axis=1)[ok]).all()
+
+
+def test_short_circuit_form_documented(inputs):
+    """Runs the failing form on the same inputs and reports it; the test asserts
+    only that the kernel ran (the fault depends on the compiler's code layout)."""
+    pack, D, exp_k, u, cnt, nitems = inputs
+    a, d, uk = run(0, pack, D, cnt, nitems)
+    k = uk[:, 1].reshape(nitems, 64)
+    bad = int((k != exp_k).sum())
+    # a stale entry: the distance fields of the winner, the parent entry of an earlier candidate
+    print(f"short-circuit form: {bad} of {k.size} lanes disagree with the lexicographic argmin "
+          f"({'reproduces' if bad else 'does not reproduce'} the round-4 fault in this shape)")

@@ -136,6 +136,49 @@ def test_shim_default_is_bit_exact_on_decimal_latencies(tmp_path, monkeypatch):
     assert g.info()["sums_exact"] == 0
 
 
+@pytest.mark.shared_trees   # the shim's own default
+@pytest.mark.parametrize("loss", ["lossy", "lossless"])
+def test_shim_default_is_bit_exact_on_integer_latencies(tmp_path, loss):
+    """Integer latencies make every path SUM exact (spe_graph_info.sums_exact), but
+    a shared / derived row multiplies a(s, c) * r_c(t) where the reference folds the
+    reliability from the source (shd-topology.c:1415-1484): with any edge loss the
+    products group differently.  The shim therefore shares rows only
+    when shared_rows_exact (sums exact AND no edge loss); either way its answers equal
+    the oracle bit for bit, reliability included."""
+    from oracle import Oracle
+    from shadow_amd import spe
+    t = graphs.gen_tiered(n_core=400, n_stub=1600, n_attached=900, seed=21)
+    rng = np.random.default_rng(21)
+    loop = t.esrc == t.edst
+    t.elat = np.where(loop, 1.0, rng.integers(1, 200, t.elat.shape[0]).astype(np.float64))
+    t.eloss = rng.uniform(0.0, 0.01, t.m) if loss == "lossy" else np.zeros(t.m)
+    t.vloss = np.zeros(t.n)
+    info = spe.Graph(t).info()
+    assert info["sums_exact"] == 1 and info["shared_rows_exact"] == (loss == "lossless"), info
+    ips = [f"10.{v // 250}.{v % 250}.{1 + v % 7}" for v in range(t.n)]
+    verts = graphs.tiered_attached(t, n_core=400, n_attached=900)[:600]
+    top = _topology(tmp_path, t, ips)
+    addrs = _attach(top, ips, verts)
+    k = len(verts)
+    ok, lat, rel = top.path_info_batch(np.repeat(addrs, k), np.tile(addrs, k))
+    ref = Oracle(t).rows(verts, verts, tie_mode=1)   # integer latencies tie: the canonical parent rule
+    okr = ref["kind"] != 0
+    np.testing.assert_array_equal(ok.reshape(k, k), okr.astype(np.uint8))
+    np.testing.assert_array_equal(lat.reshape(k, k)[okr], ref["lat"][okr])
+    np.testing.assert_array_equal(rel.reshape(k, k)[okr], ref["rel"][okr])
+    top.close()
+    if loss == "lossy":   # what the library default would change: reliability by a few ulps
+        g = spe.Graph(t)
+        sh = spe.PathTable(g, verts, engine=spe.SPE_ENGINE_BATCH, exact_sources=False)
+        sh.build()
+        assert sh.layout()["shared_sources"] == 1
+        d = sh.download()
+        np.testing.assert_array_equal(d["lat"][okr], ref["lat"][okr])
+        np.testing.assert_allclose(d["rel"][okr], ref["rel"][okr], rtol=1e-12)
+        print(f"default build on integer latencies with loss: {int((d['rel'][okr] != ref['rel'][okr]).sum())} "
+              f"reliabilities differ in the last bits")
+
+
 @pytest.mark.parametrize("threads", ["1", "8"])
 def test_threaded_batch_equals_single_calls_in_order(tmp_path, monkeypatch, threads):
     """A batch large enough for the threaded path (>= 64k queries): phase 1 looks

@@ -12,6 +12,17 @@ import os
 import sys
 
 root, out = sys.argv[1], sys.argv[2]
+# optional: the bench log of the PMC pass -- its JSON line's pmc_key (config, N,
+# groups per launch, build mode) is recorded, and bench.py attaches the summary
+# as roofline.traffic only to a run with the same key
+key = None
+if len(sys.argv) > 3:
+    for line in open(sys.argv[3]):
+        if line.startswith("{"):
+            try:
+                key = json.loads(line).get("pmc_key", key)
+            except ValueError:
+                pass
 acc = collections.defaultdict(lambda: {"fetch_kb": 0.0, "write_kb": 0.0, "dispatches": set()})
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
@@ -31,5 +42,5 @@ for k, v in acc.items():
               "write_bytes_per_dispatch": v["write_kb"] * 1024 / nd}
     res[k]["hbm_bytes_per_dispatch"] = res[k]["fetch_bytes_per_dispatch"] + res[k]["write_bytes_per_dispatch"]
 json.dump({"note": "FETCH_SIZE x2 (gfx950 correction, calibrated on k_rows_sssp); WRITE_SIZE x1",
-           "kernels": res}, open(out, "w"), indent=1)
+           "pmc_key": key, "kernels": res}, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
