@@ -366,20 +366,88 @@ void contract_degree3(HostGraph* hg) {
         }
         cx.ptr.push_back((int32_t)cx.col.size());
     }
-    // derivable sources: the removed vertices, then (greedy, core order) kept vertices
-    // of in-degree 4 with no removed or derivable neighbour and no pendant
+    // Derivable sources: the removed vertices, then a greedy independent
+    // set, in the contracted graph, of kept vertices x with at most DER_LEGS_KEPT
+    // contracted entries, at most one removed neighbour and no pendant, fewest removed
+    // neighbours and entries first.  x's legs are its contracted entries read as
+    // paths FROM x (x -> u, or x -> y -> b through a removed neighbour y) plus the
+    // direct edge to y as a one-target leg; a removed neighbour y of x then reaches
+    // x's other neighbours through x (x has no lane): its legs are its two other
+    // neighbours, each plain neighbour k of x as x's prefix y -> x -> k, and x itself
+    // as a one-target leg.  Rows read only lanes (no derived source reads another).
+    constexpr int32_t DER_LEGS_KEPT = 7;
     cx.der.assign(nc, 0);
     for (int32_t x : cx.rcore) cx.der[x] = 1;
+    auto nrem = [&](int32_t x) {
+        int32_t r = 0;
+        for (int32_t k = hg->iptr[x]; k < hg->iptr[x + 1]; ++k) r += cx.rid[hg->icol[k]] >= 0;
+        return r;
+    };
+    std::vector<int32_t> cand;
     for (int32_t x = 0; x < nc; ++x) {
-        if (cx.rid[x] >= 0 || pendants[x] || hg->iptr[x + 1] - hg->iptr[x] != 4) continue;
-        bool ok = true;
-        for (int32_t k = hg->iptr[x]; k < hg->iptr[x + 1]; ++k) {
-            const int32_t u = hg->icol[k];
-            ok &= u != x && cx.rid[u] < 0 && !cx.der[u];
-        }
-        if (!ok) continue;
+        if (cx.rid[x] >= 0 || pendants[x]) continue;
+        const int32_t kv = cx.kid[x];
+        const int32_t cdeg = cx.ptr[kv + 1] - cx.ptr[kv];
+        bool loop = false;
+        for (int32_t k = hg->iptr[x]; k < hg->iptr[x + 1]; ++k) loop |= hg->icol[k] == x;
+        if (!loop && cdeg <= DER_LEGS_KEPT && nrem(x) <= 1) cand.push_back(x);
+    }
+    std::stable_sort(cand.begin(), cand.end(), [&](int32_t p, int32_t q) {
+        const int32_t rp = nrem(p), rq = nrem(q);
+        if (rp != rq) return rp < rq;
+        return cx.ptr[cx.kid[p] + 1] - cx.ptr[cx.kid[p]] < cx.ptr[cx.kid[q] + 1] - cx.ptr[cx.kid[q]];
+    });
+    std::vector<uint8_t> near((size_t)nc, 0);   // contracted-adjacent to a derived kept vertex
+    for (int32_t x : cand) {
+        if (near[x]) continue;
+        const int32_t kv = cx.kid[x];
         cx.der[x] = 1;
         ++cx.nd4;
+        near[x] = 1;
+        for (int32_t k = cx.ptr[kv]; k < cx.ptr[kv + 1]; ++k) near[cx.kcore[cx.col[k]]] = 1;
+    }
+    // the legs, in core-id space
+    std::vector<int32_t> xnb((size_t)nc, -1);   // removed vertex -> its derived kept neighbour
+    for (int32_t x = 0; x < nc; ++x)
+        if (cx.der[x] && cx.rid[x] < 0)
+            for (int32_t k = hg->iptr[x]; k < hg->iptr[x + 1]; ++k)
+                if (cx.rid[hg->icol[k]] >= 0) xnb[hg->icol[k]] = x;
+    cx.dptr.assign((size_t)nc + 1, 0);
+    for (int32_t c = 0; c < nc; ++c) {
+        if (cx.der[c]) {
+            if (cx.rid[c] >= 0) {   // removed
+                const int32_t x = xnb[c];
+                for (int32_t k = hg->iptr[c]; k < hg->iptr[c + 1]; ++k) {
+                    const int32_t u = hg->icol[k];
+                    if (u != x) {
+                        cx.dlegs.push_back({u, 0, hg->corev[u], 1, hg->iw[k], hg->ia[k]});
+                        continue;
+                    }
+                    // through the derived x: x's plain neighbours, and x itself
+                    for (int32_t q = hg->iptr[x]; q < hg->iptr[x + 1]; ++q) {
+                        const int32_t kk = hg->icol[q];
+                        if (cx.rid[kk] >= 0) continue;   // (x's only removed neighbour is c)
+                        cx.dlegs.push_back({kk, 0, hg->corev[x], 2, hg->iw[k] + hg->iw[q], hg->ia[k] * hg->ia[q]});
+                    }
+                    cx.dlegs.push_back({-1, cx.kid[x], hg->corev[x], 1, hg->iw[k], hg->ia[k]});
+                }
+            } else {                // kept
+                for (int32_t k = hg->iptr[c]; k < hg->iptr[c + 1]; ++k) {
+                    const int32_t u = hg->icol[k];
+                    if (cx.rid[u] < 0) {
+                        cx.dlegs.push_back({u, 0, hg->corev[u], 1, hg->iw[k], hg->ia[k]});
+                        continue;
+                    }
+                    for (int32_t q = hg->iptr[u]; q < hg->iptr[u + 1]; ++q) {   // c -> u -> b
+                        const int32_t b = hg->icol[q];
+                        if (b == c) continue;
+                        cx.dlegs.push_back({b, 0, hg->corev[u], 2, hg->iw[k] + hg->iw[q], hg->ia[k] * hg->ia[q]});
+                    }
+                    cx.dlegs.push_back({-1, -2 - cx.rid[u], hg->corev[u], 1, hg->iw[k], hg->ia[k]});
+                }
+            }
+        }
+        cx.dptr[(size_t)c + 1] = (int32_t)cx.dlegs.size();
     }
     // reverse entries: (a -> v via x) <-> (v -> a via x)
     cx.rev.assign(cx.col.size(), -1);
@@ -418,10 +486,11 @@ void share_prep(HostGraph* hg) {
         omax = std::max(omax, w);
         ws.push_back(w);
     }
-    if (hg->cx.active)   // a derived source's offset is the edge to one of its neighbours
-        for (int32_t x = 0; x < hg->nc; ++x)
-            if (hg->cx.der[(size_t)x])
-                for (int32_t k = hg->iptr[(size_t)x]; k < hg->iptr[(size_t)x + 1]; ++k) omax = std::max(omax, hg->iw[(size_t)k]);
+    if (hg->cx.active)   // a derived source's offset is one of its legs' prefixes (one or two edges)
+        for (const HostGraph::Contracted::Leg& l : hg->cx.dlegs) {
+            omax = std::max(omax, l.w);
+            ws.push_back(l.w);
+        }
     double wmin = INFINITY, wmax = 0.0;
     for (double w : hg->iw) wmin = std::min(wmin, w);
     for (double w : ws) {

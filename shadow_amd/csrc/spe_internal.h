@@ -71,12 +71,24 @@ struct HostGraph {
         std::vector<int32_t> key;          // core id of the entry's parent (x for a shortcut, a for a plain edge)
         std::vector<int32_t> via;          // original id of x, -1 for a plain edge
         // Sources whose rows a shared table may derive from their neighbours' lanes
-        // (k_rows_derived): every removed vertex, and an independent set of kept
-        // vertices with exactly four neighbours, none removed, no pendant anchored
-        // (they stay relaxation vertices; only their own lane goes).  The neighbours
-        // are the core in-list (iptr / icol / iw / ia): 3 or 4 entries.
+        // (k_rows_derived): every removed vertex, and an independent set
+        // (in the contracted graph) of kept vertices with at most DER_LEGS_KEPT
+        // contracted entries, at most one removed neighbour and no pendant anchored
+        // (they stay relaxation vertices; only their own lane goes).  Each derived
+        // source's row is the best of its LEGS: a first path prefix (one or two edges)
+        // to a kept vertex whose lane is read, or a direct edge to one target.
+        struct Leg {
+            int32_t ref;                   // core id of the kept vertex whose lane the leg reads, -1: direct
+            int32_t tc;                    // direct: the one target's relaxation code (kept id, or -2 - removed index)
+            int32_t hop;                   // first hop (original id)
+            int32_t inc;                   // edges of the prefix (1 or 2)
+            double w;                      // prefix latency, summed in path order from the source
+            double a;                      // prefix reliability factors, multiplied in path order
+        };
         std::vector<uint8_t> der;          // [nc]
-        int32_t nd4 = 0;
+        std::vector<int32_t> dptr;         // [nc + 1] legs of core vertex c: dlegs[dptr[c] .. dptr[c + 1])
+        std::vector<Leg> dlegs;
+        int32_t nd4 = 0;                   // derived kept vertices
     } cx;
 
     // Shared anchor trees for the batch engine (share_prep): a pruned

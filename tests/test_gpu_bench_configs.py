@@ -112,7 +112,7 @@ def test_c3_bench_build_every_launch(spe):
 @pytest.mark.shared_trees
 def test_c3_derived_rows_full_size(spe):
     """C3 (50k BA) full table with the library default, as bench.py builds it: the
-    20k contracted degree-3 sources and ~2.9k degree-4 ones take no relaxation lane,
+    20k contracted degree-3 sources and ~9k kept ones take no relaxation lane,
     their rows derived from their neighbours' roots.  Routes (routability, next hop,
     hops) equal the oracle's exactly, latency / reliability within 1e-12 relative;
     kept (core) sources bit-exact; 96 sampled rows (half of them derived) plus the
@@ -124,14 +124,14 @@ def test_c3_derived_rows_full_size(spe):
     assert lay["shared_sources"] == 1 and lay["contracted_vertices"] > 0, lay
     st = t.stats()
     assert st["derived_sources"] > 20000, st
-    assert st["relaxed_lanes"] < 30000 + 64 * st["fallback_blocks"], st
+    assert st["relaxed_lanes"] < 25000 + 64 * st["fallback_blocks"], st
     print(f"C3 derived rows: {st['derived_sources']} derived sources, {st['relaxed_lanes']} relaxation lanes, "
           f"{st['fallback_blocks']} fallback blocks")
     nl = top.esrc != top.edst
     deg = np.bincount(np.concatenate([top.esrc[nl], top.edst[nl]]), minlength=top.n)
     rng = np.random.default_rng(33)
-    d3 = np.flatnonzero(deg[order] <= 4)   # derivable: every degree-3 source, some degree-4 ones
-    kept = np.flatnonzero(deg[order] > 4)
+    d3 = np.flatnonzero(deg[order] <= 6)   # derivable: every degree-3 source, some kept ones up to degree 6
+    kept = np.flatnonzero(deg[order] > 7)
     slots = np.unique(np.r_[rng.choice(d3, 48, replace=False), rng.choice(kept, 48, replace=False)])
     check_sampled_rows(t, top, order, slots, "C3 derived", rtol=1e-12)
     ora = Oracle(top).rows(order[kept[:8]], order, nthreads=ORACLE_THREADS)
