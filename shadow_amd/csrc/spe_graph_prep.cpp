@@ -295,7 +295,7 @@ void contract_degree3(HostGraph* hg) {
     for (double f : hg->vfac)
         if (has_attr(f) && f != 1.0) return;   // the rows' path-order re-fold walks plain entries only
     const int32_t nc = hg->nc;
-    if (nc < 8) return;
+    if (nc < 8 || hg->n >= (1 << 29)) return;   // (a leg packs its first hop's id into 29 bits)
     std::vector<int32_t> pendants(nc, 0);
     for (int32_t v = 0; v < hg->n; ++v)
         if (hg->anchor_core[v] >= 0) pendants[hg->anchor_core[v]]++;
