@@ -375,7 +375,16 @@ void contract_degree3(HostGraph* hg) {
     // x's other neighbours through x (x has no lane): its legs are its two other
     // neighbours, each plain neighbour k of x as x's prefix y -> x -> k, and x itself
     // as a one-target leg.  Rows read only lanes (no derived source reads another).
-    constexpr int32_t DER_LEGS_KEPT = 7;
+#ifndef SPE_DER_KEPT_MAX
+#define SPE_DER_KEPT_MAX 7      // contracted entries of a derived kept vertex
+#endif
+#ifndef SPE_DER_MAXDEP
+#define SPE_DER_MAXDEP 1        // removed neighbours it may have (0 or 1)
+#endif
+#ifndef SPE_DER_DEP_PLAIN
+#define SPE_DER_DEP_PLAIN 99    // with a removed neighbour: at most this many kept neighbours
+#endif
+    constexpr int32_t DER_LEGS_KEPT = SPE_DER_KEPT_MAX;
     cx.der.assign(nc, 0);
     for (int32_t x : cx.rcore) cx.der[x] = 1;
     auto nrem = [&](int32_t x) {
@@ -390,7 +399,10 @@ void contract_degree3(HostGraph* hg) {
         const int32_t cdeg = cx.ptr[kv + 1] - cx.ptr[kv];
         bool loop = false;
         for (int32_t k = hg->iptr[x]; k < hg->iptr[x + 1]; ++k) loop |= hg->icol[k] == x;
-        if (!loop && cdeg <= DER_LEGS_KEPT && nrem(x) <= 1) cand.push_back(x);
+        const int32_t r = nrem(x);
+        const int32_t plain = hg->iptr[x + 1] - hg->iptr[x] - r;
+        if (!loop && cdeg <= DER_LEGS_KEPT && r <= SPE_DER_MAXDEP && (r == 0 || plain <= SPE_DER_DEP_PLAIN))
+            cand.push_back(x);
     }
     std::stable_sort(cand.begin(), cand.end(), [&](int32_t p, int32_t q) {
         const int32_t rp = nrem(p), rq = nrem(q);
