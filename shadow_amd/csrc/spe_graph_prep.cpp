@@ -376,13 +376,13 @@ void contract_degree3(HostGraph* hg) {
     // neighbours, each plain neighbour k of x as x's prefix y -> x -> k, and x itself
     // as a one-target leg.  Rows read only lanes (no derived source reads another).
 #ifndef SPE_DER_KEPT_MAX
-#define SPE_DER_KEPT_MAX 7      // contracted entries of a derived kept vertex
+#define SPE_DER_KEPT_MAX 5      // contracted entries of a derived kept vertex
 #endif
 #ifndef SPE_DER_MAXDEP
 #define SPE_DER_MAXDEP 1        // removed neighbours it may have (0 or 1)
 #endif
 #ifndef SPE_DER_DEP_PLAIN
-#define SPE_DER_DEP_PLAIN 99    // with a removed neighbour: at most this many kept neighbours
+#define SPE_DER_DEP_PLAIN 3     // with a removed neighbour: at most this many kept neighbours
 #endif
     constexpr int32_t DER_LEGS_KEPT = SPE_DER_KEPT_MAX;
     cx.der.assign(nc, 0);
