@@ -345,6 +345,9 @@ int spe_table_build_stats(const spe_table* t, spe_build_stats* out);
 int spe_table_layout_get(const spe_table* t, spe_table_layout* out);
 /* One entry, read back from HBM (synchronous). */
 int spe_table_get(const spe_table* t, int32_t s_slot, int32_t t_slot, spe_entry* out);
+/* Only the {latency, reliability} record of one entry (one 16-B read back): what
+ * topology_getLatency / getReliability need (shd-topology.c:2036-2061). */
+int spe_table_get_latrel(const spe_table* t, int32_t s_slot, int32_t t_slot, double* latency, double* reliability);
 /* Copy owned rows [row_begin,row_end) x [0,n_attached) to host, row-major;
  * any output pointer may be NULL. */
 int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, double* latency,

@@ -50,6 +50,7 @@
 #include <queue>
 #include <random>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 

@@ -25,6 +25,7 @@
 #include <math.h>
 #include <netinet/in.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdatomic.h>
 #include <stdio.h>
@@ -101,8 +102,12 @@ typedef struct {
     spe_table* table;
     double* mlat;                  /* full host mirror [A][A], or NULL */
     double* mrel;
-    _Atomic(double*)* blocks;      /* lazy mirror per 64-source block: lat[rows][A], rel[rows][A] */
-    _Atomic int64_t row_budget;    /* bytes left for lazy blocks; beyond it: spe_table_get */
+    _Atomic(double*)* blocks;      /* lazy mirror per SOURCE ROW: lat[A], rel[A] (a row is 16 A bytes:
+                                    * 1.6 MB at A = 100k, where a 64-source block was 102 MB) */
+    _Atomic uint8_t* touch;        /* single reads of each row so far (a row is mirrored on its
+                                    * ROW_MIRROR_AFTER-th: a row read once or twice is cheaper
+                                    * as single entries) */
+    _Atomic int64_t row_budget;    /* bytes left for lazy rows; beyond it: spe_table_get_latrel */
     int64_t mirror_budget;         /* the budget this snapshot was given (full or lazy) */
     pthread_mutex_t row_mu;
     double min_latency;            /* over every routable entry */
@@ -661,8 +666,9 @@ static void snap_free(Snap* s) {
     if (!s) return;
     if (s->table) spe_table_free(s->table);
     if (s->blocks) {
-        for (int32_t b = 0; b < (s->A + 63) / 64; ++b) free(atomic_load(&s->blocks[b]));
+        for (int32_t b = 0; b < s->A; ++b) free(atomic_load(&s->blocks[b]));
         free(s->blocks);
+        free((void*)s->touch);
     }
     free(s->mlat);
     free(s->mrel);
@@ -1169,8 +1175,9 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
             tlog(top, LOG_WARNING, "could not save the path table cache: %s", spe_last_error());
     }
     /* host view: the whole table when it fits the mirror budget (mirror_budget: up to
-     * 48 GiB, A <= 56k), else 64-source blocks mirrored on first use within that
-     * budget, then single-entry device reads (spe_table_get); batches of queries
+     * 48 GiB, A <= 56k; spe_table_download streams it through pinned staging), else
+     * source rows mirrored once they are read repeatedly, within that budget, and
+     * single-record device reads (spe_table_get_latrel) otherwise; batches of queries
      * read the device table in one launch (topology_getPathInfoBatch) */
     if (budget < 0) budget = 0;
     s->mirror_budget = budget;
@@ -1181,9 +1188,10 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
         if (!s->mlat || !s->mrel) rc = SPE_ENOMEM;
         else rc = spe_table_download(s->table, 0, A, s->mlat, s->mrel, NULL, NULL);
     } else if (rc == SPE_OK) {
-        s->blocks = calloc((size_t)(A + 63) / 64, sizeof(*s->blocks));
+        s->blocks = calloc((size_t)A, sizeof(*s->blocks));
+        s->touch = calloc((size_t)A, sizeof(*s->touch));
         atomic_store(&s->row_budget, budget);
-        if (!s->blocks) rc = SPE_ENOMEM;
+        if (!s->blocks || !s->touch) rc = SPE_ENOMEM;
     }
     if (rc == SPE_OK) rc = spe_table_min_latency(s->table, &s->min_latency);
     if (rc != SPE_OK) {
@@ -1246,6 +1254,8 @@ int32_t topology_seal(Topology* top) {
 
 /* Latency and reliability of table entry (s, t) of a published snapshot; the
  * caller holds state_lock shared. */
+#define ROW_MIRROR_AFTER 3
+
 static void snap_value(Topology* top, Snap* sn, int32_t s, int32_t t, double* lat, double* rel) {
     const int32_t A = sn->A;
     if (sn->mlat) {
@@ -1253,29 +1263,29 @@ static void snap_value(Topology* top, Snap* sn, int32_t s, int32_t t, double* la
         *rel = sn->mrel[(size_t)s * A + t];
         return;
     }
-    const int32_t b = s / 64, r0 = b * 64, nr = (A - r0) < 64 ? A - r0 : 64;
-    const int64_t bytes = (int64_t)nr * A * 16;
-    double* blk = atomic_load_explicit(&sn->blocks[b], memory_order_acquire);
-    if (!blk) {
+    const int64_t bytes = (int64_t)A * 16;
+    double* row = atomic_load_explicit(&sn->blocks[s], memory_order_acquire);
+    if (!row && atomic_fetch_add(&sn->touch[s], 1) + 1 >= ROW_MIRROR_AFTER && atomic_load(&sn->row_budget) >= bytes) {
         pthread_mutex_lock(&sn->row_mu);
-        blk = atomic_load_explicit(&sn->blocks[b], memory_order_acquire);
-        if (!blk && atomic_load(&sn->row_budget) >= bytes) {
-            blk = malloc((size_t)bytes);
-            if (blk && spe_table_download(sn->table, r0, r0 + nr, blk, blk + (size_t)nr * A, NULL, NULL) == SPE_OK) {
+        row = atomic_load_explicit(&sn->blocks[s], memory_order_acquire);
+        if (!row && atomic_load(&sn->row_budget) >= bytes) {
+            row = malloc((size_t)bytes);
+            if (row && spe_table_download(sn->table, s, s + 1, row, row + A, NULL, NULL) == SPE_OK) {
                 atomic_fetch_sub(&sn->row_budget, bytes);
-                atomic_store_explicit(&sn->blocks[b], blk, memory_order_release);
+                atomic_store_explicit(&sn->blocks[s], row, memory_order_release);
             } else {
-                free(blk);
-                blk = NULL;
+                free(row);
+                row = NULL;
             }
         }
         pthread_mutex_unlock(&sn->row_mu);
     }
-    if (blk) {
-        *lat = blk[(size_t)(s - r0) * A + t];
-        *rel = blk[((size_t)nr + (s - r0)) * A + t];
+    if (row) {
+        *lat = row[t];
+        *rel = row[(size_t)A + t];
         return;
     }
+    if (spe_table_get_latrel(sn->table, s, t, lat, rel) == SPE_OK) return;
     spe_entry e;
     if (spe_table_get(sn->table, s, t, &e) == SPE_OK) {
         *lat = e.latency;
@@ -1698,7 +1708,10 @@ typedef struct {
     const double* lat;
     uint8_t* routable;
     int64_t count;
+    int resolve_only;   /* phase 1 without the cache entries (batch_entries does them) */
 } BatchJob;
+
+static void* batch_entries(void* p);
 
 static void* batch_phase1(void* p) {
     BatchJob* j = p;
@@ -1716,6 +1729,18 @@ static void* batch_phase1(void* p) {
             j->uncovered = 1;
             return NULL;
         }
+        j->st[i] = BQ_MISS;
+    }
+    return j->resolve_only ? NULL : batch_entries(p);
+}
+
+/* the answering cache entry of every resolved query (read-only: hits) */
+static void* batch_entries(void* p) {
+    BatchJob* j = p;
+    Topology* top = j->top;
+    for (int64_t i = j->a; i < j->b; ++i) {
+        if (j->st[i] == BQ_BAD) continue;
+        const int32_t sv = j->sv[i], dv = j->dv[i];
         int32_t x, y, kind = K_NONE;
         if (find_entry(top, sv, dv, !top->directed, &x, &y, &kind)) {
             j->st[i] = BQ_HIT;
@@ -1770,13 +1795,33 @@ static void batch_run(int T, BatchJob* jobs, void* (*fn)(void*)) {
     }
 }
 
+/* the CPUs this process may use: its affinity mask, within a cgroup CPU quota if one is set */
+static int host_cpus(void) {
+    static int cached = 0;
+    if (cached > 0) return cached;
+    int n = 0;
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
+    if (n <= 0) n = (int)sysconf(_SC_NPROCESSORS_ONLN);
+    FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r");
+    if (f) {
+        char q[32] = {0};
+        long per = 0;
+        if (fscanf(f, "%31s %ld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0) {
+            const int quota = (int)((atol(q) + per - 1) / per);
+            if (quota > 0 && quota < n) n = quota;
+        }
+        fclose(f);
+    }
+    cached = n > 0 ? n : 1;
+    return cached;
+}
+
 static int batch_threads(int64_t n) {
     if (n < 65536) return 1;
-    int t = 16;
+    int t = host_cpus();   /* every CPU the process has (SHADOW_SPE_BATCH_THREADS overrides) */
     const char* e = getenv("SHADOW_SPE_BATCH_THREADS");
     if (e && atoi(e) > 0) t = atoi(e);
-    const long nc = sysconf(_SC_NPROCESSORS_ONLN);
-    if (nc > 0 && t > nc) t = (int)nc;
     if ((int64_t)t > n / 16384) t = (int)(n / 16384);
     return t < 1 ? 1 : (t > 64 ? 64 : t);
 }
@@ -1830,9 +1875,11 @@ static int batch_res_alloc(Topology* top, int64_t n, BatchRes* r) {
     return 1;
 }
 
-/* Phase 1.  Returns the snapshot with state_lock held shared, or NULL (lock
- * released) when no covering table could be sealed or memory ran out. */
-static Snap* batch_prepare(Topology* top, int64_t n, const spe_in_addr_t* src, const spe_in_addr_t* dst, BatchRes* r) {
+/* Phase 1 (resolve_only: addresses only, the entries left to batch_entries).
+ * Returns the snapshot with state_lock held shared, or NULL (lock released) when
+ * no covering table could be sealed or memory ran out. */
+static Snap* batch_prepare(Topology* top, int64_t n, const spe_in_addr_t* src, const spe_in_addr_t* dst, BatchRes* r,
+                           int resolve_only) {
     if (!batch_res_alloc(top, n, r)) {
         batch_res_free(r);
         return NULL;
@@ -1846,7 +1893,7 @@ static Snap* batch_prepare(Topology* top, int64_t n, const spe_in_addr_t* src, c
         if (covered) {
             for (int k = 0; k < T; ++k)
                 jobs[k] = (BatchJob){top, sn, src, dst, n * k / T, n * (k + 1) / T,
-                                     r->sv, r->dv, r->x, r->y, r->st, r->kind, 0, NULL, NULL, NULL, 0};
+                                     r->sv, r->dv, r->x, r->y, r->st, r->kind, 0, NULL, NULL, NULL, 0, resolve_only};
             batch_run(T, jobs, batch_phase1);
             for (int k = 0; k < T; ++k) covered &= !jobs[k].uncovered;
         }
@@ -1892,6 +1939,22 @@ static void batch_phase2(Topology* top, Snap* sn, int64_t n, const spe_in_addr_t
     }
 }
 
+typedef struct {
+    const spe_table* table;
+    const int32_t* pairs;
+    int64_t n;
+    double* lat;
+    double* rel;
+    uint8_t* ok;
+    int rc;
+} LookupJob;
+
+static void* batch_lookup(void* p) {   /* the device read of a batch, beside the cache bookkeeping */
+    LookupJob* j = p;
+    j->rc = spe_lookup_batch_host(j->table, j->pairs, j->n, j->lat, j->rel, j->ok);
+    return NULL;
+}
+
 int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t* srcAddress,
                                   const spe_in_addr_t* dstAddress, double* latency, double* reliability,
                                   uint8_t* routable) {
@@ -1899,8 +1962,11 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
     if (n == 0) return 0;
     const int timing = getenv("SHADOW_SPE_BATCH_TIMING") != NULL;
     const double t0 = timing ? now_s() : 0.0;
+    const int ref = top->cache_mode == TOPOLOGY_ANSWER_REFERENCE;
     BatchRes r;
-    Snap* sn = batch_prepare(top, n, srcAddress, dstAddress, &r);
+    /* rows mode: every query reads its own (s, t), so the table read can start as soon
+     * as the addresses are resolved and run beside the path-cache bookkeeping */
+    Snap* sn = batch_prepare(top, n, srcAddress, dstAddress, &r, !ref);
     if (!sn) {   /* no table could be sealed (or scratch failed): every query unanswered */
         for (int64_t i = 0; i < n; ++i) {
             latency[i] = -1.0;
@@ -1910,44 +1976,52 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
         return -1;
     }
     const double t1 = timing ? now_s() : 0.0;
-    int min_updated = 0;
-    batch_phase2(top, sn, n, srcAddress, dstAddress, &r, &min_updated);
-    const double t2 = timing ? now_s() : 0.0;
     /* (random reads of a whole-table host mirror cost ~100 ns each; one device launch
      * for a large batch costs ~25 B of PCIe traffic per query) */
     const int dev = n >= (sn->mlat ? 4096 : 256);
-    const int ref = top->cache_mode == TOPOLOGY_ANSWER_REFERENCE;
     int32_t* pairs = r.pairs;
     int64_t* at = r.at;
     int64_t nd = 0;
     const int T = batch_threads(n);
     BatchJob jobs[64];
-    if (dev && !ref) {   /* every query reads its own (s, t): slot pairs in parallel */
-        for (int k = 0; k < T; ++k)
-            jobs[k] = (BatchJob){top, sn, NULL, NULL, n * k / T, n * (k + 1) / T, r.sv, r.dv, NULL, NULL, r.st,
-                                 NULL, 0, pairs, NULL, NULL, 0};
-        batch_run(T, jobs, batch_gather);
-        int64_t nbad = 0;
-        for (int k = 0; k < T; ++k) nbad += jobs[k].count;
-        if (nbad == 0) {
-            nd = n;
-        } else {   /* compact the readable ones */
+    int min_updated = 0;
+    double t2 = t1, t3 = t1;
+    if (!ref) {
+        LookupJob lj = {sn->table, pairs, n, latency, reliability, routable, SPE_OK};
+        pthread_t lth;
+        int lstarted = 0;
+        if (dev) {   /* slot pairs (unknown addresses: -1, answered unroutable), then the read */
+            for (int k = 0; k < T; ++k)
+                jobs[k] = (BatchJob){top, sn, NULL, NULL, n * k / T, n * (k + 1) / T, r.sv, r.dv, NULL, NULL, r.st,
+                                     NULL, 0, pairs, NULL, NULL, 0, 0};
+            batch_run(T, jobs, batch_gather);
+            lstarted = pthread_create(&lth, NULL, batch_lookup, &lj) == 0;
+            if (!lstarted) batch_lookup(&lj);
+        }
+        for (int k = 0; k < T; ++k)   /* the cache entries of the hits (read-only) */
+            jobs[k] = (BatchJob){top, sn, srcAddress, dstAddress, n * k / T, n * (k + 1) / T, r.sv, r.dv, r.x, r.y,
+                                 r.st, r.kind, 0, NULL, NULL, NULL, 0, 0};
+        batch_run(T, jobs, batch_entries);
+        t2 = timing ? now_s() : 0.0;
+        batch_phase2(top, sn, n, srcAddress, dstAddress, &r, &min_updated);
+        t3 = timing ? now_s() : 0.0;
+        if (lstarted) pthread_join(lth, NULL);
+        if (!dev || lj.rc != SPE_OK) {
+            if (dev) tlog(top, LOG_WARNING, "batched path table read failed (%s): reading per query", spe_last_error());
             for (int64_t i = 0; i < n; ++i) {
                 latency[i] = reliability[i] = -1.0;
-                if (pairs[2 * i] < 0) continue;
-                pairs[2 * nd] = pairs[2 * i];
-                pairs[2 * nd + 1] = pairs[2 * i + 1];
-                at[nd++] = i;
+                if (r.st[i] == BQ_BAD) continue;
+                snap_value(top, sn, sn->slot_of_vertex[r.sv[i]], sn->slot_of_vertex[r.dv[i]], &latency[i],
+                           &reliability[i]);
             }
         }
-    }
-    for (int64_t i = 0; i < n && !(dev && !ref); ++i) {
-        latency[i] = reliability[i] = -1.0;
-        if (r.st[i] == BQ_BAD) continue;
-        const int hit = r.st[i] == BQ_HIT;
-        int32_t s = sn->slot_of_vertex[r.sv[i]], t = sn->slot_of_vertex[r.dv[i]];
-        if (ref) {
-            if (!hit) {   /* :2023-2029 */
+    } else {   /* reference answers: the cached Path each query hits, after the misses in order */
+        batch_phase2(top, sn, n, srcAddress, dstAddress, &r, &min_updated);
+        t2 = t3 = timing ? now_s() : 0.0;
+        for (int64_t i = 0; i < n; ++i) {
+            latency[i] = reliability[i] = -1.0;
+            if (r.st[i] == BQ_BAD) continue;
+            if (r.st[i] != BQ_HIT) {   /* :2023-2029 */
                 tlog(top, LOG_ERROR, "unable to find path between vertex %d (%s) and vertex %d (%s)", r.sv[i],
                      top->vstr[VS_ID][r.sv[i]], r.dv[i], top->vstr[VS_ID][r.dv[i]]);
                 continue;
@@ -1959,50 +2033,43 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
                 reliability[i] = e.reliability;
                 continue;
             }
-            s = sn->slot_of_vertex[r.x[i]];
-            t = sn->slot_of_vertex[r.y[i]];
-        }
-        if (dev) {
-            pairs[2 * nd] = s;
-            pairs[2 * nd + 1] = t;
-            at[nd++] = i;
-        } else {
-            snap_value(top, sn, s, t, &latency[i], &reliability[i]);
-        }
-    }
-    const double t3 = timing ? now_s() : 0.0;
-    if (nd == n) {   /* every query reads the table: answers straight into the outputs */
-        if (spe_lookup_batch_host(sn->table, pairs, nd, latency, reliability, routable) != SPE_OK) {
-            tlog(top, LOG_WARNING, "batched path table read failed (%s): reading per query", spe_last_error());
-            for (int64_t k = 0; k < nd; ++k) snap_value(top, sn, pairs[2 * k], pairs[2 * k + 1], &latency[k], &reliability[k]);
-        }
-    } else if (nd > 0) {
-        double* lr = malloc((size_t)nd * 2 * sizeof(double));
-        uint8_t* okd = malloc((size_t)nd);
-        if (lr && okd && spe_lookup_batch_host(sn->table, pairs, nd, lr, lr + nd, okd) == SPE_OK) {
-            for (int64_t k = 0; k < nd; ++k) {
-                latency[at[k]] = lr[k];
-                reliability[at[k]] = lr[nd + k];
+            const int32_t s = sn->slot_of_vertex[r.x[i]], t = sn->slot_of_vertex[r.y[i]];
+            if (dev) {
+                pairs[2 * nd] = s;
+                pairs[2 * nd + 1] = t;
+                at[nd++] = i;
+            } else {
+                snap_value(top, sn, s, t, &latency[i], &reliability[i]);
             }
-        } else {   /* per query */
-            tlog(top, LOG_WARNING, "batched path table read failed (%s): reading per query", spe_last_error());
-            for (int64_t k = 0; k < nd; ++k)
-                snap_value(top, sn, pairs[2 * k], pairs[2 * k + 1], &latency[at[k]], &reliability[at[k]]);
         }
-        free(lr);
-        free(okd);
+        if (nd > 0) {
+            double* lr = malloc((size_t)nd * 2 * sizeof(double));
+            uint8_t* okd = malloc((size_t)nd);
+            if (lr && okd && spe_lookup_batch_host(sn->table, pairs, nd, lr, lr + nd, okd) == SPE_OK) {
+                for (int64_t k = 0; k < nd; ++k) {
+                    latency[at[k]] = lr[k];
+                    reliability[at[k]] = lr[nd + k];
+                }
+            } else {   /* per query */
+                tlog(top, LOG_WARNING, "batched path table read failed (%s): reading per query", spe_last_error());
+                for (int64_t k = 0; k < nd; ++k)
+                    snap_value(top, sn, pairs[2 * k], pairs[2 * k + 1], &latency[at[k]], &reliability[at[k]]);
+            }
+            free(lr);
+            free(okd);
+        }
     }
     pthread_rwlock_unlock(&top->state_lock);
     if (timing)
         fprintf(stderr,
-                "[topology] batch of %lld: resolve + cached entries %.3f s, misses in order %.3f s, "
-                "gather %.3f s, table reads %.3f s\n",
+                "[topology] batch of %lld: resolve %.3f s, cached entries %.3f s, misses in order %.3f s, "
+                "table reads (beside the two before, rows mode) done %.3f s later\n",
                 (long long)n, t1 - t0, t2 - t1, t3 - t2, now_s() - t3);
     batch_res_free(&r);
     batch_min_callback(top, min_updated);
     for (int k = 0; k < T; ++k)
         jobs[k] = (BatchJob){top, NULL, NULL, NULL, n * k / T, n * (k + 1) / T, NULL, NULL, NULL, NULL, NULL, NULL,
-                             0, NULL, latency, routable, 0};
+                             0, NULL, latency, routable, 0, 0};
     batch_run(T, jobs, batch_finish);
     int64_t nok = 0;
     for (int k = 0; k < T; ++k) nok += jobs[k].count;
@@ -2013,7 +2080,7 @@ void topology_incrementPathPacketCounterBatch(Topology* top, int64_t n, const sp
                                               const spe_in_addr_t* dstAddress) {
     if (!top || n <= 0 || !srcAddress || !dstAddress) return;
     BatchRes r;
-    Snap* sn = batch_prepare(top, n, srcAddress, dstAddress, &r);
+    Snap* sn = batch_prepare(top, n, srcAddress, dstAddress, &r, 0);
     if (!sn) return;
     int min_updated = 0;
     batch_phase2(top, sn, n, srcAddress, dstAddress, &r, &min_updated);
@@ -2021,7 +2088,7 @@ void topology_incrementPathPacketCounterBatch(Topology* top, int64_t n, const sp
     BatchJob jobs[64];
     for (int k = 0; k < T; ++k)
         jobs[k] = (BatchJob){top, sn, NULL, NULL, n * k / T, n * (k + 1) / T, NULL, NULL, r.x, r.y, r.st, NULL, 0,
-                             NULL, NULL, NULL, 0};
+                             NULL, NULL, NULL, 0, 0};
     batch_run(T, jobs, batch_count);
     pthread_rwlock_unlock(&top->state_lock);
     batch_res_free(&r);

@@ -136,7 +136,7 @@ EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_
            "spe_graph_set_edge_aux", "spe_table_download_aux", "spe_fw_apsp", "spe_fw_closure", "spe_graph_self_path",
            "spe_graph_adjacent", "spe_device_shares", "spe_graph_edge", "spe_table_source_tree",
            "spe_device_split", "spe_lookup_batch_replica", "spe_table_replica_device", "spe_table_check",
-           "spe_lookup_batch_host", "spe_table_compare"]
+           "spe_lookup_batch_host", "spe_table_compare", "spe_table_get_latrel"]
 
 _lib = None
 
@@ -172,6 +172,7 @@ def lib():
         L.spe_table_build_stats.argtypes = [P, P]
         L.spe_table_layout_get.argtypes = [P, P]
         L.spe_table_get.argtypes = [P, C.c_int32, C.c_int32, P]
+        L.spe_table_get_latrel.argtypes = [P, C.c_int32, C.c_int32, P, P]
         L.spe_table_download.argtypes = [P, C.c_int32, C.c_int32, P, P, P, P]
         L.spe_lookup_batch.argtypes = [P, P, C.c_int64, P, P, P, P]
         L.spe_lookup_batch_replica.argtypes = [P, C.c_int32, P, C.c_int64, P, P, P, P]
