@@ -76,9 +76,11 @@ def workload(name: str):
 
 
 def host_cores():
-    """Every host core this process may run on (sched_getaffinity: on the GPU box
-    the whole machine, 256 threads), plus the cgroup CPU quota when one is set --
-    the all-cores CPU legs run one thread per core and state both."""
+    """The host cores this job may use: its affinity mask (on the GPU box the whole
+    machine, 256 threads) within the cgroup CPU quota (16 CPUs there) -- the
+    all-cores CPU legs run one thread per usable core and state the machine's count,
+    the quota and the threads used (256 threads on a 16-CPU quota ran 4-5x slower
+    than 16: time-slicing, measured r05)."""
     try:
         n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
@@ -90,7 +92,7 @@ def host_cores():
             quota = round(float(q) / float(per), 2)
     except (OSError, ValueError):
         pass
-    return n, quota
+    return (min(n, max(1, math.ceil(quota))) if quota else n), quota
 
 
 def cpu_baseline(top, att, seconds: float, sources: int = 0, seed: int = 6):
@@ -137,7 +139,7 @@ def cpu_baseline(top, att, seconds: float, sources: int = 0, seed: int = 6):
             "sample": f"{done} seeded-random source rows (seed {seed}, cycling over A = {A}) x {A} targets, full "
                       f"row build, {el:.1f} s; {dij}",
             "optimistic_all_cores": {"value": round(done_all / el_all, 1), "threads": nt,
-                                     "cgroup_cpu_quota": quota,
+                                     "cgroup_cpu_quota": quota, "host_nproc": os.cpu_count(),
                                      "sample": f"{done_all} source rows, {el_all:.1f} s"},
             "cpu_model": model, "host_nproc": os.cpu_count()}
 
@@ -282,7 +284,7 @@ def cpu_lookup_baseline(A: int, seconds: float, seed: int = 5):
             "sample": f"{done} lookups over a 4M-pair cache (seed {seed}): 2 IP->slot probes + src and (src,dst) "
                       f"cache probes per query, {el:.1f} s",
             "optimistic_all_cores": {"value": round(reps * npairs / el_all, 1), "threads": nt,
-                                     "cgroup_cpu_quota": quota}}
+                                     "cgroup_cpu_quota": quota, "host_nproc": os.cpu_count()}}
 
 
 def bench_complete(args):

@@ -348,6 +348,9 @@ int spe_table_get(const spe_table* t, int32_t s_slot, int32_t t_slot, spe_entry*
 /* Only the {latency, reliability} record of one entry (one 16-B read back): what
  * topology_getLatency / getReliability need (shd-topology.c:2036-2061). */
 int spe_table_get_latrel(const spe_table* t, int32_t s_slot, int32_t t_slot, double* latency, double* reliability);
+/* The {latency, reliability} records of one whole source row (n_attached each), read
+ * back in one gather on the device (a host mirror of a row that is read repeatedly). */
+int spe_table_get_row_latrel(const spe_table* t, int32_t s_slot, double* latency, double* reliability);
 /* Copy owned rows [row_begin,row_end) x [0,n_attached) to host, row-major;
  * any output pointer may be NULL. */
 int spe_table_download(const spe_table* t, int32_t row_begin, int32_t row_end, double* latency,

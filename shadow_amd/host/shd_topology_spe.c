@@ -32,6 +32,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <strings.h>
+#include <sys/mman.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -105,8 +106,8 @@ typedef struct {
     _Atomic(double*)* blocks;      /* lazy mirror per SOURCE ROW: lat[A], rel[A] (a row is 16 A bytes:
                                     * 1.6 MB at A = 100k, where a 64-source block was 102 MB) */
     _Atomic uint8_t* touch;        /* single reads of each row so far (a row is mirrored on its
-                                    * ROW_MIRROR_AFTER-th: a row read once or twice is cheaper
-                                    * as single entries) */
+                                    * ROW_MIRROR_AFTER-th: a row read a few times is cheaper as
+                                    * single records) */
     _Atomic int64_t row_budget;    /* bytes left for lazy rows; beyond it: spe_table_get_latrel */
     int64_t mirror_budget;         /* the budget this snapshot was given (full or lazy) */
     pthread_mutex_t row_mu;
@@ -662,6 +663,19 @@ static int cmp_u64(const void* a, const void* b) {
     return x < y ? -1 : x > y;
 }
 
+/* the whole-table host mirror (tens of GB): anonymous pages, transparent huge pages
+ * asked for, so filling it faults 2-MB pages instead of 4-KB ones */
+static void* big_alloc(size_t bytes) {
+    void* p = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) return NULL;
+    (void)madvise(p, bytes, MADV_HUGEPAGE);
+    return p;
+}
+
+static void big_free(void* p, size_t bytes) {
+    if (p) munmap(p, bytes);
+}
+
 static void snap_free(Snap* s) {
     if (!s) return;
     if (s->table) spe_table_free(s->table);
@@ -670,8 +684,8 @@ static void snap_free(Snap* s) {
         free(s->blocks);
         free((void*)s->touch);
     }
-    free(s->mlat);
-    free(s->mrel);
+    big_free(s->mlat, (size_t)s->A * s->A * sizeof(double));
+    big_free(s->mrel, (size_t)s->A * s->A * sizeof(double));
     free(s->slot_of_vertex);
     free(s->attached);
     pthread_mutex_destroy(&s->row_mu);
@@ -1183,8 +1197,8 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
     s->mirror_budget = budget;
     const int64_t full = (int64_t)A * A * 16;
     if (rc == SPE_OK && full <= budget) {
-        s->mlat = malloc((size_t)A * A * sizeof(double));
-        s->mrel = malloc((size_t)A * A * sizeof(double));
+        s->mlat = big_alloc((size_t)A * A * sizeof(double));
+        s->mrel = big_alloc((size_t)A * A * sizeof(double));
         if (!s->mlat || !s->mrel) rc = SPE_ENOMEM;
         else rc = spe_table_download(s->table, 0, A, s->mlat, s->mrel, NULL, NULL);
     } else if (rc == SPE_OK) {
@@ -1254,7 +1268,7 @@ int32_t topology_seal(Topology* top) {
 
 /* Latency and reliability of table entry (s, t) of a published snapshot; the
  * caller holds state_lock shared. */
-#define ROW_MIRROR_AFTER 3
+#define ROW_MIRROR_AFTER 4
 
 static void snap_value(Topology* top, Snap* sn, int32_t s, int32_t t, double* lat, double* rel) {
     const int32_t A = sn->A;
@@ -1270,7 +1284,7 @@ static void snap_value(Topology* top, Snap* sn, int32_t s, int32_t t, double* la
         row = atomic_load_explicit(&sn->blocks[s], memory_order_acquire);
         if (!row && atomic_load(&sn->row_budget) >= bytes) {
             row = malloc((size_t)bytes);
-            if (row && spe_table_download(sn->table, s, s + 1, row, row + A, NULL, NULL) == SPE_OK) {
+            if (row && spe_table_get_row_latrel(sn->table, s, row, row + A) == SPE_OK) {
                 atomic_fetch_sub(&sn->row_budget, bytes);
                 atomic_store_explicit(&sn->blocks[s], row, memory_order_release);
             } else {

@@ -136,7 +136,8 @@ EXPORTS = ["spe_last_error", "spe_device_count", "spe_graph_create", "spe_graph_
            "spe_graph_set_edge_aux", "spe_table_download_aux", "spe_fw_apsp", "spe_fw_closure", "spe_graph_self_path",
            "spe_graph_adjacent", "spe_device_shares", "spe_graph_edge", "spe_table_source_tree",
            "spe_device_split", "spe_lookup_batch_replica", "spe_table_replica_device", "spe_table_check",
-           "spe_lookup_batch_host", "spe_table_compare", "spe_table_get_latrel"]
+           "spe_lookup_batch_host", "spe_table_compare", "spe_table_get_latrel",
+           "spe_table_get_row_latrel"]
 
 _lib = None
 

@@ -134,10 +134,12 @@ def test_attach_after_seal_rebuilds_and_keeps_counts(tmp_path):
     top.close()
 
 
-@pytest.mark.parametrize("budget", ["0", "2000"], ids=["device-reads", "one-block"])
+@pytest.mark.parametrize("budget", ["0", "2000"], ids=["device-reads", "one-row"])
 def test_bounded_host_mirror(tmp_path, monkeypatch, budget):
-    """Above SHADOW_SPE_MIRROR_BYTES the host keeps only the 64-source blocks it
-    has been asked for (then reads single entries from HBM): same answers."""
+    """Above SHADOW_SPE_MIRROR_BYTES the host mirrors only source rows read
+    repeatedly, within the budget (a 70-host row is 1,120 B: one fits 2,000), and
+    reads single {latency, reliability} records from HBM otherwise
+    (spe_table_get_latrel / spe_table_get_row_latrel): same answers."""
     monkeypatch.setenv("SHADOW_SPE_MIRROR_BYTES", budget)
     t = graphs.gen_random_small(200, 600, 25)
     top, verts, addrs = setup(tmp_path, t, 70, 25)
