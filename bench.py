@@ -519,8 +519,11 @@ def calibrate_split(t, lr, blk_elems, nblk, world, rank, dev, dist, span_blocks)
     """N > 1: the inputs of dist.shared_fraction, measured untimed on this job --
     the one-GPU whole-table build time T1 (from a build of this rank's share of a
     pure-sharding schedule, scaled by N) and the all-gather bandwidth B (one
-    in-place all_gather_into_tensor of up to 2 GB per rank) -- agreed over the
-    ranks (max T1, min B) so every rank takes the same schedule."""
+    in-place gather of up to 2 GB per rank) -- agreed over the ranks (max T1,
+    min B) so every rank takes the same schedule.  B is measured for both
+    gathers, RCCL's all_gather_into_tensor and world - 1 concurrent peer
+    exchanges (dist.allgather_span_p2p: every xGMI link at once), and the faster
+    one gathers the table (returned as `mode`)."""
     import torch
     share = max(1, nblk // world)
     b0 = min(nblk - 1, rank * share)
@@ -536,17 +539,21 @@ def calibrate_split(t, lr, blk_elems, nblk, world, rank, dev, dist, span_blocks)
     del nx, hp
     from shadow_amd import dist as sd
     per = max(1, min(span_blocks // world, int(2e9 // (blk_elems * 16))))
-    sd.allgather_span(lr, 0, per, world, rank, blk_elems, dist)   # warm the communicator
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    t0 = time.perf_counter()
-    sd.allgather_span(lr, 0, per, world, rank, blk_elems, dist)
-    torch.cuda.synchronize(dev)
-    el = time.perf_counter() - t0
     recv = (world - 1) * per * blk_elems * 16.0
-    x = torch.tensor([t1, -recv / max(el, 1e-9)], dtype=torch.float64, device=dev)
+    rates = []
+    for fn in (sd.allgather_span, sd.allgather_span_p2p):
+        fn(lr, 0, per, world, rank, blk_elems, dist)   # warm the communicator / peer connections
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        fn(lr, 0, per, world, rank, blk_elems, dist)
+        torch.cuda.synchronize(dev)
+        rates.append(-recv / max(time.perf_counter() - t0, 1e-9))
+    x = torch.tensor([t1] + rates, dtype=torch.float64, device=dev)
     dist.all_reduce(x, op=dist.ReduceOp.MAX)
-    return float(x[0].item()), float(-x[1].item())
+    coll, p2p = float(-x[1].item()), float(-x[2].item())
+    mode = "p2p" if p2p > coll else "all_gather"
+    return float(x[0].item()), max(coll, p2p), mode, {"all_gather": round(coll / 1e9, 1), "p2p": round(p2p / 1e9, 1)}
 
 
 def bench_table(args, rank, world, local, dist, config=None, replica_only=False):
@@ -598,10 +605,13 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
     if gpl == 0:
         gpl = t.layout()["groups_per_launch"]
     calib = None
+    gather_fn = sd.allgather_span_p2p if args.gather == "p2p" else sd.allgather_span
     frac = 1.0 if not gather else args.shared_frac
     if gather and frac < 0:   # auto: measure T1 and B on this job, then plan
         calib = calibrate_split(t, lr, blk_elems, nblk, world, rank, dev, dist, pad_blocks)
         frac = sd.shared_fraction(world, calib[0], nblk * blk_elems * 16.0, calib[1])
+        if args.gather == "auto":
+            gather_fn = sd.allgather_span_p2p if calib[2] == "p2p" else sd.allgather_span
     # one GPU with shared anchor trees: the whole table is one build call,
     # so the library batches by anchor roots (its state holds `gpl` blocks of roots)
     sched_gpl = nblk if (world == 1 and not emulated and t.layout()["shared_sources"]) else gpl
@@ -635,7 +645,7 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
                 derived_run[1] += st["fallback_blocks"]
             tb += time.perf_counter() - t0
             if gather:   # overlaps the next round's build and the local part (RCCL runs on its own stream)
-                w = sd.allgather_span(lr, off, gk, world, rank, blk_elems, dist, async_op=True)
+                w = gather_fn(lr, off, gk, world, rank, blk_elems, dist, async_op=True)
                 if w is not None:
                     works.append(w)
         if l1 > l0 and not emulated:   # built by every rank itself: no exchange
@@ -781,8 +791,10 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
         if gather:
             line["split"] = {"shared_fraction": round(frac, 4), "shared_blocks": min(S, nblk), "local_blocks": l1 - l0,
                              "model": "x* = T1 N / ((N - 1) (S / B + T1)) (DESIGN 6)",
+                             "gather": "p2p" if gather_fn is sd.allgather_span_p2p else "all_gather",
                              "calibration": None if calib is None else {"t1_s": round(calib[0], 4),
-                                                                        "gather_GBps": round(calib[1] / 1e9, 1)},
+                                                                        "gather_GBps": round(calib[1] / 1e9, 1),
+                                                                        "gather_GBps_by_mode": calib[3]},
                              "per_rank_build_gather_s": per_rank}
         line.update(extra)
         if cpu:
@@ -1052,6 +1064,9 @@ def main():
                          "and report its differences from the default build (spe_table_compare)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the all-gather (build only)")
+    ap.add_argument("--gather", choices=("auto", "all_gather", "p2p"), default="auto",
+                    help="N > 1: RCCL all_gather_into_tensor or world - 1 concurrent peer exchanges; auto = the faster "
+                         "one measured by the split calibration (all_gather when the fraction is given)")
     ap.add_argument("--queries", type=int, default=100_000_000, help="c5: lookups per step")
     ap.add_argument("--c5-table", default="c3", choices=("c3", "c4"),
                     help="c5: the table the lookups read (c4: 100k x 100k, 220 GB on one GPU)")

@@ -155,6 +155,42 @@ def allgather_span(lr, off: int, g: int, world: int, rank: int, blk_elems: int, 
     return dist.all_gather_into_tensor(grp, own, async_op=async_op)
 
 
+class _Requests:
+    """The P2P requests of one gather, waited on together (the async handle)."""
+
+    def __init__(self, reqs):
+        self.reqs = list(reqs)
+
+    def wait(self):
+        for r in self.reqs:
+            r.wait()
+        return True
+
+
+def allgather_span_p2p(lr, off: int, g: int, world: int, rank: int, blk_elems: int, dist, async_op: bool = False):
+    """The same in-place gather as allgather_span, as world - 1 concurrent
+    point-to-point exchanges per rank (one batch_isend_irecv group: every peer's part
+    arrives over its own xGMI link at once, SURVEY §5's 7 concurrent peer copies per
+    GPU) instead of the collective's own algorithm.  bench.py measures both and
+    gathers with the faster (split.calibration)."""
+    grp = lr[off * blk_elems:(off + world * g) * blk_elems]
+    parts = list(grp.chunk(world))
+    own = parts[rank]
+    ops = []
+    for p in range(world):
+        if p == rank:
+            continue
+        ops.append(dist.P2POp(dist.isend, own, p))
+        ops.append(dist.P2POp(dist.irecv, parts[p], p))
+    if not ops:
+        return None
+    reqs = _Requests(dist.batch_isend_irecv(ops))
+    if async_op:
+        return reqs
+    reqs.wait()
+    return None
+
+
 def allgather_round(lr, k: int, world: int, rank: int, chunk_elems: int, dist, async_op: bool = False):
     """All-gather round k's records in place: rank r's chunk (k * world + r) sits
     at element (k * world + r) * chunk_elems of `lr` on every rank, so the round

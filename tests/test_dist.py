@@ -122,8 +122,10 @@ def test_chunk_schedule_front_loaded_and_covering():
                 assert sorted(seen) == list(range(nblk))
 
 
-def _sched_worker(rank, world, port, out_q):
-    """The same with chunk_schedule + allgather_span (what bench.py runs)."""
+def _sched_worker(rank, world, port, out_q, mode="all_gather"):
+    """The same with chunk_schedule + allgather_span (what bench.py runs); mode
+    "p2p" gathers with allgather_span_p2p (world - 1 concurrent peer exchanges,
+    asynchronous and waited at the end, as bench.py overlaps them)."""
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -138,13 +140,21 @@ def _sched_worker(rank, world, port, out_q):
     blk = top.n * 64
     lr = torch.full((world * sum(sizes) * blk, 2), float("nan"), dtype=torch.float64)
     o = Oracle(top)
+    works = []
     for k, off, g, b0, b1 in sd.rank_chunks_sched(nblk, world, rank, sizes):
         if b1 > b0:
             rows = o.rows(A[b0 * 64:min(top.n, b1 * 64)], A)
             rows["hops"] = rows["hops"].astype(np.uint16)
             f = sd.rows_to_sb64(rows, b0 * 64, top.n, b1 - b0)
             lr[b0 * blk:b1 * blk] = torch.from_numpy(f["lr"])
-        sd.allgather_span(lr, off, g, world, rank, blk, dist)
+        if mode == "p2p":
+            w = sd.allgather_span_p2p(lr, off, g, world, rank, blk, dist, async_op=True)
+            if w is not None:
+                works.append(w)
+        else:
+            sd.allgather_span(lr, off, g, world, rank, blk, dist)
+    for w in works:
+        w.wait()
     ref = o.rows(A, A)
     e = sd.sb64_index(np.repeat(A, top.n), np.tile(A, top.n), top.n)
     got = lr.numpy()[e]
@@ -153,8 +163,8 @@ def _sched_worker(rank, world, port, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_chunk_schedule_allgather(world):
+@pytest.mark.parametrize("world,mode", [(2, "all_gather"), (3, "all_gather"), (2, "p2p"), (3, "p2p")])
+def test_gloo_chunk_schedule_allgather(world, mode):
     import socket
     import torch.multiprocessing as mp
     with socket.socket() as s:
@@ -162,7 +172,7 @@ def test_gloo_chunk_schedule_allgather(world):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_sched_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_sched_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=180) for _ in procs)
