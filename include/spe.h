@@ -171,7 +171,7 @@ typedef struct spe_table_opts {
     int32_t waves_per_simd;         /* occupancy the relaxation kernel is held to (0 = the shape's
                                      * default, 1 = the compiler's choice) */
     int32_t no_overlap;             /* 1: batch i's rows do not overlap batch i+1's relaxation */
-    double delta_ms;                /* > 0: Delta-stepping schedule (measured slower) */
+    double delta_ms;                /* > 0: Delta-stepping schedule (measured slower, MEASUREMENTS.md) */
     int32_t trace;                  /* 1: per-launch kernel times to stderr while profiling */
     /* Multi-device compute-versus-gather split: the first S source blocks
      * are sharded (contiguous shares, built in chunks whose records are broadcast to

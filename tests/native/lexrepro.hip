@@ -1,5 +1,5 @@
 // lexrepro.hip -- test-only reproducer of a gfx950 code-generation fault (ROCm 7.2)
-// behind wrong route tie-breaks at hubs.  Not part of
+// behind wrong route tie-breaks at hubs (MEASUREMENTS.md, round 4).  Not part of
 // libspe: tests/test_gpu_lexrepro.py loads it as a checker of the compiler.
 //
 // The heavy partial kept a running lexicographic best (alt, d[u], u) over

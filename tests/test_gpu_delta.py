@@ -1,5 +1,5 @@
 """GPU parity of the batch engine's experimental Delta-stepping schedule
-(SPE_DELTA=<ms>): each lane group relaxes only offers below its
+(SPE_DELTA=<ms>, MEASUREMENTS.md): each lane group relaxes only offers below its
 bucket bound, parks rows with larger offers and rescans them when its bound
 advances.  The fixpoint is the same, so the rows must equal the oracle's bit for
 bit at both relaxation widths (64 and 128 sources per row), on tie-free, pendant,
@@ -56,7 +56,7 @@ def test_delta_schedule_rows_match_oracle(spe, monkeypatch, name, delta, lanes):
 
 def test_delta_schedule_takes_more_rounds(spe, monkeypatch):
     """Buckets serialise the relaxation: a small Delta needs more rounds than
-    the Gauss-Seidel default on the same table (the cost DESIGN §8 measures)."""
+    the Gauss-Seidel default on the same table (the cost MEASUREMENTS.md measures)."""
     top = graphs.gen_ba(3000, 3, seed=11)
     A = np.arange(top.n, dtype=np.int32)
     g = spe.Graph(top)

@@ -1,5 +1,5 @@
 """Guard for the gfx950 code-generation fault behind round 4's wrong tie-breaks at
-hubs: a running lexicographic best (alt, d[u], u) over candidates
+hubs (MEASUREMENTS.md): a running lexicographic best (alt, d[u], u) over candidates
 whose vertex u is wave-uniform.  The short-circuit compare
 `alt < ba || (alt == ba && (du < bdu || (du == bdu && u < bu)))` followed by four
 assignments compiled (ROCm 7.2) to code whose tie-winning lanes took the new

@@ -5,7 +5,7 @@ the route must then follow the canonical parent argmin (d[u], u),
 which the oracle restates (tie_mode 1, shd-topology.c:1741's Dijkstra with a
 documented tie-break).
 
-Regression for a gfx950 code-generation fault: the short-circuit form
+Regression for a gfx950 code-generation fault (MEASUREMENTS.md): the short-circuit form
 of the heavy-vertex partial's lexicographic compare kept the old parent entry on
 lanes that won a tie on (d[u], u), so hubs recorded the losing parent on about
 1 % of sources.  Every relaxation kernel shape, with and without the degree-3

@@ -2,7 +2,7 @@
 
 The gfx950 backend (ROCm 7.2) miscompiled `a < A || (a == A && (...))` followed by
 several assignments when a key was wave-uniform: tie-winning lanes kept stale
-fields (reproducer tests/native/lexrepro.hip,
+fields (MEASUREMENTS.md; reproducer tests/native/lexrepro.hip,
 tests/test_gpu_lexrepro.py).  Every lexicographic compare in the kernels is written
 branch-free (lex_less3 / lex_less2: bitwise & / | on bools, then selects); this test
 keeps the short-circuit form from coming back."""

@@ -24,6 +24,7 @@ for C in ${CONFIGS:-c3 c4 c1 c5_on_c4 c2 c5 c2fw}; do
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_$C -o run --output-format csv -- python bench.py $A > $O/pmc_write_$C.log 2>&1
     mkdir -p $O/pmc_$C && cp -r $O/pmc_fetch_$C $O/pmc_write_$C $O/pmc_$C/
     python tools/pmc_to_json.py $O/pmc_$C profiles/${R}_pmc_$C.json $O/pmc_fetch_$C.log > /dev/null
+    cp profiles/${R}_pmc_$C.json $O/   # only gpurun_out/ comes back from the box
   fi
   timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $O/kt_$C -o run --output-format csv -- python bench.py $A > $O/kt_$C.log 2>&1
   timeout -k 10 300 python -u bench.py $A > $O/bench_$C.log 2>&1

@@ -5,7 +5,7 @@ taken from a Voronoi-cell source order like spe_order_sources'.
     gcc -O2 -shared -fPIC -o tools/_sim_records.so tools/sim_records.c
     python tools/sim_records.py [c3|c4] [groups]
 
-Result (C3, 3 groups): GS 605 weighted lines per vertex and group,
+Result (C3, 3 groups, MEASUREMENTS.md): GS 605 weighted lines per vertex and group,
 REC 795, DIST 771 -- neither alternative beats the shipped schedule.
 """
 import ctypes as C
