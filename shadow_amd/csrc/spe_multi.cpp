@@ -8,11 +8,14 @@
 // host thread per device on that device's own stream.  The parts write their
 // {latency, reliability} records straight into a full-size replica on their own
 // device (at their share's offset), and one all-gather then fills every replica:
-//   RCCL  ncclCommInitAll over the device list + ncclGroupStart / ncclAllGather
-//         (in place: each device's send buffer is its own share of its replica)
-//         / ncclGroupEnd -- RCCL's collective over the xGMI links;
-//   PEER  hipMemcpyPeerAsync of every share to every other device (also the path
-//         for a device list that repeats a GPU, which RCCL refuses).
+//   RCCL  ncclCommInitAll over the device list; per gather round one group of
+//         ncclSend / ncclRecv pairs, every share's chunk from its owner to every
+//         other device in place -- N - 1 concurrent point-to-point transfers into
+//         each device, one per xGMI link (SPE_RCCL_BCAST=1: one ncclBroadcast
+//         per root instead, RCCL's ring / tree);
+//   PEER  hipMemcpyPeerAsync of every share to every other device, each source
+//         device on its own stream so a receiver's N - 1 copies run concurrently
+//         (also the path for a device list that repeats a GPU, which RCCL refuses).
 // Next hop and hop count stay with the device that built them.  RCCL is loaded
 // with dlopen on first use, so single-device users never load it.
 #include <dlfcn.h>
@@ -22,6 +25,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -43,6 +47,8 @@ struct Rccl {
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*group_start)() = nullptr;
     ncclResult_t (*group_end)() = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
@@ -61,6 +67,8 @@ Rccl& rccl_lib() {
     r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
     r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
     r.broadcast = (decltype(r.broadcast))dlsym(h, "ncclBroadcast");
+    r.send = (decltype(r.send))dlsym(h, "ncclSend");   // optional: broadcasts without them
+    r.recv = (decltype(r.recv))dlsym(h, "ncclRecv");
     r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
     r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
     r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
@@ -91,6 +99,8 @@ struct MultiDev {
     std::vector<void*> next, hops;         // the device's own share
     std::vector<void*> lnext, lhops;       // the device's own copy of the local remainder
     std::vector<hipStream_t> streams;      // per device: the gather stream
+    std::vector<std::vector<hipStream_t>> pstreams;   // PEER: [receiver][source device] copy streams
+    std::vector<std::vector<hipEvent_t>> pevents;     // ... and their completion events (joined into streams)
     std::vector<ncclComm_t> comms;
     bool built = false;
     bool fw = false;                       // FW-engine parts: one closure across the devices
@@ -181,6 +191,17 @@ int multi_create(spe_graph* g, const int32_t* attached, int32_t A, const spe_tab
         }
         hipError_t e = hipSetDevice(m->devs[d]);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->streams[d], hipStreamNonBlocking);
+        if (m->gather == SPE_GATHER_PEER) {
+            m->pstreams.resize(nd);
+            m->pevents.resize(nd);
+            m->pstreams[d].assign(nd, nullptr);
+            m->pevents[d].assign(nd, nullptr);
+            for (int q = 0; q < nd && e == hipSuccess; ++q) {
+                if (q == d) continue;
+                e = hipStreamCreateWithFlags(&m->pstreams[d][q], hipStreamNonBlocking);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&m->pevents[d][q], hipEventDisableTiming);
+            }
+        }
         if (e == hipSuccess) e = hipMalloc(&m->replica[d], rep_bytes);
         if (e == hipSuccess) e = hipMalloc(&m->next[d], std::max<size_t>(1, own) * sizeof(int32_t));
         if (e == hipSuccess) e = hipMalloc(&m->hops[d], std::max<size_t>(1, own) * sizeof(uint16_t));
@@ -246,17 +267,61 @@ void multi_free(MultiDev* m) {
         for (void* p : {m->replica[d], m->next[d], m->hops[d], m->lnext[d], m->lhops[d]})
             if (p) (void)hipFree(p);
         if (m->streams[d]) (void)hipStreamDestroy(m->streams[d]);
+        if (d < (int)m->pstreams.size())
+            for (int q = 0; q < (int)m->pstreams[d].size(); ++q) {
+                if (m->pstreams[d][q]) {
+                    (void)hipStreamSynchronize(m->pstreams[d][q]);
+                    (void)hipStreamDestroy(m->pstreams[d][q]);
+                }
+                if (m->pevents[d][q]) (void)hipEventDestroy(m->pevents[d][q]);
+            }
         if (m->graphs[d] && m->graphs[d] != m->home) spe_graph_free(m->graphs[d]);
     }
     delete m;
 }
 
 // Round k of the gather: every share's chunk k -- blocks [b0 + k c, b0 + (k + 1) c)
-// clipped to the share -- to every other device.  RCCL: one group of ncclBroadcast,
-// one per root, in place on every replica (the chunks of a round are not
-// contiguous, so an all-gather does not fit); PEER: each device pulls the other
-// chunks on its gather stream.  The chunks were built synchronously before.
+// clipped to the share -- to every other device, in place on every replica (the
+// chunks of a round are not contiguous, so an all-gather does not fit).  RCCL: one
+// group of send / receive pairs (each device receives its N - 1 chunks over N - 1
+// links at once), or one ncclBroadcast per root; PEER: each device pulls the other
+// chunks, one stream per source device, joined into its gather stream.  The chunks
+// were built synchronously before.
 static int gather_round(MultiDev* m, int32_t k) {
+    static const bool bcast = [] {
+        const char* e = getenv("SPE_RCCL_BCAST");
+        return e && *e && *e != '0';
+    }();
+    if (m->gather == SPE_GATHER_RCCL && !bcast && rccl_lib().send && rccl_lib().recv) {
+        Rccl& R = rccl_lib();
+        R.group_start();
+        ncclResult_t nr = ncclSuccess;
+        for (int root = 0; root < m->n && nr == ncclSuccess; ++root) {
+            const int32_t c0 = std::min(m->b1[root], m->b0[root] + k * m->chunk);
+            const int32_t c1 = std::min(m->b1[root], c0 + m->chunk);
+            if (c1 <= c0) continue;
+            const size_t off = (size_t)c0 * m->blk_bytes();
+            const size_t cnt = (size_t)(c1 - c0) * m->blk_elems() * 2;
+            for (int d = 0; d < m->n && nr == ncclSuccess; ++d) {
+                if (d == root) continue;
+                if (hipSetDevice(m->devs[root]) != hipSuccess) {
+                    R.group_end();
+                    return set_error(SPE_EHIP, "hipSetDevice");
+                }
+                nr = R.send((char*)m->replica[root] + off, cnt, ncclDouble, d, m->comms[root], m->streams[root]);
+                if (nr != ncclSuccess) break;
+                if (hipSetDevice(m->devs[d]) != hipSuccess) {
+                    R.group_end();
+                    return set_error(SPE_EHIP, "hipSetDevice");
+                }
+                nr = R.recv((char*)m->replica[d] + off, cnt, ncclDouble, root, m->comms[d], m->streams[d]);
+            }
+        }
+        const ncclResult_t ne = R.group_end();
+        if (nr != ncclSuccess || ne != ncclSuccess)
+            return set_error(SPE_EHIP, std::string("ncclSend/ncclRecv: ") + R.error_string(nr != ncclSuccess ? nr : ne));
+        return SPE_OK;
+    }
     if (m->gather == SPE_GATHER_RCCL) {
         Rccl& R = rccl_lib();
         R.group_start();
@@ -289,9 +354,11 @@ static int gather_round(MultiDev* m, int32_t k) {
             const int32_t c1 = std::min(m->b1[d], c0 + m->chunk);
             if (c1 <= c0) continue;
             const size_t off = (size_t)c0 * m->blk_bytes();
-            const hipError_t he = hipMemcpyPeerAsync((char*)m->replica[e] + off, m->devs[e],
-                                                     (const char*)m->replica[d] + off, m->devs[d],
-                                                     (size_t)(c1 - c0) * m->blk_bytes(), m->streams[e]);
+            hipError_t he = hipMemcpyPeerAsync((char*)m->replica[e] + off, m->devs[e],
+                                               (const char*)m->replica[d] + off, m->devs[d],
+                                               (size_t)(c1 - c0) * m->blk_bytes(), m->pstreams[e][d]);
+            if (he == hipSuccess) he = hipEventRecord(m->pevents[e][d], m->pstreams[e][d]);
+            if (he == hipSuccess) he = hipStreamWaitEvent(m->streams[e], m->pevents[e][d], 0);
             if (he != hipSuccess) return hip_fail("hipMemcpyPeerAsync", he);
         }
     }
