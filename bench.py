@@ -377,9 +377,11 @@ def bench_shim(args, config: str):
     ok, lat, rel = top.path_info_batch(src[:1 << 16], dst[:1 << 16])   # warm-up (code objects, staging)
     print(f"[shim] warm-up batch of {1 << 16} queries {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
     steps = args.steps if args.steps > 0 else 3
+    # the answer buffers a worker reuses every round (allocated and touched untimed)
+    out = (np.zeros(q, np.uint8), np.zeros(q, np.float64), np.zeros(q, np.float64))
     t0 = time.perf_counter()
     for _ in range(steps):
-        ok, lat, rel = top.path_info_batch(src, dst)
+        ok, lat, rel = top.path_info_batch(src, dst, out=out)
     el = time.perf_counter() - t0
     print(f"[shim] {steps} batches of {q} queries {el:.1f} s", file=sys.stderr, flush=True)
     assert ok.all(), "every pair of the synthetic topologies is routable"

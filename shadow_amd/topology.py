@@ -128,18 +128,26 @@ class Topology:
         ok = lib().topology_getPathInfo(self.h, a, b, C.byref(lat), C.byref(rel))
         return bool(ok), lat.value, rel.value
 
-    def path_info_batch(self, src, dst):
+    def path_info_batch(self, src, dst, out=None):
         """topology_getPathInfoBatch: (routable u8, latency, reliability) arrays for
-        address arrays src / dst (in_addr_t values)."""
+        address arrays src / dst (in_addr_t values).  `out` = (ok, lat, rel) arrays
+        of the batch's length to fill instead of fresh ones (a worker reuses its
+        buffers every round; fresh 20M-entry arrays cost their page faults)."""
         import numpy as np
         s = np.ascontiguousarray(src, np.uint32)
         d = np.ascontiguousarray(dst, np.uint32)
         if s.ndim != 1 or s.shape != d.shape:
             raise ValueError("path_info_batch: src and dst must be 1-D arrays of equal length")
         n = int(s.shape[0])
-        lat = np.empty(n, np.float64)
-        rel = np.empty(n, np.float64)
-        ok = np.empty(n, np.uint8)
+        if out is None:
+            lat = np.empty(n, np.float64)
+            rel = np.empty(n, np.float64)
+            ok = np.empty(n, np.uint8)
+        else:
+            ok, lat, rel = out
+            for a, dt in ((ok, np.uint8), (lat, np.float64), (rel, np.float64)):
+                if a.dtype != dt or a.shape != (n,) or not a.flags.c_contiguous or not a.flags.writeable:
+                    raise ValueError("path_info_batch: out = (ok u8, lat f64, rel f64) contiguous arrays of the batch's length")
         r = lib().topology_getPathInfoBatch(self.h, n, s.ctypes.data, d.ctypes.data, lat.ctypes.data,
                                             rel.ctypes.data, ok.ctypes.data)
         if r < 0:

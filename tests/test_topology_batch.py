@@ -58,6 +58,15 @@ def test_batch_equals_single_queries_and_oracle(tmp_path, monkeypatch, mirror):
     np.testing.assert_array_equal(ok.reshape(k, k), (ref["kind"] != 0).astype(np.uint8))
     for i in range(0, k * k, 97):
         assert top.path_info(int(src[i]), int(dst[i])) == (bool(ok[i]), lat[i], rel[i])
+    # caller-owned answer buffers (reused across rounds) get the same answers
+    out = (np.full(k * k, 7, np.uint8), np.full(k * k, 7.0), np.full(k * k, 7.0))
+    ok3, lat3, rel3 = top.path_info_batch(src, dst, out=out)
+    assert ok3 is out[0] and lat3 is out[1] and rel3 is out[2]
+    np.testing.assert_array_equal(lat3, lat)
+    np.testing.assert_array_equal(rel3, rel)
+    np.testing.assert_array_equal(ok3, ok)
+    with pytest.raises(ValueError):
+        top.path_info_batch(src, dst, out=(out[0][:-1], out[1], out[2]))
     # unknown addresses answer -1 / not routable, like topology_getLatency
     bad = np.array([addrs[0], 0x7F000009], np.uint32)
     ok2, lat2, _ = top.path_info_batch(bad, bad[::-1])
