@@ -380,8 +380,11 @@ def bench_shim(args, config: str):
     # the answer buffers a worker reuses every round (allocated and touched untimed)
     out = (np.zeros(q, np.uint8), np.zeros(q, np.float64), np.zeros(q, np.float64))
     t0 = time.perf_counter()
+    call_s = []
     for _ in range(steps):
+        tc = time.perf_counter()
         ok, lat, rel = top.path_info_batch(src, dst, out=out)
+        call_s.append(round(time.perf_counter() - tc, 4))
     el = time.perf_counter() - t0
     print(f"[shim] {steps} batches of {q} queries {el:.1f} s", file=sys.stderr, flush=True)
     assert ok.all(), "every pair of the synthetic topologies is routable"
@@ -407,7 +410,7 @@ def bench_shim(args, config: str):
             "startup_s": {"graphml_write_untimed": round(write_s, 3), "topology_new": round(new_s, 3),
                           "attach_all_hosts": round(attach_s, 3), "seal_table_and_mirror": round(seal_s, 3),
                           "end_to_end": round(new_s + attach_s + seal_s, 3)},
-            "single_call_queries_per_s": round(ns / single_s, 1),
+            "single_call_queries_per_s": round(ns / single_s, 1), "batch_call_s": call_s,
             "single_call_note": f"{ns} topology_getPathInfo calls through ctypes (Python call overhead included)",
             "cpu_baseline": cpu}
     if cpu:

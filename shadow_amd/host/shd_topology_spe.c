@@ -2074,11 +2074,7 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
         }
     }
     pthread_rwlock_unlock(&top->state_lock);
-    if (timing)
-        fprintf(stderr,
-                "[topology] batch of %lld: resolve %.3f s, cached entries %.3f s, misses in order %.3f s, "
-                "table reads (beside the two before, rows mode) done %.3f s later\n",
-                (long long)n, t1 - t0, t2 - t1, t3 - t2, now_s() - t3);
+    const double t4 = timing ? now_s() : 0.0;
     batch_res_free(&r);
     batch_min_callback(top, min_updated);
     for (int k = 0; k < T; ++k)
@@ -2087,6 +2083,11 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
     batch_run(T, jobs, batch_finish);
     int64_t nok = 0;
     for (int k = 0; k < T; ++k) nok += jobs[k].count;
+    if (timing)
+        fprintf(stderr,
+                "[topology] batch of %lld: resolve %.3f s, cached entries %.3f s, misses in order %.3f s, "
+                "table reads (beside the two before, rows mode) done %.3f s later, finish %.3f s, total %.3f s\n",
+                (long long)n, t1 - t0, t2 - t1, t3 - t2, t4 - t3, now_s() - t4, now_s() - t0);
     return nok;
 }
 
