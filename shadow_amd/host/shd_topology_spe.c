@@ -676,6 +676,51 @@ static void big_free(void* p, size_t bytes) {
     if (p) munmap(p, bytes);
 }
 
+/* Page faults of a fresh tens-of-GB mirror cost seconds on a host without free huge
+ * pages; touching its pages on several threads while the GPU builds the table hides
+ * them behind the build (pre_touch_start before spe_table_build, _join after). */
+typedef struct {
+    char* p;
+    size_t a, b;
+} TouchJob;
+
+static void* touch_pages(void* x) {
+    TouchJob* j = x;
+    for (size_t i = j->a; i < j->b; i += 4096) ((volatile char*)j->p)[i] = 0;
+    return NULL;
+}
+
+enum { TOUCH_MAX = 32 };
+typedef struct {
+    pthread_t th[TOUCH_MAX];
+    TouchJob job[TOUCH_MAX];
+    int started[TOUCH_MAX];
+    int n;
+} PreTouch;
+
+static int host_cpus(void);
+
+static void pre_touch_start(PreTouch* pt, char* p0, char* p1, size_t bytes) {
+    memset(pt, 0, sizeof *pt);
+    int n = host_cpus();
+    if (n > TOUCH_MAX) n = TOUCH_MAX;
+    if (n < 2) n = 2;
+    pt->n = n;
+    for (int k = 0; k < n; ++k) {   /* half the threads per array */
+        char* p = k % 2 ? p1 : p0;
+        const int h = k / 2, H = (n + 1 - k % 2) / 2;
+        pt->job[k] = (TouchJob){p, bytes * (size_t)h / (size_t)H & ~(size_t)4095, bytes * (size_t)(h + 1) / (size_t)H};
+        pt->started[k] = pthread_create(&pt->th[k], NULL, touch_pages, &pt->job[k]) == 0;
+    }
+}
+
+static void pre_touch_join(PreTouch* pt) {
+    for (int k = 0; k < pt->n; ++k) {
+        if (pt->started[k]) pthread_join(pt->th[k], NULL);
+        else touch_pages(&pt->job[k]);
+    }
+}
+
 static void snap_free(Snap* s) {
     if (!s) return;
     if (s->table) spe_table_free(s->table);
@@ -1183,24 +1228,34 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
         loaded = spe_table_load(s->table, cpath) == SPE_OK;
         tlog(top, LOG_MESSAGE, "path table cache %s: %s", loaded ? "hit" : "miss", cpath);
     }
+    /* host view: the whole table when it fits the mirror budget (mirror_budget: up to
+     * 48 GiB, A <= 56k; spe_table_download streams it through pinned staging), else
+     * source rows mirrored once they are read repeatedly, within that budget, and
+     * single-record device reads (spe_table_get_latrel) otherwise; batches of queries
+     * read the device table in one launch (topology_getPathInfoBatch).  The whole-table
+     * mirror is allocated first and its pages touched while the GPU builds. */
+    if (budget < 0) budget = 0;
+    s->mirror_budget = budget;
+    const int64_t full = (int64_t)A * A * 16;
+    PreTouch pt;
+    int touching = 0;
+    if (rc == SPE_OK && full <= budget) {
+        s->mlat = big_alloc((size_t)A * A * sizeof(double));
+        s->mrel = big_alloc((size_t)A * A * sizeof(double));
+        if (!s->mlat || !s->mrel) rc = SPE_ENOMEM;
+        else {
+            pre_touch_start(&pt, (char*)s->mlat, (char*)s->mrel, (size_t)A * A * sizeof(double));
+            touching = 1;
+        }
+    }
     if (rc == SPE_OK && !loaded) {
         rc = spe_table_build(s->table, NULL);
         if (rc == SPE_OK && cpath[0] && spe_table_save(s->table, cpath) != SPE_OK)
             tlog(top, LOG_WARNING, "could not save the path table cache: %s", spe_last_error());
     }
-    /* host view: the whole table when it fits the mirror budget (mirror_budget: up to
-     * 48 GiB, A <= 56k; spe_table_download streams it through pinned staging), else
-     * source rows mirrored once they are read repeatedly, within that budget, and
-     * single-record device reads (spe_table_get_latrel) otherwise; batches of queries
-     * read the device table in one launch (topology_getPathInfoBatch) */
-    if (budget < 0) budget = 0;
-    s->mirror_budget = budget;
-    const int64_t full = (int64_t)A * A * 16;
+    if (touching) pre_touch_join(&pt);
     if (rc == SPE_OK && full <= budget) {
-        s->mlat = big_alloc((size_t)A * A * sizeof(double));
-        s->mrel = big_alloc((size_t)A * A * sizeof(double));
-        if (!s->mlat || !s->mrel) rc = SPE_ENOMEM;
-        else rc = spe_table_download(s->table, 0, A, s->mlat, s->mrel, NULL, NULL);
+        rc = spe_table_download(s->table, 0, A, s->mlat, s->mrel, NULL, NULL);
     } else if (rc == SPE_OK) {
         s->blocks = calloc((size_t)A, sizeof(*s->blocks));
         s->touch = calloc((size_t)A, sizeof(*s->touch));
