@@ -248,7 +248,12 @@ def bench_lookup(args, rank=0, world=1, local=0, dist=None):
                        "parallelism": f"{world} replica(s) of the table, each GPU answering its own queries (no communication)"},
             "roofline": {"bound": "hbm", "kernel": "k_lookup", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, "k_lookup", c5name, pmc_key(c5name, world, 0)),
-                         "algorithmic_bytes_per_query": 41},
+                         "algorithmic_bytes_per_query": 41,
+                         # a uniform query's 16-B record is a random 128-B L2 line: 8 + 128 + 17 B move per
+                         # query at best, so 8 TB/s caps it at 8e12 / 153 queries/s (PMC r05: 153 B/query)
+                         "random_line_bound": {"bytes_moved_per_query": 153,
+                                               "queries_per_s_at_peak": round(HBM_PEAK_GBS * 1e9 / 153, 1),
+                                               "frac": round(ach * 153 / 41 / HBM_PEAK_GBS, 4)}},
             "cpu_baseline": cpu, "pmc_key": pmc_key(c5name, world, 0)}
     if cpu:
         line["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)
@@ -756,10 +761,13 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
                 "fallback_blocks_per_step": round(derived_run[1] / steps, 2),
                 "shared_anchor_trees": bool(lay.get("shared_sources", 0)),
                 "lanes_per_group": lay["lanes_per_group"],
-                "bytes_basis": "relaxation graph: 12 m_relax + 28 n_relax + 8 (SURVEY 8d B_s minus the row stage)"}
+                "bytes_basis": ("12 m_relax + 28 n_relax + 8 per relaxed lane (SURVEY 8d B_s minus the row stage), "
+                                "m_relax / n_relax of the uncontracted relaxation graph (SURVEY's per-source "
+                                "definition; the contracted graph the lanes run on keeps fewer state rows)")}
         rw = kp["rows"]
         rows_s = rw["ms"] / 1e3
-        rows_k = ("k_rows_derived (+ k_expand_removed)" if derived_run[0] > 0 else
+        # (SPE_ROWS_LM = 1 in kernels_rows.inc: derived sources go through the lane-major pair)
+        rows_k = ("k_stage_lanes + k_rows_lm (+ k_rows_self)" if derived_run[0] > 0 else
                   "k_rows_shared_lds" if lay.get("shared_sources", 0) else "k_rows_sssp")
         extra["roofline_rows"] = {"kernel": rows_k, "achieved": round(b_rows * done / rows_s / 1e9, 1)
                                   if rows_s > 0 else 0.0, "unit": "GB/s", "launches": rw["launches"],
@@ -878,6 +886,81 @@ SIDE_CONFIGS = (
     ("c3_shim", ["--config", "c3shim", "--steps", "3", "--cpu-seconds", "4", "--queries", "20000000"]),
     ("c4_shim", ["--config", "c4shim", "--steps", "2", "--cpu-seconds", "4", "--queries", "20000000"]),
 )
+
+
+LINE_MAX_BYTES = 6000   # the driver parses the LAST stdout line from a tail of about 8 KB
+
+
+def side_summary(v: dict) -> dict:
+    """One side config's record cut to what the headline line carries (VERDICT r05
+    Next #1): value, unit, its time per step or per table, the dominant kernel's
+    roofline fraction, and the default-vs-exact verdict; the full record stays in
+    the file named by `full_record`."""
+    if "error" in v or "skipped" in v:
+        return {k: (str(x)[:160] if isinstance(x, str) else x) for k, x in v.items() if k in ("error", "skipped", "wall_s")}
+    s = {"value": v.get("value"), "unit": v.get("unit")}
+    for k in ("full_table_time_s", "ms_per_step"):
+        if v.get(k) is not None:
+            s[k] = v[k]
+            break
+    roof = v.get("roofline") or {}
+    if "frac" in roof:
+        s["frac"] = roof["frac"]
+        s["kernel"] = roof.get("kernel", "").split(" ")[0]
+    vx = v.get("vs_default_build")
+    if vx:
+        s["vs_default_build"] = {k: vx.get(k) for k in ("route_mismatch", "delivery_flips", "max_latency_rel_err")}
+    if "single_call_queries_per_s" in v:
+        s["single_call_queries_per_s"] = v["single_call_queries_per_s"]
+        s["seal_s"] = (v.get("startup_s") or {}).get("seal_table_and_mirror")
+    if v.get("cpu_baseline"):
+        s["cpu_1core"] = v["cpu_baseline"].get("value")
+    s["wall_s"] = v.get("wall_s")
+    return s
+
+
+def compact_line(line: dict, full_path) -> dict:
+    """The line rank 0 prints: every headline field, `roofline` and `cpu_baseline`
+    in full, side configs as summaries (side_summary); bounded by LINE_MAX_BYTES so
+    that the driver's tail of stdout always holds the whole line."""
+    out = {k: v for k, v in line.items() if k != "side_configs"}
+    if "side_configs" in line:
+        out["side_configs"] = {k: side_summary(v) for k, v in line["side_configs"].items()}
+    if full_path:
+        out["full_record"] = full_path
+    # shed optional detail, least useful first, until the line fits
+    for k in ("kernel_launches", "rank0_step_s", "precompute_end_to_end_s", "speedup_vs_cpu_1core", "split",
+              "kernel_ms", "roofline_rows"):
+        if len(json.dumps(out)) <= LINE_MAX_BYTES:
+            break
+        out.pop(k, None)
+    if len(json.dumps(out)) > LINE_MAX_BYTES and "side_configs" in out:
+        out["side_configs"] = {k: {"value": v.get("value"), "unit": v.get("unit")} for k, v in out["side_configs"].items()}
+    return out
+
+
+def emit(line: dict, tag: str = "") -> None:
+    """Print the line on stdout as the LAST thing this process writes there.  A
+    line that carries side configs (or would exceed LINE_MAX_BYTES) is written in
+    full to gpurun_out/ and printed compacted; the headline value is echoed on
+    stderr as the side configs' are."""
+    full_path = None
+    if "side_configs" in line or len(json.dumps(line)) > LINE_MAX_BYTES:
+        d = os.path.join(ROOT, "gpurun_out")
+        try:
+            os.makedirs(d, exist_ok=True)
+            full_path = os.path.join("gpurun_out", f"bench_full{tag}_n{line.get('n_gpus', 1)}.json")
+            with open(os.path.join(ROOT, full_path), "w") as f:
+                json.dump(line, f, indent=1)
+        except OSError:
+            full_path = None
+        line = compact_line(line, full_path)
+    roof = line.get("roofline") or {}
+    print(f"[bench] headline: {line.get('value')} {line.get('unit')} ({line.get('ms_per_step')} ms/step, "
+          f"roofline frac {roof.get('frac')} on {roof.get('kernel')}, cpu_baseline "
+          f"{(line.get('cpu_baseline') or {}).get('value')})", file=sys.stderr, flush=True)
+    sys.stderr.flush()
+    print(json.dumps(line), flush=True)
 
 
 def _free_port() -> int:
@@ -1055,7 +1138,7 @@ def run_multi(args, n: int):
             side[f"inproc_{cfg}"]["wall_s"] = round(time.perf_counter() - t0, 1)
             print(f"[bench] in-process {cfg} over {n} devices: {side[f'inproc_{cfg}'].get('value', side[f'inproc_{cfg}'].get('error'))}",
                   file=sys.stderr, flush=True)
-    print(json.dumps(out), flush=True)
+    emit(out)
 
 
 def main():
@@ -1170,7 +1253,7 @@ def main():
                 gc.collect()
                 torch.cuda.empty_cache()
                 line["side_configs"] = side_configs()
-            print(json.dumps(line), flush=True)
+            emit(line, "" if rank == 0 and world == 1 and args.config == "c3" else f"_{args.config}")
     if dist is not None:
         dist.destroy_process_group()
 
