@@ -2016,11 +2016,13 @@ typedef struct {
     double* rel;
     uint8_t* ok;
     int rc;
+    char err[256];   /* spe_last_error() is per thread: copied here on the thread that failed */
 } LookupJob;
 
 static void* batch_lookup(void* p) {   /* the device read of a batch, beside the cache bookkeeping */
     LookupJob* j = p;
     j->rc = spe_lookup_batch_host(j->table, j->pairs, j->n, j->lat, j->rel, j->ok);
+    if (j->rc != SPE_OK) snprintf(j->err, sizeof(j->err), "%s", spe_last_error());
     return NULL;
 }
 
@@ -2056,7 +2058,7 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
     int min_updated = 0;
     double t2 = t1, t3 = t1;
     if (!ref) {
-        LookupJob lj = {sn->table, pairs, n, latency, reliability, routable, SPE_OK};
+        LookupJob lj = {sn->table, pairs, n, latency, reliability, routable, SPE_OK, {0}};
         pthread_t lth;
         int lstarted = 0;
         if (dev) {   /* slot pairs (unknown addresses: -1, answered unroutable), then the read */
@@ -2076,7 +2078,7 @@ int64_t topology_getPathInfoBatch(Topology* top, int64_t n, const spe_in_addr_t*
         t3 = timing ? now_s() : 0.0;
         if (lstarted) pthread_join(lth, NULL);
         if (!dev || lj.rc != SPE_OK) {
-            if (dev) tlog(top, LOG_WARNING, "batched path table read failed (%s): reading per query", spe_last_error());
+            if (dev) tlog(top, LOG_WARNING, "batched path table read failed (%s): reading per query", lj.err);
             for (int64_t i = 0; i < n; ++i) {
                 latency[i] = reliability[i] = -1.0;
                 if (r.st[i] == BQ_BAD) continue;

@@ -1,7 +1,8 @@
 """GPU parity of the derived rows, the batch engine's default for
 contracted sources on shared tables: a removed degree-3 vertex x (or a kept vertex
-of at most 7 contracted entries and one removed neighbour, an independent set in
-the contracted graph) whose legs' vertices are relaxation roots of its batch takes
+of at most SPE_DER_KEPT_MAX = 5 contracted entries and at most one removed
+neighbour -- then at most 3 plain ones -- an independent set in the contracted
+graph, spe_graph_prep.cpp contract_degree3) whose legs' vertices are relaxation roots of its batch takes
 no lane; its row is min over legs fl(w_leg + d_u(t)) with the leg's first hop, its
 edges more hops, reliability a_leg r_u(t).
 
@@ -161,9 +162,11 @@ def test_derived_rows_kept_sources_bit_exact(spe):
     nl = top.esrc != top.edst
     deg = np.bincount(np.concatenate([top.esrc[nl], top.edst[nl]]), minlength=top.n)
     lat_diff = (got["lat"] != ex["lat"]).any(axis=1)
-    # every differing row is a derivable source: degree 3 (contracted), or a kept
-    # vertex of at most 7 contracted entries and one removed neighbour (degree <= 6)
-    assert lat_diff.any() and (deg[A[lat_diff]] <= 7).all()
+    # every differing row is a derivable source: a removed vertex (degree 3), a kept
+    # vertex without removed neighbours and at most SPE_DER_KEPT_MAX = 5 contracted
+    # entries (degree <= 5), or one with a removed neighbour and <= 3 plain ones
+    # (degree <= 4)
+    assert lat_diff.any() and (deg[A[lat_diff]] <= 5).all()
     np.testing.assert_allclose(got["lat"], ex["lat"], rtol=RTOL, atol=0)
 
 
