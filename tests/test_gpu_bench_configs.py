@@ -44,9 +44,10 @@ def compare_rows(got, ref, label, rtol=0.0):
     assert (got["lat"][~ok] == -1).all() and (got["hops"][~ok] == 0).all()
 
 
-def launch_sample_slots(A, groups, extra_per_launch=0, seed=0):
+def launch_sample_slots(A, groups, extra_per_launch=0, seed=0, per_block=0):
     """First and last source slot of every build launch (launch k covers 64-source
-    blocks [k*groups, (k+1)*groups)), plus `extra_per_launch` seeded-random ones."""
+    blocks [k*groups, (k+1)*groups)), plus `extra_per_launch` seeded-random ones,
+    plus `per_block` seeded-random ones in every 64-source block."""
     rng = np.random.default_rng(seed)
     nblk = (A + 63) // 64
     slots = []
@@ -55,6 +56,8 @@ def launch_sample_slots(A, groups, extra_per_launch=0, seed=0):
         slots += [lo, hi - 1]
         if extra_per_launch:
             slots += list(rng.integers(lo, hi, extra_per_launch))
+    for b in range(nblk if per_block else 0):
+        slots += list(rng.integers(b * 64, min(A, b * 64 + 64), per_block))
     return np.unique(np.array(slots, dtype=np.int64))
 
 
@@ -94,16 +97,21 @@ def check_whole_table(t, A, label, hop_rule=True):
 
 
 def test_c3_bench_build_every_launch(spe):
-    """C3 (50k BA) full table, bench settings: 64 rows of every launch vs the
-    oracle, and the whole-table invariants over all 2.5e9 entries."""
+    """C3 (50k BA) full table, bench settings with exact_sources (the build the
+    default-vs-exact full-size comparison, test_gpu_fullsize_parity.py, takes as its
+    reference): 64 rows of every launch and one seeded-random source of every
+    64-source block (782 blocks) vs the oracle on 16 threads, and
+    the whole-table invariants over all 2.5e9 entries."""
     top = graphs.gen_ba(50000, 3, 3)
     att = np.arange(top.n, dtype=np.int32)
     g, t, order = bench_table(spe, top, att)
     lay = t.layout()
     assert lay["engine"] == spe.SPE_ENGINE_BATCH
-    slots = launch_sample_slots(t.A, lay["groups_per_launch"], extra_per_launch=62, seed=3)
+    slots = launch_sample_slots(t.A, lay["groups_per_launch"], extra_per_launch=62, seed=3, per_block=1)
     nlaunch = -(-t.nblocks // lay["groups_per_launch"])
     assert len(slots) >= 32 * nlaunch
+    covered = np.unique(slots // 64)
+    assert covered.size == t.nblocks, "one sampled source in every 64-source block"
     check_sampled_rows(t, top, order, slots, "C3")
     r = check_whole_table(t, t.A, "C3")
     assert r["hop_checked"] > 0.9 * r["pairs"]   # every vertex is attached: most next hops are too
