@@ -245,6 +245,11 @@ typedef struct spe_table_layout {
                                      * vertices (0: the table relaxes the graph itself) */
     int32_t shared_sources;         /* 1: pendant sources take their anchor's relaxation
                                      * (spe_table_opts.exact_sources) */
+    int32_t host_reads;             /* single entries (spe_table_get / _get_latrel): 1 = host
+                                     * loads of the device memory, mapped into the process on a
+                                     * large-BAR host; 0 = a device-to-host copy each; -1 = not
+                                     * decided yet (decided at the first read of a built table;
+                                     * SPE_HOST_READS=0 forces copies) */
 } spe_table_layout;
 
 typedef struct spe_entry {

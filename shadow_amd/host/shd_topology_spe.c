@@ -109,6 +109,7 @@ typedef struct {
                                     * ROW_MIRROR_AFTER-th: a row read a few times is cheaper as
                                     * single records) */
     _Atomic int64_t row_budget;    /* bytes left for lazy rows; beyond it: spe_table_get_latrel */
+    _Atomic int host_reads;        /* spe_table_layout.host_reads of the table (-1: not known yet) */
     int64_t mirror_budget;         /* the budget this snapshot was given (full or lazy) */
     pthread_mutex_t row_mu;
     double min_latency;            /* over every routable entry */
@@ -1163,6 +1164,7 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
     *out = NULL;
     Snap* s = calloc(1, sizeof(Snap));
     pthread_mutex_init(&s->row_mu, NULL);
+    atomic_store(&s->host_reads, -1);
     s->A = A;
     s->attached = malloc(((size_t)A + 1) * sizeof(int32_t));
     s->slot_of_vertex = malloc(((size_t)top->n + 1) * sizeof(int32_t));
@@ -1322,8 +1324,12 @@ int32_t topology_seal(Topology* top) {
 }
 
 /* Latency and reliability of table entry (s, t) of a published snapshot; the
- * caller holds state_lock shared. */
+ * caller holds state_lock shared.  A source row is mirrored on its
+ * ROW_MIRROR_AFTER-th single read, or its ROW_MIRROR_AFTER_HOST-th when the table
+ * answers single entries with host loads (spe_table_layout.host_reads: ~2.6 us per
+ * record, where a row's copy costs ~50 of them at A = 100k). */
 #define ROW_MIRROR_AFTER 4
+#define ROW_MIRROR_AFTER_HOST 64
 
 static void snap_value(Topology* top, Snap* sn, int32_t s, int32_t t, double* lat, double* rel) {
     const int32_t A = sn->A;
@@ -1334,7 +1340,10 @@ static void snap_value(Topology* top, Snap* sn, int32_t s, int32_t t, double* la
     }
     const int64_t bytes = (int64_t)A * 16;
     double* row = atomic_load_explicit(&sn->blocks[s], memory_order_acquire);
-    if (!row && atomic_fetch_add(&sn->touch[s], 1) + 1 >= ROW_MIRROR_AFTER && atomic_load(&sn->row_budget) >= bytes) {
+    const int after = atomic_load_explicit(&sn->host_reads, memory_order_relaxed) == 1 ? ROW_MIRROR_AFTER_HOST
+                                                                                       : ROW_MIRROR_AFTER;
+    if (!row && atomic_load_explicit(&sn->touch[s], memory_order_relaxed) < 255 &&
+        atomic_fetch_add(&sn->touch[s], 1) + 1 >= after && atomic_load(&sn->row_budget) >= bytes) {
         pthread_mutex_lock(&sn->row_mu);
         row = atomic_load_explicit(&sn->blocks[s], memory_order_acquire);
         if (!row && atomic_load(&sn->row_budget) >= bytes) {
@@ -1354,7 +1363,15 @@ static void snap_value(Topology* top, Snap* sn, int32_t s, int32_t t, double* la
         *rel = row[(size_t)A + t];
         return;
     }
-    if (spe_table_get_latrel(sn->table, s, t, lat, rel) == SPE_OK) return;
+    if (spe_table_get_latrel(sn->table, s, t, lat, rel) == SPE_OK) {
+        if (atomic_load_explicit(&sn->host_reads, memory_order_relaxed) < 0) {   /* decided by that read */
+            spe_table_layout l;
+            memset(&l, 0, sizeof l);
+            l.struct_size = sizeof l;
+            if (spe_table_layout_get(sn->table, &l) == SPE_OK) atomic_store(&sn->host_reads, l.host_reads);
+        }
+        return;
+    }
     spe_entry e;
     if (spe_table_get(sn->table, s, t, &e) == SPE_OK) {
         *lat = e.latency;

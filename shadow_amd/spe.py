@@ -87,7 +87,7 @@ class TableLayout(_Sized):
                 ("next_hop", C.c_void_p), ("hops", C.c_void_p), ("groups_per_launch", C.c_int32),
                 ("engine", C.c_int32), ("n_devices", C.c_int32), ("device", C.c_int32),
                 ("lanes_per_group", C.c_int32), ("relax_kernel", C.c_int32), ("contracted_vertices", C.c_int32),
-                ("shared_sources", C.c_int32)]
+                ("shared_sources", C.c_int32), ("host_reads", C.c_int32)]
 
 
 class Entry(C.Structure):
@@ -406,6 +406,12 @@ class PathTable:
         e = Entry()
         _check(lib().spe_table_get(self.h, int(s_slot), int(t_slot), C.byref(e)), "spe_table_get")
         return {"latency": e.latency, "reliability": e.reliability, "next_hop": e.next_hop, "hops": e.hops}
+
+    def get_latrel(self, s_slot: int, t_slot: int):
+        lat, rel = C.c_double(), C.c_double()
+        _check(lib().spe_table_get_latrel(self.h, int(s_slot), int(t_slot), C.byref(lat), C.byref(rel)),
+               "spe_table_get_latrel")
+        return lat.value, rel.value
 
     def download(self, row_begin: int = 0, row_end: Optional[int] = None,
                  fields=("lat", "rel", "next", "hops")) -> dict:
