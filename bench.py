@@ -351,17 +351,14 @@ def bench_shim(args, config: str):
     top_g, att, desc = workload(config)
     ips = [f"10.{(v >> 16) & 255}.{(v >> 8) & 255}.{v & 255}" for v in range(top_g.n)]
     tmp = tempfile.mkdtemp(prefix="spe-shim-")
-    try:
-        path = os.path.join(tmp, "topology.graphml")
-        t0 = time.perf_counter()
-        graphs.write_graphml(top_g, path, ips=ips)
-        write_s = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        top = T.Topology(path)
-        new_s = time.perf_counter() - t0
-        print(f"[shim] graphml {write_s:.1f} s, topology_new {new_s:.1f} s", file=sys.stderr, flush=True)
-    finally:
-        shutil.rmtree(tmp, ignore_errors=True)
+    path = os.path.join(tmp, "topology.graphml")
+    t0 = time.perf_counter()
+    graphs.write_graphml(top_g, path, ips=ips)
+    write_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    top = T.Topology(path)
+    new_s = time.perf_counter() - t0
+    print(f"[shim] graphml {write_s:.1f} s, topology_new {new_s:.1f} s", file=sys.stderr, flush=True)
     A = int(att.shape[0])
     hosts = np.array([T.ip(f"11.{(i >> 16) & 255}.{(i >> 8) & 255}.{i & 255}") for i in range(A)], np.uint32)
     t0 = time.perf_counter()
@@ -411,6 +408,24 @@ def bench_shim(args, config: str):
     single_s = time.perf_counter() - t1
     print(f"[shim] {ns} single calls {single_s:.1f} s", file=sys.stderr, flush=True)
     top.close()
+    # the same single calls from C (examples/shd_topology_single_calls.c: no Python in the
+    # loop), one worker thread and the job's CPU quota of threads, on its own topology_new /
+    # attach / seal of the same file (Shadow's workers call from C, concurrently)
+    c_single = None
+    exe = os.path.join(ROOT, "shadow_amd", "shd_topology_single_calls")
+    if os.path.exists(exe):
+        hints = os.path.join(tmp, "hints.txt")
+        with open(hints, "w") as f:
+            f.write("\n".join(ips[int(v)] for v in att) + "\n")
+        nt, _ = host_cores()
+        try:
+            r = subprocess.run([exe, path, hints, str(ns), str(nt)], capture_output=True, text=True, timeout=240)
+            c_single = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+                {"error": f"exit status {r.returncode}", "tail": (r.stdout + r.stderr)[-300:]}
+        except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+            c_single = {"error": str(e)[:200]}
+        print(f"[shim] C single calls: {c_single}", file=sys.stderr, flush=True)
+    shutil.rmtree(tmp, ignore_errors=True)
     value = q * steps / el
     cpu = None if args.no_cpu_baseline else cpu_lookup_baseline(A, args.cpu_seconds)
     line = {"metric": "per-packet lookups through the drop-in (topology_getPathInfoBatch), queries/s",
@@ -421,7 +436,8 @@ def bench_shim(args, config: str):
             "startup_s": {"graphml_write_untimed": round(write_s, 3), "topology_new": round(new_s, 3),
                           "attach_all_hosts": round(attach_s, 3), "seal_table_and_mirror": round(seal_s, 3),
                           "end_to_end": round(new_s + attach_s + seal_s, 3)},
-            "single_call_queries_per_s": round(ns / single_s, 1), "batch_call_s": call_s,
+            "single_call_queries_per_s": round(ns / single_s, 1),
+            "single_call_queries_per_s_c": c_single, "batch_call_s": call_s,
             "first_batch_s": warm_s[0], "warmup": len(warm_s),
             "single_call_note": f"{ns} topology_getPathInfo calls through ctypes (Python call overhead included)",
             "cpu_baseline": cpu}
@@ -912,6 +928,9 @@ def side_summary(v: dict) -> dict:
         s["vs_default_build"] = {k: vx.get(k) for k in ("route_mismatch", "delivery_flips", "max_latency_rel_err")}
     if "single_call_queries_per_s" in v:
         s["single_call_queries_per_s"] = v["single_call_queries_per_s"]
+        c = v.get("single_call_queries_per_s_c") or {}
+        if "single_calls_per_s_1_thread" in c:
+            s["single_call_c"] = [c["single_calls_per_s_1_thread"], c["single_calls_per_s_all_threads"], c["threads"]]
         s["seal_s"] = (v.get("startup_s") or {}).get("seal_table_and_mirror")
     if v.get("cpu_baseline"):
         s["cpu_1core"] = v["cpu_baseline"].get("value")

@@ -57,12 +57,18 @@ def build_topo(force: bool = False) -> str:
     return LIB_TOPO
 
 
+SINGLE = os.path.join(HERE, "shd_topology_single_calls")
+
+
 def build_demo(force: bool = False) -> str:
-    """examples/shd_topology_demo.c: a Shadow-worker-shaped C user of libshdtopo."""
-    src = os.path.join(ROOT, "examples", "shd_topology_demo.c")
-    if force or _stale(DEMO, [src, LIB_TOPO, os.path.join(ROOT, "include", "shd_topology_spe.h")]):
-        _run(["gcc", "-O2", "-std=c11", "-D_GNU_SOURCE", "-Wall", "-o", DEMO, src, "-I", os.path.join(ROOT, "include"),
-              "-L", HERE, "-lshdtopo", "-lspe", "-Wl,-rpath,$ORIGIN", "-lpthread"])
+    """examples/shd_topology_demo.c: a Shadow-worker-shaped C user of libshdtopo;
+    examples/shd_topology_single_calls.c: per-packet single calls timed in C (bench.py's shim lines)."""
+    hdr = os.path.join(ROOT, "include", "shd_topology_spe.h")
+    for src, out in ((os.path.join(ROOT, "examples", "shd_topology_demo.c"), DEMO),
+                     (os.path.join(ROOT, "examples", "shd_topology_single_calls.c"), SINGLE)):
+        if force or _stale(out, [src, LIB_TOPO, hdr]):
+            _run(["gcc", "-O2", "-std=c11", "-D_GNU_SOURCE", "-Wall", "-o", out, src, "-I", os.path.join(ROOT, "include"),
+                  "-L", HERE, "-lshdtopo", "-lspe", "-Wl,-rpath,$ORIGIN", "-lpthread"])
     return DEMO
 
 
