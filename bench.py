@@ -158,7 +158,7 @@ def pmc_traffic(args, kernel, config=None, key=None):
     this line's traffic."""
     path = args.pmc_json
     if path is None:   # the newest committed summary of this config
-        for rnd in ("r05", "r04", "r03", "r02", "r01"):
+        for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
             cand = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{config or args.config}.json")
             if os.path.exists(cand):
                 path = cand
@@ -769,7 +769,8 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
         roof = {"bound": "hbm", "kernel": kname + (" (SSSP + rows, LDS-resident state)" if lds else
                                                    (" (DIRECT rows)" if direct else " (SSSP stage)")),
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(args, kname, config, key), "launches": rl["launches"],
+                "traffic": pmc_traffic(args, kname, config + ("_exact" if args.exact else ""), key),
+                "launches": rl["launches"],
                 "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
                 "algorithmic_bytes_per_source": b_relax,
                 "relaxed_lanes_per_step": round(relaxed / steps),
@@ -1181,6 +1182,8 @@ def main():
     ap.add_argument("--exact", action="store_true",
                     help="build with spe_table_opts.exact_sources = 1 (the drop-in's table on non-dyadic latencies) "
                          "and report its differences from the default build (spe_table_compare)")
+    ap.add_argument("--no-compare", action="store_true",
+                    help="--exact: skip the entry-by-entry comparison with the default build (PMC passes)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the all-gather (build only)")
     ap.add_argument("--gather", choices=("auto", "all_gather", "p2p"), default="auto",
@@ -1263,7 +1266,7 @@ def main():
                 c4 = bench_table(args, rank, world, local, dist, config="c4")
                 if line is not None:
                     line["side_configs"] = {"c4": c4}
-        if line is not None and args.exact and world == 1 and args.config in ("c3", "c4"):
+        if line is not None and args.exact and world == 1 and args.config in ("c3", "c4") and not args.no_compare:
             gc.collect()
             torch.cuda.empty_cache()
             line["vs_default_build"] = default_vs_exact(args.config)

@@ -2,9 +2,9 @@
 # (MI355X_MICROARCH.md HBM section) -> profiles/${R}_pmc_<config>.json on the box,
 # then rocprofv3 kernel-trace stats of the same command, then the bench line itself
 # (which reads the PMC summary back as roofline.traffic).
-# Configs: c3 c2 c4 c5 (on the C3 table) c5_on_c4 (on the C4 table) c1 c2fw.
+# Configs: c3 c2 c4 c5 (on the C3 table) c5_on_c4 (on the C4 table) c1 c2fw c3_exact c4_exact.
 set -e
-R=${ROUND:-r05}
+R=${ROUND:-r06}
 O=gpurun_out/$R
 mkdir -p $O
 export TMPDIR=/tmp
@@ -14,6 +14,8 @@ args() {
     c5_on_c4) echo "--config c5 --c5-table c4 --steps 4 --warmup 1 --no-cpu-baseline" ;;
     c2fw) echo "--config c2fw --steps 1" ;;
     c1) echo "--config c1 --steps 20 --warmup 2 --no-cpu-baseline --no-side" ;;
+    c3_exact) echo "--config c3 --exact --no-compare --steps 2 --warmup 1 --no-cpu-baseline --no-side" ;;
+    c4_exact) echo "--config c4 --exact --no-compare --steps 2 --warmup 1 --no-cpu-baseline --no-side" ;;
     *) echo "--config $1 --steps 2 --warmup 1 --no-cpu-baseline --no-side" ;;
   esac
 }

@@ -28,8 +28,9 @@ typedef struct {
 
 /* returns the number of rounds (<= max_rounds); per-round stats in out[] */
 int sim_final(int32_t n, const int32_t* ptr, const int32_t* col, const double* w, const int32_t* src,
-              double w_min, int32_t max_rounds, round_out* out, int per_item) {
+              double w_min, int32_t max_rounds, round_out* out, int per_item, int order) {
     double* d = malloc(sizeof(double) * (size_t)n * L);
+    double* dprev = malloc(sizeof(double) * (size_t)n * L);
     uint8_t* cur = calloc((size_t)ptr[n], 1);   /* in-edge flag: changed segments of col[k] */
     uint8_t* nxt = calloc((size_t)ptr[n], 1);
     uint8_t* fin = calloc((size_t)n, 1);        /* segments whose every lane is final */
@@ -61,7 +62,9 @@ int sim_final(int32_t n, const int32_t* ptr, const int32_t* col, const double* w
         memset(o, 0, sizeof(*o));
         int any = 0;
         for (int l = 0; l < L; ++l) Fn[l] = INFINITY;
-        for (int32_t v = 0; v < n; ++v) {
+        if (order == 2) memcpy(dprev, d, sizeof(double) * (size_t)n * L);
+        for (int32_t vi = 0; vi < n; ++vi) {
+            const int32_t v = (order == 1 && (rounds & 1)) ? n - 1 - vi : vi;
             uint8_t segs = 0;
             for (int32_t k = ptr[v]; k < ptr[v + 1]; ++k) segs |= cur[k];
             if (!segs) continue;
@@ -89,7 +92,7 @@ int sim_final(int32_t n, const int32_t* ptr, const int32_t* col, const double* w
                 if (!f) continue;
                 cur[k] = 0;
                 const int32_t u = col[k];
-                const double* du = d + (size_t)u * L;
+                const double* du = (order == 2 ? dprev : d) + (size_t)u * L;
                 o->nbr_lines += __builtin_popcount(f);
                 for (int q = 0; q < NSEG; ++q) {
                     if (!(f >> q & 1)) continue;
@@ -117,6 +120,6 @@ int sim_final(int32_t n, const int32_t* ptr, const int32_t* col, const double* w
         for (int l = 0; l < L; ++l) F[l] = Fn[l];
         if (!any) break;
     }
-    free(d); free(cur); free(nxt); free(fin); free(rev);
+    free(d); free(dprev); free(cur); free(nxt); free(fin); free(rev);
     return rounds;
 }

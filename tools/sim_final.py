@@ -31,6 +31,16 @@ def main():
     n = top.n
     m = top.esrc != top.edst
     a, b, w = top.esrc[m], top.edst[m], top.elat[m]
+    relabel = os.environ.get("RELABEL", "")
+    if relabel:   # vertex processing order: new id = rank under the key
+        deg = np.bincount(np.r_[a, b], minlength=n)
+        rng0 = np.random.default_rng(9)
+        key = {"degree": -deg, "random": rng0.permutation(n), "revid": -np.arange(n)}[relabel]
+        perm = np.empty(n, np.int64)
+        perm[np.argsort(key, kind="stable")] = np.arange(n)
+        a, b = perm[a], perm[b]
+    else:
+        perm = np.arange(n)
     A = sp.coo_matrix((np.r_[w, w], (np.r_[a, b], np.r_[b, a])), shape=(n, n)).tocsr()
     A.sum_duplicates()
     A.sort_indices()
@@ -48,7 +58,7 @@ def main():
         outs = (RoundOut * MAXR)()
         r = lib.sim_final(C.c_int32(n), ptr.ctypes.data_as(C.c_void_p), col.ctypes.data_as(C.c_void_p),
                           ww.ctypes.data_as(C.c_void_p), src.ctypes.data_as(C.c_void_p), C.c_double(float(ww.min())),
-                          C.c_int32(MAXR), outs, C.c_int(int(os.environ.get('PER_ITEM', '0'))))
+                          C.c_int32(MAXR), outs, C.c_int(int(os.environ.get('PER_ITEM', '0'))), C.c_int(int(os.environ.get('ORDER', '0'))))
         arr = np.array([[getattr(outs[i], f) for f in FIELDS] for i in range(r)], dtype=float)
         if tot is None or arr.shape[0] > tot.shape[0]:
             pad = np.zeros((arr.shape[0], len(FIELDS)))
