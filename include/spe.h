@@ -377,7 +377,10 @@ int spe_fw_apsp(spe_graph* g, double* d_dist, int64_t ld, int32_t* d_next, void*
  * last improved the pair), d_next(i,j) = the first hop (relaxation vertex id,
  * -1 unreachable / i == j).  Replaces the all-pairs step of the offline tool
  * (compute-topology-paths.py:89-94) and, in the table, igraph's per-source
- * Dijkstra (shd-topology.c:1741). */
+ * Dijkstra (shd-topology.c:1741).  d_rel may be NULL: the (latency, first hop)
+ * pair only -- what the FW engine's table build runs, since its rows re-fold
+ * latency and reliability in path order along the first hops (half the LDS
+ * panels and registers of the triple). */
 int spe_fw_closure(spe_graph* g, double* d_dist, double* d_rel, int32_t* d_next, int64_t ld, void* stream,
                    double* seconds);
 /* The shortest-path tree the SSSP row of source slot s_slot follows:

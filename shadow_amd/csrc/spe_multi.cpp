@@ -471,7 +471,7 @@ static int fw_closure_multi(MultiDev* m, double* seconds) {
     for (int32_t kb = 0; kb < nb && !r; ++kb) {
         const int own = kb / rbs;
         r = fw_pivot_owner(P[own], kb);
-        if (!r) r = bc.rows(own, (int64_t)kb * 64, (int64_t)kb * 64 + 64, 1 | 2);
+        if (!r) r = bc.rows(own, (int64_t)kb * 64, (int64_t)kb * 64 + 64, P[own].R ? (1 | 2) : 1);   // (R: triple builds)
         for (int d = 0; d < m->n && !r; ++d)
             r = fw_pivot_rows(P[d], kb, std::min(nb, d * rbs), std::min(nb, (d + 1) * rbs));
     }

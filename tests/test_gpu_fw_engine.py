@@ -121,6 +121,27 @@ def test_fw_closure_carries_the_triple(spe, n, extra, seed, directed, monkeypatc
     assert rel_err < 1e-12, rel_err
 
 
+@pytest.mark.parametrize("n,extra,seed,directed", [(300, 900, 2, False), (200, 700, 5, True)])
+def test_fw_pair_closure_equals_the_triple(spe, n, extra, seed, directed, monkeypatch):
+    """spe_fw_closure with d_rel = NULL (the closure the FW engine's table build
+    runs): latency and first hop bit for bit those of the triple closure -- R only
+    rides along, it never decides an update."""
+    import torch
+    monkeypatch.setenv("SPE_NO_PRUNE", "1")
+    top = graphs.gen_random_small(n, extra, seed, directed=directed)
+    g = spe.Graph(top)
+    ld = (n + 63) // 64 * 64
+    D3 = torch.empty(ld * ld, dtype=torch.float64, device="cuda")
+    R3 = torch.empty(ld * ld, dtype=torch.float64, device="cuda")
+    N3 = torch.empty(ld * ld, dtype=torch.int32, device="cuda")
+    D2 = torch.empty_like(D3)
+    N2 = torch.empty_like(N3)
+    g.fw_closure(D3.data_ptr(), R3.data_ptr(), N3.data_ptr(), ld)
+    assert g.fw_closure(D2.data_ptr(), 0, N2.data_ptr(), ld) > 0
+    assert torch.equal(D2.view(torch.int64), D3.view(torch.int64))
+    assert torch.equal(N2, N3)
+
+
 def test_fw_engine_c2_full_table_equals_lds_engine(spe):
     """C2 at full size (RGG n = 10,000, every vertex attached): the FW engine's
     whole table equals the LDS SSSP engine's, entry for entry (both bit-exact
