@@ -813,7 +813,8 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
                                  "the path-order folds bit for bit (what topology_seal builds on non-dyadic "
                                  "latencies)" if args.exact else
                                  "library default: derived / shared-anchor rows (routes exact, latency / "
-                                 "reliability within 1e-12 relative)"),
+                                 "reliability within 8.3e-16 relative of the exact build on C3, 7.5e-16 on C4: "
+                                 "c3_exact / c4_exact vs_default_build; tests assert 1e-12)"),
                        "step": "one whole path table (every source row)" + (
                            f"; emulated share {args.share_index} of {shares} (no gather)" if emulated else ""),
                        "chunk_blocks": max(sizes) if sizes else 0, "rounds": len(sizes), "chunk_schedule": sizes,
