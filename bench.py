@@ -334,6 +334,18 @@ def bench_complete(args):
 
 
 def bench_shim(args, config: str):
+    """bench_shim_in in a scratch directory that is removed whatever happens (the
+    GraphML of C4 is ~0.5 GB)."""
+    import shutil
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="spe-shim-")
+    try:
+        return bench_shim_in(args, config, tmp)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def bench_shim_in(args, config: str, tmp: str):
     """The drop-in end to end (include/shd_topology_spe.h, libshdtopo): the config's
     topology written once as GraphML (every vertex an "ip"), then what Shadow does
     at start-up -- topology_new (libxml2 ingest + the reference's validation +
@@ -344,13 +356,10 @@ def bench_shim(args, config: str):
     topology_getPathInfoBatch (per query the reference's path-cache bookkeeping on
     the host, the table read in one device launch), against the reference's
     per-packet lookup restated on one core."""
-    import shutil
-    import tempfile
     from shadow_amd import graphs
     from shadow_amd import topology as T
     top_g, att, desc = workload(config)
     ips = [f"10.{(v >> 16) & 255}.{(v >> 8) & 255}.{v & 255}" for v in range(top_g.n)]
-    tmp = tempfile.mkdtemp(prefix="spe-shim-")
     path = os.path.join(tmp, "topology.graphml")
     t0 = time.perf_counter()
     graphs.write_graphml(top_g, path, ips=ips)
@@ -425,7 +434,6 @@ def bench_shim(args, config: str):
         except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
             c_single = {"error": str(e)[:200]}
         print(f"[shim] C single calls: {c_single}", file=sys.stderr, flush=True)
-    shutil.rmtree(tmp, ignore_errors=True)
     value = q * steps / el
     cpu = None if args.no_cpu_baseline else cpu_lookup_baseline(A, args.cpu_seconds)
     line = {"metric": "per-packet lookups through the drop-in (topology_getPathInfoBatch), queries/s",
@@ -439,7 +447,10 @@ def bench_shim(args, config: str):
             "single_call_queries_per_s": round(ns / single_s, 1),
             "single_call_queries_per_s_c": c_single, "batch_call_s": call_s,
             "first_batch_s": warm_s[0], "warmup": len(warm_s),
-            "single_call_note": f"{ns} topology_getPathInfo calls through ctypes (Python call overhead included)",
+            "single_call_note": (f"{ns} topology_getPathInfo calls through ctypes (Python call overhead included); "
+                                 "single_call_queries_per_s_c: the same calls from C on a fresh topology_new / attach "
+                                 "/ seal of the same file, one thread and the job's CPU quota of threads (its seal_s "
+                                 "includes the driver clearing the VRAM this process just freed)"),
             "cpu_baseline": cpu}
     if cpu:
         line["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)

@@ -71,3 +71,19 @@ def test_host_reads_on_a_block_range_table(spe):
     for s, u in zip(rng.integers(2 * 64, 5 * 64, 400), rng.integers(0, t.A, 400)):
         assert t.get_latrel(int(s), int(u)) == (ref["lat"][s, u], ref["rel"][s, u])
         assert t.get(int(s), int(u))["next_hop"] == ref["next"][s, u]
+
+
+def test_download_by_dma_equals_staged(spe, monkeypatch):
+    """spe_table_download of many blocks DMAs straight into the caller's arrays
+    (hipHostRegister); SPE_DOWNLOAD_STAGED=1 forces the pinned staging path.  Both
+    give the same table, every field."""
+    top = graphs.gen_random_small(1200, 3600, 13)
+    A = np.arange(top.n, dtype=np.int32)
+    g = spe.Graph(top)
+    t = spe.PathTable(g, A)
+    t.build()
+    direct = t.download()
+    monkeypatch.setenv("SPE_DOWNLOAD_STAGED", "1")
+    staged = t.download()
+    for k in ("lat", "rel", "next", "hops"):
+        assert direct[k].tobytes() == staged[k].tobytes(), k
