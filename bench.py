@@ -931,6 +931,8 @@ def side_summary(v: dict) -> dict:
     the file named by `full_record`."""
     if "error" in v or "skipped" in v:
         return {k: (str(x)[:160] if isinstance(x, str) else x) for k, x in v.items() if k in ("error", "skipped", "wall_s")}
+    if "metric" not in v:   # already a summary (a rank's compacted line passed on by run_multi)
+        return v
     s = {"value": v.get("value"), "unit": v.get("unit")}
     for k in ("full_table_time_s", "ms_per_step"):
         if v.get(k) is not None:
