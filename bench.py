@@ -650,7 +650,13 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
     # the table owns no storage of its own that is ever written: every build goes
     # into the caller's buffers (spe_table_build_blocks_into); lr doubles as its
     # nominal external storage
-    t = spe.PathTable(g, att, blocks=(0, nblk), ext=[lr.data_ptr(), lr.data_ptr(), lr.data_ptr()], groups=gpl,
+    # The table's own batch size stays the library's (spe_table_create's rule: a shared
+    # table holds every root of a build call in one batch), whatever the chunk size of
+    # the gather schedule: a chunk or the local remainder built in batches of `gpl`
+    # groups would re-relax the hubs every batch (round 6: the N = 2 rehearsal's local
+    # span ran 922 row launches instead of one)
+    tgroups = gpl if (lds_engine or args.groups > 0) else 0
+    t = spe.PathTable(g, att, blocks=(0, nblk), ext=[lr.data_ptr(), lr.data_ptr(), lr.data_ptr()], groups=tgroups,
                       engine=args.engine, exact_sources=bool(args.exact))
     if gpl == 0:
         gpl = t.layout()["groups_per_launch"]
