@@ -2,13 +2,16 @@
  * what Shadow's workers pay per topology_getPathInfo (shd-worker.c:235-247 asks
  * isRoutable / getReliability / getLatency for every packet).
  *
- *   shd_topology_single_calls <graph.graphml> <hints.txt> <calls> [threads] [seed]
+ *   shd_topology_single_calls <graph.graphml> <hints.txt> <calls> [threads] [seed] [settle_s]
  *
  * hints.txt: one IP hint per line; host i (address 11.x.y.z = i) attaches by the
  * exact-IP hint of line i (shd-topology.c:2354-2413), as bench.py's shim lines do.
  * After topology_seal, `threads` workers each make calls/threads calls on seeded
  * uniform (src, dst) host pairs.  Prints one JSON line: calls per second for one
- * worker alone, then for all workers at once. */
+ * worker alone, then for all workers at once.  settle_s > 0: both again after that many
+ * more seconds, when the library's background pre-fault of the table's host mapping
+ * (spe_table_layout.host_prefault) has had time to finish: the rates a long simulation
+ * runs at. */
 #include <arpa/inet.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -16,6 +19,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "shd_topology_spe.h"
 
@@ -73,12 +77,13 @@ static double timed(Topology* top, int32_t hosts, int64_t calls, int32_t threads
 
 int main(int argc, char** argv) {
     if (argc < 4) {
-        fprintf(stderr, "usage: %s <graph.graphml> <hints.txt> <calls> [threads] [seed]\n", argv[0]);
+        fprintf(stderr, "usage: %s <graph.graphml> <hints.txt> <calls> [threads] [seed] [settle_s]\n", argv[0]);
         return 2;
     }
     const int64_t calls = atoll(argv[3]);
     const int32_t threads = argc > 4 ? atoi(argv[4]) : 16;
     const unsigned seed = argc > 5 ? (unsigned)atoi(argv[5]) : 5u;
+    const double settle = argc > 6 ? atof(argv[6]) : 0.0;
     FILE* f = fopen(argv[2], "r");
     if (!f || calls < 1 || threads < 1) return 2;
     int32_t cap = 1024, hosts = 0;
@@ -106,12 +111,22 @@ int main(int argc, char** argv) {
     timed(top, hosts, calls / 4 + 1, 1, seed + 1, &r1);   /* warm: code, the path-cache model's first stores */
     const double one = timed(top, hosts, calls, 1, seed, &r1);
     const double all = timed(top, hosts, calls, threads, seed + 99, &rn);
+    double one_s = 0.0, all_s = 0.0;
+    int64_t r1s = calls, rns = calls / threads * threads;
+    if (settle > 0.0) {
+        const double until = now_s() + settle;
+        while (now_s() < until) usleep(10000);
+        one_s = timed(top, hosts, calls, 1, seed + 3, &r1s);
+        all_s = timed(top, hosts, calls, threads, seed + 199, &rns);
+    }
     printf("{\"hosts\": %d, \"load_s\": %.3f, \"attach_s\": %.3f, \"seal_s\": %.3f, \"calls\": %lld, "
            "\"single_calls_per_s_1_thread\": %.1f, \"threads\": %d, \"single_calls_per_s_all_threads\": %.1f, "
+           "\"settle_s\": %.1f, \"settled_calls_per_s_1_thread\": %.1f, \"settled_calls_per_s_all_threads\": %.1f, "
            "\"routable\": %lld}\n",
-           hosts, t1 - t0, t2 - t1, t3 - t2, (long long)calls, one, threads, all, (long long)(r1 + rn));
+           hosts, t1 - t0, t2 - t1, t3 - t2, (long long)calls, one, threads, all, settle, one_s, all_s,
+           (long long)(r1 + rn));
     topology_free(top);
     for (int32_t i = 0; i < hosts; ++i) free(hint[i]);
     free(hint);
-    return (r1 == calls && rn == calls / threads * threads) ? 0 : 1;
+    return (r1 == calls && rn == calls / threads * threads && r1s == calls && rns == calls / threads * threads) ? 0 : 1;
 }

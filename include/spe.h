@@ -251,6 +251,13 @@ typedef struct spe_table_layout {
                                      * large-BAR host; 0 = a device-to-host copy each; -1 = not
                                      * decided yet (decided at the first read of a built table;
                                      * SPE_HOST_READS=0 forces copies) */
+    int32_t host_prefault;          /* host_reads = 1: the host mapping of the latrel field is
+                                     * faulted in by a background thread from the first host read
+                                     * on, so later reads take no page fault: 0 not started,
+                                     * 1 running, 2 done, -1 off (SPE_HOST_PREFAULT=0; =N: N
+                                     * threads, 1 by default) */
+    int32_t reserved0;
+    double host_prefault_s;         /* seconds the pre-fault took (2) or has taken so far (1) */
 } spe_table_layout;
 
 typedef struct spe_entry {

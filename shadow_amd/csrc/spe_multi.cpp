@@ -661,7 +661,9 @@ int multi_layout(const MultiDev* m, spe_table_layout* out) {
     out->relax_kernel = p.relax_kernel;
     out->contracted_vertices = p.contracted_vertices;
     out->shared_sources = p.shared_sources;
-    out->host_reads = 0;   // multi-device gets route to the part that built the row (copies)
+    out->host_reads = 0;
+    out->host_prefault = -1;
+    out->host_prefault_s = 0.0;   // multi-device gets route to the part that built the row (copies)
     out->n_devices = m->n;
     out->device = m->devs[0];
     return SPE_OK;

@@ -87,7 +87,8 @@ class TableLayout(_Sized):
                 ("next_hop", C.c_void_p), ("hops", C.c_void_p), ("groups_per_launch", C.c_int32),
                 ("engine", C.c_int32), ("n_devices", C.c_int32), ("device", C.c_int32),
                 ("lanes_per_group", C.c_int32), ("relax_kernel", C.c_int32), ("contracted_vertices", C.c_int32),
-                ("shared_sources", C.c_int32), ("host_reads", C.c_int32)]
+                ("shared_sources", C.c_int32), ("host_reads", C.c_int32),
+                ("host_prefault", C.c_int32), ("reserved0", C.c_int32), ("host_prefault_s", C.c_double)]
 
 
 class Entry(C.Structure):

@@ -87,3 +87,42 @@ def test_download_by_dma_equals_staged(spe, monkeypatch):
     staged = t.download()
     for k in ("lat", "rel", "next", "hops"):
         assert direct[k].tobytes() == staged[k].tobytes(), k
+
+
+@pytest.mark.parametrize("threads", ["0", "3"])
+def test_host_prefault(spe, threads, monkeypatch):
+    """The first host read starts the background pre-fault of the mapping
+    (spe_table_layout.host_prefault: 1 running, 2 done; SPE_HOST_PREFAULT=0: -1 off);
+    entries read while it runs and after it ends equal the download, and closing the
+    table while it runs stops it."""
+    monkeypatch.setenv("SPE_HOST_PREFAULT", threads)
+    top = graphs.gen_random_small(1400, 4200, 14)
+    A = np.arange(top.n, dtype=np.int32)
+    g = spe.Graph(top)
+    t = spe.PathTable(g, A)
+    t.build()
+    ref = t.download()
+    assert t.layout()["host_prefault"] == 0
+    rng = np.random.default_rng(5)
+    pairs = rng.integers(0, t.A, (600, 2))
+    _check_entries(t, ref, pairs[:300])
+    lay = t.layout()
+    if lay["host_reads"] != 1:
+        assert lay["host_prefault"] == 0
+        pytest.skip("no large-BAR host mapping: copies, nothing to pre-fault")
+    if threads == "0":
+        assert lay["host_prefault"] == -1
+    else:
+        assert lay["host_prefault"] in (1, 2)
+        t0 = time.perf_counter()
+        while t.layout()["host_prefault"] == 1 and time.perf_counter() - t0 < 30:
+            time.sleep(0.01)
+        lay = t.layout()
+        assert lay["host_prefault"] == 2 and lay["host_prefault_s"] > 0
+        print(f"pre-fault of {lay['elems'] * 16 / 1e6:.0f} MB on {threads} threads: {lay['host_prefault_s']:.4f} s")
+    _check_entries(t, ref, pairs[300:])
+    t2 = spe.PathTable(g, A)   # closed while (probably) still running
+    t2.build()
+    t2.get_latrel(0, 1)
+    t2.close()
+    t.close()

@@ -16,7 +16,9 @@
 //       (written by a kernel, then synchronised) against the expected pattern,
 //   (j) bulk device-to-host copies for a host mirror: 8 GB into touched anonymous
 //       memory registered with hipHostRegister (time to register, DMA rate) against
-//       pinned staging + memcpy on 8 threads.
+//       pinned staging + memcpy on 8 threads,
+//   (k) host loads from 1 / 4 / 16 threads at once (do uncached BAR reads overlap?),
+//   (l) the service wave with 1 / 4 / 16 threads, each on its own request slot.
 // build: hipcc -O3 --offload-arch=gfx950 -o build_ab/probe_single_call tools/probe_single_call.hip
 #include <hip/hip_runtime.h>
 
@@ -329,6 +331,73 @@ int main() {
             printf("(i) host 16-B load of a hipMalloc record: %.2f us/read -> %.0f reads/s, %lld of %d values wrong\n",
                    1e6 * el / n, n / el, (long long)bad, n);
         }
+    }
+    // (k) concurrent host loads
+    for (int nt : {1, 4, 16}) {
+        const int per = 50000;
+        std::vector<std::thread> th;
+        const double t0 = now_s();
+        for (int k = 0; k < nt; ++k)
+            th.emplace_back([=] {
+                uint64_t x = 77 + k;
+                double acc = 0.0;
+                for (int i = 0; i < per; ++i) {
+                    x = x * 6364136223846793005ull + 1442695040888963407ull;
+                    const __m128d v = _mm_load_pd(reinterpret_cast<const double*>(lr + (int64_t)((x >> 36) % (uint64_t)nrec)));
+                    double o[2];
+                    _mm_storeu_pd(o, v);
+                    acc += o[0];
+                }
+                if (acc == -1.0) printf("x");
+            });
+        for (auto& x : th) x.join();
+        const double el = now_s() - t0;
+        printf("(k) host loads, %2d threads: %.0f reads/s in all\n", nt, nt * per / el);
+    }
+    // (l) service wave, several callers
+    {
+        Slot* h = nullptr;
+        int* stop = nullptr;
+        CK(hipHostMalloc((void**)&h, sizeof(Slot) * 64, hipHostMallocMapped | hipHostMallocCoherent));
+        CK(hipHostMalloc((void**)&stop, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        Slot* hd = nullptr;
+        int* sd = nullptr;
+        CK(hipHostGetDevicePointer((void**)&hd, h, 0));
+        CK(hipHostGetDevicePointer((void**)&sd, stop, 0));
+        for (int nt : {1, 4, 16}) {
+            memset((void*)h, 0, sizeof(Slot) * 64);
+            *stop = 0;
+            std::atomic_thread_fence(std::memory_order_seq_cst);
+            hipLaunchKernelGGL(k_service, dim3(1), dim3(64), 0, st, hd, 64, lr, sd, 200000000LL);
+            const int per = 20000;
+            std::vector<std::thread> th;
+            std::atomic<int> late{0};
+            const double t0 = now_s();
+            for (int k = 0; k < nt; ++k)
+                th.emplace_back([&, k] {
+                    Slot* sl = &h[k];
+                    uint64_t x = 99 + k;
+                    for (int i = 0; i < per; ++i) {
+                        x = x * 6364136223846793005ull + 1442695040888963407ull;
+                        const unsigned long long seq = (unsigned long long)i + 1;
+                        __atomic_store_n(&sl->s, (int32_t)((x >> 36) % (uint64_t)nrec), __ATOMIC_RELAXED);
+                        __atomic_store_n(&sl->req, seq, __ATOMIC_RELEASE);
+                        const double tl = now_s() + 1.0;
+                        while (__atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) != seq)
+                            if (now_s() > tl) {
+                                late++;
+                                return;
+                            }
+                    }
+                });
+            for (auto& x : th) x.join();
+            const double el = now_s() - t0;
+            __atomic_store_n(stop, 1, __ATOMIC_SEQ_CST);
+            CK(hipStreamSynchronize(st));
+            printf("(l) service wave, %2d callers: %.0f calls/s in all%s\n", nt, nt * per / el, late ? " (some timed out)" : "");
+        }
+        CK(hipHostFree(h));
+        CK(hipHostFree(stop));
     }
     // (j) mirror copies
     {

@@ -48,8 +48,16 @@ def main():
     lib = C.CDLL(os.path.join(HERE, "_sim_final.so"))
     rng = np.random.default_rng(1)
     K = (n + 63) // 64
-    D, _, srcs = dijkstra(A, directed=False, indices=rng.permutation(n)[:K], min_only=True, return_predecessors=True)
+    grouping = os.environ.get("GROUPING", "voronoi")
+    Ag = A.copy()
+    if grouping == "hops":   # Voronoi cells by hop count instead of latency
+        Ag.data[:] = 1.0
+    D, _, srcs = dijkstra(Ag, directed=False, indices=rng.permutation(n)[:K], min_only=True, return_predecessors=True)
     order = np.lexsort((D, srcs))
+    if grouping == "cell128":   # cells of 128 sources (K/2 centres): one cell per group
+        D, _, srcs = dijkstra(A, directed=False, indices=rng.permutation(n)[:K // 2], min_only=True,
+                              return_predecessors=True)
+        order = np.lexsort((D, srcs))
     pick = rng.choice(n // 128, ng, replace=False)
     tot = None
     MAXR = 64
