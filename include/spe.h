@@ -347,6 +347,7 @@ int spe_table_build_blocks_into(spe_table* t, int32_t block_begin, int32_t block
 /* Per-kernel device time, from HIP events recorded around every launch on the
  * build stream while profiling is enabled (costs one event pair per launch). */
 enum { SPE_K_INIT = 0, SPE_K_SEED, SPE_K_HEAVY, SPE_K_RELAX, SPE_K_ROWS, SPE_K_DIRECT, SPE_K_LDS, SPE_K_FW,
+       SPE_K_ROUTES,   /* the route pass after an LDS-ring relaxation (k_routes_init, k_routes) */
        SPE_K_COUNT };
 typedef struct spe_kernel_profile {
     double ms[SPE_K_COUNT];

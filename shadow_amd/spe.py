@@ -96,7 +96,7 @@ class Entry(C.Structure):
                 ("hops", C.c_int32)]
 
 
-KERNELS = ["init", "seed", "heavy", "relax", "rows", "direct", "lds", "fw"]
+KERNELS = ["init", "seed", "heavy", "relax", "rows", "direct", "lds", "fw", "routes"]
 
 
 class CheckReport(C.Structure):
@@ -115,7 +115,7 @@ class CompareReport(_Sized):
 
 
 class KernelProfile(C.Structure):
-    _fields_ = [("ms", C.c_double * 8), ("launches", C.c_int64 * 8)]
+    _fields_ = [("ms", C.c_double * 9), ("launches", C.c_int64 * 9)]
 
 
 class BuildStats(_Sized):

@@ -10,7 +10,7 @@ for rep in $(seq ${REPS:-2}); do
     for C in ${CONFIGS:-c3 c4}; do
       F=$O/b_${C}_${LIB}_${RX}_${RW}_${OC}_$rep.log
       if [ "$LIB" = tree ]; then unset SPE_LIB; else export SPE_LIB=$PWD/build_ab/$LIB/libspe.so; fi
-      SPE_RELAX=$RX SPE_INFL=$RW SPE_OCC=$OC timeout -k 10 240 python -u bench.py --config $C --steps 2 --warmup 1 --no-cpu-baseline --no-side > $F 2>&1 || { tail -20 $F; exit 1; }
+      SPE_RELAX=$RX SPE_INFL=$RW SPE_OCC=$OC timeout -k 10 240 python -u bench.py --config $C --steps 2 --warmup 1 --no-cpu-baseline --no-side $EXTRA > $F 2>&1 || { tail -20 $F; exit 1; }
       python - $F "$C $V rep=$rep" <<'PY'
 import json,sys
 l=json.loads([x for x in open(sys.argv[1]) if x.startswith("{")][-1])
