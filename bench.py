@@ -924,10 +924,14 @@ SIDE_CONFIGS = (
     ("c3_exact", ["--config", "c3", "--exact", "--steps", "3", "--no-cpu-baseline"]),
     ("c4_exact", ["--config", "c4", "--exact", "--steps", "2", "--no-cpu-baseline"]),
     ("c1", ["--config", "c1", "--cpu-seconds", "4", "--cpu-sources", "0"]),
-    ("c2fw", ["--config", "c2fw", "--steps", "1"]),   # the FW engine's whole C2 table (DESIGN 4.2)
-    ("c5_on_c4", ["--config", "c5", "--c5-table", "c4", "--steps", "10", "--warmup", "2", "--cpu-seconds", "6"]),
-    # the drop-in end to end: GraphML -> topology_new -> attach -> seal, then batched lookups
+    # the drop-in end to end: GraphML -> topology_new -> attach -> seal, then batched
+    # lookups.  Each shim line follows a config that frees little device memory: the
+    # driver clears the VRAM a finished child released (≈ 50 GB/s), and a seal started
+    # right after a 160-GB child waits for it (C3 seal 3.6 s after c5_on_c4, 1.2 s after
+    # a small config or alone, MEASUREMENTS.md round 6)
     ("c3_shim", ["--config", "c3shim", "--steps", "3", "--cpu-seconds", "4", "--queries", "20000000"]),
+    ("c5_on_c4", ["--config", "c5", "--c5-table", "c4", "--steps", "10", "--warmup", "2", "--cpu-seconds", "6"]),
+    ("c2fw", ["--config", "c2fw", "--steps", "1"]),   # the FW engine's whole C2 table (DESIGN 4.2)
     ("c4_shim", ["--config", "c4shim", "--steps", "2", "--cpu-seconds", "4", "--queries", "20000000"]),
 )
 

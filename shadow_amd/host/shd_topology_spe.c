@@ -1204,6 +1204,11 @@ static int64_t snap_mirror_bytes(const Snap* s) {
 
 static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t budget, Snap** out) {
     *out = NULL;
+    /* SHADOW_SPE_SEAL_TIMING: one stderr line of the seal's phases */
+    const int timing = getenv("SHADOW_SPE_SEAL_TIMING") != NULL;
+    double tp[8] = {0};
+    int np = 0;
+    if (timing) tp[np++] = now_s();
     Snap* s = calloc(1, sizeof(Snap));
     pthread_mutex_init(&s->row_mu, NULL);
     atomic_store(&s->host_reads, -1);
@@ -1255,11 +1260,13 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
     const char* ex = getenv("SHADOW_SPE_EXACT_SOURCES");
     o.exact_sources = top->shared_rows_exact ? 0 : 1;
     if (ex && *ex) o.exact_sources = strcmp(ex, "0") != 0;
+    if (timing) tp[np++] = now_s();   /* slot order */
     int rc = spe_table_create(top->graph, s->attached, A, &o, &s->table);
     if (rc == SPE_EUNSUPPORTED && o.engine != SPE_ENGINE_AUTO) {
         o.engine = SPE_ENGINE_AUTO;
         rc = spe_table_create(top->graph, s->attached, A, &o, &s->table);
     }
+    if (timing) tp[np++] = now_s();   /* table create: device memory */
     /* SHADOW_SPE_TABLE_CACHE=<dir>: reuse the rows of an earlier run on the same
      * graph / hosts (keyed file), else build and save them */
     const char* cdir = getenv("SHADOW_SPE_TABLE_CACHE");
@@ -1292,12 +1299,15 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
             touching = 1;
         }
     }
+    if (timing) tp[np++] = now_s();   /* mirror allocation */
     if (rc == SPE_OK && !loaded) {
         rc = spe_table_build(s->table, NULL);
         if (rc == SPE_OK && cpath[0] && spe_table_save(s->table, cpath) != SPE_OK)
             tlog(top, LOG_WARNING, "could not save the path table cache: %s", spe_last_error());
     }
+    if (timing) tp[np++] = now_s();   /* build */
     if (touching) pre_touch_join(&pt);
+    if (timing) tp[np++] = now_s();   /* rest of the mirror's page touching */
     if (rc == SPE_OK && full <= budget) {
         rc = spe_table_download(s->table, 0, A, s->mlat, s->mrel, NULL, NULL);
     } else if (rc == SPE_OK) {
@@ -1314,7 +1324,14 @@ static int snap_build(Topology* top, const int32_t* att_in, int32_t A, int64_t b
             if (spe_table_layout_get(s->table, &l) == SPE_OK) atomic_store(&s->host_reads, l.host_reads);
         }
     }
+    if (timing) tp[np++] = now_s();   /* download / first read */
     if (rc == SPE_OK) rc = spe_table_min_latency(s->table, &s->min_latency);
+    if (timing) {
+        tp[np++] = now_s();
+        fprintf(stderr, "[topology] seal of %d hosts: order %.3f s, create %.3f s, mirror alloc %.3f s, build %.3f s, "
+                        "touch wait %.3f s, download %.3f s, min latency %.3f s\n", A, tp[1] - tp[0], tp[2] - tp[1],
+                tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], tp[6] - tp[5], tp[7] - tp[6]);
+    }
     if (rc != SPE_OK) {
         tlog(top, LOG_CRITICAL, "path table build failed: %s", spe_last_error());
         snap_free(s);
