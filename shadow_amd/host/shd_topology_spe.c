@@ -86,6 +86,13 @@ typedef struct {
     int32_t kind;      /* K_DIRECT / K_SELF when seq > 0 */
 } PairRec;
 
+/* one slot of the address map: v >= 0 the vertex, IP_EMPTY / IP_GONE (a detached address) */
+enum { IP_EMPTY = -1, IP_GONE = -2 };
+typedef struct {
+    uint32_t ip;
+    int32_t v;
+} IpSlot;
+
 #define NSHARD 64
 typedef struct {
     pthread_mutex_t mu;
@@ -158,9 +165,7 @@ struct _Topology {
      * and the published snapshot; queries hold it shared for their whole duration,
      * attach / publish exclusive */
     StateSlot* state;
-    uint32_t* ip_keys;
-    int32_t* ip_vals;
-    uint8_t* ip_used;
+    IpSlot* ips;               /* open-addressed address -> vertex map: one 8-B slot per probe */
     size_t ip_cap, ip_size;
     uint8_t* is_attached;      /* [n] */
     int32_t* attached;         /* vertices in first-attach order */
@@ -799,7 +804,7 @@ static void topo_release(Topology* top) {
     for (int a = 0; a < VN_COUNT; ++a) free(top->vnum[a]);
     free(top->esrc); free(top->edst); free(top->elat); free(top->eloss);
     free(top->vip); free(top->vip_index);
-    free(top->ip_keys); free(top->ip_vals); free(top->ip_used);
+    free(top->ips);
     free(top->is_attached); free(top->attached);
     free((void*)top->run_seq);
     free((void*)top->xflag);
@@ -871,9 +876,8 @@ Topology* topology_new_on_device(const char* graphPath, int32_t device) {
     }
     qsort(top->vip_index, (size_t)top->n_vip, sizeof(uint64_t), cmp_u64);
     top->ip_cap = 1024;
-    top->ip_keys = calloc(top->ip_cap, sizeof(uint32_t));
-    top->ip_vals = calloc(top->ip_cap, sizeof(int32_t));
-    top->ip_used = calloc(top->ip_cap, 1);
+    top->ips = malloc(top->ip_cap * sizeof(IpSlot));
+    for (size_t i = 0; i < top->ip_cap; ++i) top->ips[i] = (IpSlot){0, IP_EMPTY};
     top->is_attached = calloc((size_t)top->n + 1, 1);
     top->attached = malloc(((size_t)top->n + 1) * sizeof(int32_t));
     top->run_seq = calloc((size_t)top->n + 1, sizeof(uint64_t));
@@ -943,53 +947,47 @@ static uint64_t mix64(uint64_t x) {
 static uint64_t hash_ip(uint32_t ip) { return mix64(ip); }
 
 static void ip_put(Topology* top, uint32_t ip, int32_t v) {
-    if ((top->ip_size + 1) * 2 > top->ip_cap) {
-        size_t nc = top->ip_cap * 2;
-        uint32_t* nk = calloc(nc, sizeof(uint32_t));
-        int32_t* nv = calloc(nc, sizeof(int32_t));
-        uint8_t* nu = calloc(nc, 1);
+    if ((top->ip_size + 1) * 2 > top->ip_cap) {   /* grow (detached slots are dropped) */
+        const size_t nc = top->ip_cap * 2;
+        IpSlot* n = malloc(nc * sizeof(IpSlot));
+        for (size_t i = 0; i < nc; ++i) n[i] = (IpSlot){0, IP_EMPTY};
+        size_t live = 0;
         for (size_t i = 0; i < top->ip_cap; ++i)
-            if (top->ip_used[i] == 1) {
-                size_t j = hash_ip(top->ip_keys[i]) & (nc - 1);
-                while (nu[j]) j = (j + 1) & (nc - 1);
-                nk[j] = top->ip_keys[i];
-                nv[j] = top->ip_vals[i];
-                nu[j] = 1;
+            if (top->ips[i].v >= 0) {
+                size_t j = hash_ip(top->ips[i].ip) & (nc - 1);
+                while (n[j].v != IP_EMPTY) j = (j + 1) & (nc - 1);
+                n[j] = top->ips[i];
+                ++live;
             }
-        free(top->ip_keys); free(top->ip_vals); free(top->ip_used);
-        top->ip_keys = nk;
-        top->ip_vals = nv;
-        top->ip_used = nu;
+        free(top->ips);
+        top->ips = n;
         top->ip_cap = nc;
+        top->ip_size = live;
     }
     size_t j = hash_ip(ip) & (top->ip_cap - 1);
-    while (top->ip_used[j]) {
-        if (top->ip_used[j] == 1 && top->ip_keys[j] == ip) {
-            top->ip_vals[j] = v;
+    while (top->ips[j].v != IP_EMPTY) {
+        if (top->ips[j].v >= 0 && top->ips[j].ip == ip) {
+            top->ips[j].v = v;
             return;
         }
         j = (j + 1) & (top->ip_cap - 1);
     }
-    top->ip_used[j] = 1;
-    top->ip_keys[j] = ip;
-    top->ip_vals[j] = v;
+    top->ips[j] = (IpSlot){ip, v};
     top->ip_size++;
 }
 
-static int32_t ip_get(Topology* top, uint32_t ip) {
+static int32_t ip_get(const Topology* top, uint32_t ip) {
     size_t j = hash_ip(ip) & (top->ip_cap - 1);
-    while (top->ip_used[j]) {
-        if (top->ip_used[j] == 1 && top->ip_keys[j] == ip) return top->ip_vals[j];
-        j = (j + 1) & (top->ip_cap - 1);
-    }
+    for (IpSlot x; (x = top->ips[j]).v != IP_EMPTY; j = (j + 1) & (top->ip_cap - 1))
+        if (x.v >= 0 && x.ip == ip) return x.v;
     return -1;
 }
 
 static void ip_del(Topology* top, uint32_t ip) {
     size_t j = hash_ip(ip) & (top->ip_cap - 1);
-    while (top->ip_used[j]) {
-        if (top->ip_used[j] == 1 && top->ip_keys[j] == ip) {
-            top->ip_used[j] = 2;   /* tombstone */
+    while (top->ips[j].v != IP_EMPTY) {
+        if (top->ips[j].v >= 0 && top->ips[j].ip == ip) {
+            top->ips[j].v = IP_GONE;   /* tombstone: probes continue past it */
             return;
         }
         j = (j + 1) & (top->ip_cap - 1);
