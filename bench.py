@@ -170,6 +170,13 @@ def pmc_traffic(args, kernel, config=None, key=None):
         if key is not None and doc.get("pmc_key") != key:
             return None
         k = doc["kernels"][kernel]
+        if kernel == "k_lookup":   # random 16-B reads: FETCH_SIZE is 64 B per location (profiles/r06_line_fetch.json)
+            fetch = k["fetch_bytes_raw_per_dispatch"]
+            return {"hbm_bytes_per_launch": round(fetch + k["write_bytes_per_dispatch"]),
+                    "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(k["write_bytes_per_dispatch"]),
+                    "fetch_basis": "FETCH_SIZE raw: the streaming-read x2 does not apply to random 16-B reads "
+                                   "(tools/probe_line_fetch.hip)",
+                    "source": os.path.relpath(path, ROOT), "pmc_key": doc.get("pmc_key")}
         return {"hbm_bytes_per_launch": round(k["hbm_bytes_per_dispatch"]),
                 "fetch_bytes_per_launch": round(k["fetch_bytes_per_dispatch"]),
                 "write_bytes_per_launch": round(k["write_bytes_per_dispatch"]),
@@ -249,11 +256,15 @@ def bench_lookup(args, rank=0, world=1, local=0, dist=None):
             "roofline": {"bound": "hbm", "kernel": "k_lookup", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, "k_lookup", c5name, pmc_key(c5name, world, 0)),
                          "algorithmic_bytes_per_query": 41,
-                         # a uniform query's 16-B record is a random 128-B L2 line: 8 + 128 + 17 B move per
-                         # query at best, so 8 TB/s caps it at 8e12 / 153 queries/s (PMC r05: 153 B/query)
-                         "random_line_bound": {"bytes_moved_per_query": 153,
-                                               "queries_per_s_at_peak": round(HBM_PEAK_GBS * 1e9 / 153, 1),
-                                               "frac": round(ach * 153 / 41 / HBM_PEAK_GBS, 4)}},
+                         # a uniform query reads one 16-B record at a random location: what bounds it is
+                         # the rate of random accesses, measured with the same access alone
+                         # (tools/probe_line_fetch.hip, profiles/r06_line_fetch.json): 37.2 G random 16-B
+                         # reads/s with an 8-B store each (64-B reads 38.6 G/s, whole 128-B lines 33.8 G/s;
+                         # FETCH_SIZE reads 64 B per location for all three, so the streaming x2 does not
+                         # apply to this access)
+                         "random_access_bound": {"measured_random_16B_reads_per_s": RANDOM_16B_READS_PER_S,
+                                                 "source": "profiles/r06_line_fetch.json",
+                                                 "frac": round(value / world / RANDOM_16B_READS_PER_S, 4)}},
             "cpu_baseline": cpu, "pmc_key": pmc_key(c5name, world, 0)}
     if cpu:
         line["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)
@@ -936,6 +947,7 @@ SIDE_CONFIGS = (
 )
 
 
+RANDOM_16B_READS_PER_S = 37.15e9   # tools/probe_line_fetch.hip on one MI355X (profiles/r06_line_fetch.json)
 LINE_MAX_BYTES = 6000   # the driver parses the LAST stdout line from a tail of about 8 KB
 
 
