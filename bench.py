@@ -803,10 +803,11 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
         #  -- the bytes the kernel is priced on are per relaxed lane
         relaxed = lanes_run[0] if (not lds and not direct and lanes_run[0] > 0) else done
         ach = b_relax * relaxed / relax_s / 1e9 if relax_s > 0 else 0.0
+        traffic = pmc_traffic(args, kname, config + ("_exact" if args.exact else ""), key)
         roof = {"bound": "hbm", "kernel": kname + (" (SSSP + rows, LDS-resident state)" if lds else
                                                    (" (DIRECT rows)" if direct else " (SSSP stage)")),
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(args, kname, config + ("_exact" if args.exact else ""), key),
+                "traffic": traffic,
                 "launches": rl["launches"],
                 "launch_avg_us": round(1e3 * rl["ms"] / max(1, rl["launches"]), 2),
                 "algorithmic_bytes_per_source": b_relax,
@@ -818,6 +819,15 @@ def bench_table(args, rank, world, local, dist, config=None, replica_only=False)
                 "bytes_basis": ("12 m_relax + 28 n_relax + 8 per relaxed lane (SURVEY 8d B_s minus the row stage), "
                                 "m_relax / n_relax of the uncontracted relaxation graph (SURVEY's per-source "
                                 "definition; the contracted graph the lanes run on keeps fewer state rows)")}
+        if traffic and rl["launches"] > 0 and relax_s > 0:
+            # the request view: L2-miss reads (raw FETCH_SIZE / 64 B) per second of the kernel
+            # against the rate one MI355X sustains for uniformly random reads
+            # (tools/probe_line_fetch.hip): a row visit is ~74 scattered line requests
+            rq = traffic["fetch_bytes_per_launch"] / 2 / 64 * rl["launches"] / relax_s
+            roof["read_request_rate"] = {"l2_miss_reads_per_s": round(rq / 1e9, 2) * 1e9,
+                                         "random_read_ceiling_per_s": RANDOM_16B_READS_PER_S,
+                                         "frac": round(rq / RANDOM_16B_READS_PER_S, 3),
+                                         "source": "PMC summary (traffic) + profiles/r06_line_fetch.json"}
         rw = kp["rows"]
         rows_s = rw["ms"] / 1e3
         # (SPE_ROWS_LM = 1 in kernels_rows.inc: derived sources go through the lane-major pair)
